@@ -1,0 +1,314 @@
+/*
+ * tachikoma.h — C ABI of the MI355X (gfx950) integer inference-and-trace engine.
+ *
+ * Drop-in boundary for the reference's per-op CPU execution path
+ * (CortexFoundation/tachikoma, a TVM 0.11.dev0 fork).  Every entry point is
+ * plain C: raw pointers, sizes and POD structs, no C++ or torch types.
+ *
+ * Conventions (mirroring the reference's packed-function convention,
+ * include/tvm/runtime/c_backend_api.h:49-51 and graph_executor.cc:486-493):
+ *   - tensors are passed as `const tk_tensor*` (layout-identical to DLPack's
+ *     DLTensor, include/tvm/runtime/c_runtime_api.h:174-208); inputs first,
+ *     outputs after;
+ *   - tensors are BORROWED: the caller owns device memory, nothing is retained
+ *     past the call;
+ *   - kernels are enqueued asynchronously on the given stream (`void*` =
+ *     hipStream_t) and never synchronise; one stream per host thread makes
+ *     concurrent calls safe;
+ *   - return 0 on success or a negative tk_status; `tk_last_error()` returns a
+ *     thread-local message (the analogue of TVMAPISetLastError).
+ *
+ * Integer semantics are the reference's pinned CPU semantics (target llvm, no
+ * -mcpu): qnn conv/dense = Σ(a−zp_a)(w−zp_w) in int32,
+ * requantize = RequantizeLowerInt + q_multiply_shift (UPWARD default).
+ */
+#ifndef TACHIKOMA_H_
+#define TACHIKOMA_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* every declaration below is part of the exported ABI (the library builds with
+ * -fvisibility=hidden) */
+#pragma GCC visibility push(default)
+
+#define TK_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status */
+typedef enum {
+  TK_OK = 0,
+  TK_ERR_INVALID_ARG = -1,
+  TK_ERR_UNSUPPORTED = -2,
+  TK_ERR_SHAPE = -3,
+  TK_ERR_DTYPE = -4,
+  TK_ERR_HIP = -5,
+  TK_ERR_IO = -6,
+  TK_ERR_FORMAT = -7,
+} tk_status;
+
+/* Thread-local message for the last failing call on this thread. */
+const char* tk_last_error(void);
+/* Library/ABI version (TK_ABI_VERSION) and the offload arch it was built for. */
+int tk_abi_version(void);
+const char* tk_build_arch(void);
+
+/* ---------------------------------------------------------------- tensors */
+/* Layout-identical to DLPack DLDevice / DLDataType / DLTensor. */
+typedef struct { int32_t device_type; int32_t device_id; } tk_device;
+typedef struct { uint8_t code; uint8_t bits; uint16_t lanes; } tk_dtype;
+typedef struct {
+  void* data;
+  tk_device device;
+  int32_t ndim;
+  tk_dtype dtype;
+  int64_t* shape;
+  int64_t* strides; /* must be NULL (compact row-major) */
+  uint64_t byte_offset;
+} tk_tensor;
+
+enum { TK_DL_INT = 0, TK_DL_UINT = 1, TK_DL_FLOAT = 2 };
+enum { TK_DEV_CPU = 1, TK_DEV_ROCM = 10 };
+
+/* ---------------------------------------------------------------- fixed point
+ * Host ports of the reference's compile-time constant folding.            */
+
+/* GetFixedPointMultiplierShift (src/relay/qnn/utils.cc:33-57). */
+int tk_fixed_point_multiplier_shift(double multiplier, int32_t* significand, int32_t* shift);
+
+enum { TK_ROUND_UPWARD = 0, TK_ROUND_TONEAREST = 1 };
+
+/* Requantize modes chosen by tk_requantize_prepare
+ * (RequantizeLowerInt, src/relay/qnn/op/requantize.cc:195-273). */
+enum {
+  TK_RQ_IDENTITY = 0,           /* per-tensor, input_scale == output_scale: FPM skipped (:226) */
+  TK_RQ_TENSOR_POW2 = 1,        /* per-tensor UPWARD, m == 1<<30: int32 shift path (intrin_rule.cc:223-237) */
+  TK_RQ_TENSOR_UPWARD = 2,      /* per-tensor UPWARD general (intrin_rule.cc:166-195) */
+  TK_RQ_TENSOR_TONEAREST = 3,   /* FixedPointMultiplyToNearest (utils.cc:59-109) */
+  TK_RQ_AXIS_UPWARD = 4,        /* q_multiply_shift_per_axis (intrin_rule.cc:252-267) */
+  TK_RQ_AXIS_TONEAREST = 5,     /* FixedPointMultiplyPerChannel TONEAREST (utils.cc:137-216) */
+};
+
+/* Fold float32 scales into fixed-point constants exactly as the reference's
+ * canonicalisation does.  `input_scales` has n_scales entries; n_scales == 0
+ * means a rank-0 (per-tensor) scale held in input_scales[0].  On return
+ * multipliers[i]/shifts[i] (capacity max(1, n_scales)) and *mode are set. */
+int tk_requantize_prepare(const float* input_scales, int n_scales, float output_scale, int rounding,
+                          int32_t* multipliers, int32_t* shifts, int* mode);
+
+/* ---------------------------------------------------------------- op attrs */
+
+/* qnn.requantize (src/relay/qnn/op/requantize.cc:195-273). */
+typedef struct {
+  int32_t mode;                 /* TK_RQ_* from tk_requantize_prepare */
+  int32_t axis;                 /* channel axis for per-axis constants / zero points */
+  int32_t multiplier;           /* per-tensor modes */
+  int32_t shift;
+  const int32_t* multipliers;   /* device, per-axis modes (len = shape[axis]) */
+  const int32_t* shifts;        /* device, per-axis modes */
+  int32_t input_zero_point;     /* used when input_zero_points == NULL */
+  const int32_t* input_zero_points; /* device, optional per-axis */
+  int32_t output_zero_point;
+} tk_requantize_attrs;
+
+/* qnn.conv2d, NCHW data / OIHW weight → int32 NCHW. */
+typedef struct {
+  int32_t strides[2];
+  int32_t padding[4];           /* top, left, bottom, right */
+  int32_t dilation[2];
+  int32_t groups;
+  int32_t input_zero_point;
+  int32_t kernel_zero_point;    /* used when kernel_zero_points == NULL */
+  const int32_t* kernel_zero_points; /* device, optional per-output-channel */
+} tk_conv2d_attrs;
+
+/* qnn.dense [M,K] x [N,K]^T → int32 [M,N]. */
+typedef struct {
+  int32_t input_zero_point;
+  int32_t kernel_zero_point;
+  const int32_t* kernel_zero_points; /* device, optional per-unit */
+} tk_dense_attrs;
+
+/* qnn.add with per-tensor parameters (src/relay/qnn/op/add.cc:40-96). The two
+ * requantize-to-int32 plans come from tk_requantize_prepare (mode IDENTITY
+ * with equal zero points = plain upcast, op_common.h:186-200). */
+typedef struct {
+  tk_requantize_attrs lhs;      /* lhs → output params, int32 result */
+  tk_requantize_attrs rhs;
+  int32_t output_zero_point;
+  int32_t lhs_upcast;           /* 1: RequantizeOrUpcast took the Cast branch */
+  int32_t rhs_upcast;
+} tk_qnn_add_attrs;
+
+typedef struct {
+  int32_t pool_size[2];
+  int32_t strides[2];
+  int32_t padding[4];
+  int32_t dilation[2];
+  int32_t count_include_pad;
+} tk_pool2d_attrs;
+
+/* ---------------------------------------------------------------- per-op entry points
+ * Each replaces one canonicalised reference op on the CPU graph executor
+ * (graph_executor.cc:524-572 → LLVM TOPI kernel).                          */
+
+/* Packed-weight workspace for the MFMA implicit-GEMM conv: [Cout][KH][KW][Cin_pad]
+ * int8 (uint8 weights are stored xor 0x80) plus int32 per-channel sums. */
+int64_t tk_conv2d_packed_weight_bytes(const tk_tensor* weight, int groups);
+int tk_conv2d_pack_weight(const tk_tensor* weight, int groups, void* packed, int32_t* weight_sums,
+                          void* stream);
+/* NHWC int8 activation copy with channels padded to 16 (uint8 data stored xor 0x80). */
+int64_t tk_conv2d_shadow_bytes(const tk_tensor* data);
+int tk_nchw_to_nhwc_i8(const tk_tensor* data, void* shadow, void* stream);
+/* qnn.conv2d on a prepared shadow + packed weight (what the executor runs). */
+/* `patch_sums` (int32 per output pixel, N*OH*OW) is scratch used only when the kernel
+ * zero point is non-zero; may be NULL otherwise. */
+int tk_qnn_conv2d_prepared(const tk_tensor* data, const void* shadow, const tk_tensor* weight,
+                           const void* packed, const int32_t* weight_sums, tk_tensor* out,
+                           const tk_conv2d_attrs* attrs, void* patch_sums, void* stream);
+/* One-shot qnn.conv2d (src/relay/qnn/op/convolution.cc:708-811; x86 legalization
+ * python/tvm/relay/qnn/op/legalizations.py:177-232): prepares into `workspace`
+ * (tk_qnn_conv2d_workspace_bytes) then runs. */
+int64_t tk_qnn_conv2d_workspace_bytes(const tk_tensor* data, const tk_tensor* weight,
+                                      const tk_conv2d_attrs* attrs);
+int tk_qnn_conv2d(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
+                  const tk_conv2d_attrs* attrs, void* workspace, void* stream);
+
+/* qnn.dense (src/relay/qnn/op/dense.cc:87-206). */
+int64_t tk_qnn_dense_workspace_bytes(const tk_tensor* data, const tk_tensor* weight);
+int tk_qnn_dense(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
+                 const tk_dense_attrs* attrs, void* workspace, void* stream);
+
+int tk_requantize(const tk_tensor* data, tk_tensor* out, const tk_requantize_attrs* attrs, void* stream);
+int tk_qnn_add(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const tk_qnn_add_attrs* attrs,
+               void* stream);
+/* nn.bias_add / add with a broadcast vector along `axis` (int32 wraps). */
+int tk_bias_add(const tk_tensor* data, const tk_tensor* bias, tk_tensor* out, int axis, void* stream);
+/* clip: max(min(x, a_max), a_min) with bounds already cast to the dtype. */
+int tk_clip(const tk_tensor* data, tk_tensor* out, int64_t a_min, int64_t a_max, void* stream);
+/* integer cast (truncating narrow / sign- or zero-extending widen). */
+int tk_cast(const tk_tensor* data, tk_tensor* out, void* stream);
+int tk_max_pool2d(const tk_tensor* data, tk_tensor* out, const tk_pool2d_attrs* attrs, void* stream);
+int tk_avg_pool2d(const tk_tensor* data, tk_tensor* out, const tk_pool2d_attrs* attrs, void* stream);
+int tk_global_avg_pool2d(const tk_tensor* data, tk_tensor* out, void* stream);
+/* batch_flatten / reshape: byte copy (kept as a node so it is traced). */
+int tk_copy(const tk_tensor* data, tk_tensor* out, void* stream);
+
+/* ---------------------------------------------------------------- executor
+ * Native run loop replacing GraphExecutor::Run (graph_executor.cc:61-66) and
+ * the debug executor's per-node copy-out (graph_executor_debug.cc:249-284).
+ * A module holds a flat list of nodes whose tensors are borrowed from the
+ * caller for the module's lifetime (the caller keeps them alive).          */
+
+enum {
+  TK_NODE_CONV2D = 1,      /* in: data, weight; ext: shadow, packed, weight_sums, patch_sums */
+  TK_NODE_DENSE = 2,       /* in: data, weight; ext: workspace */
+  TK_NODE_REQUANTIZE = 3,
+  TK_NODE_BIAS_ADD = 4,
+  TK_NODE_CLIP = 5,
+  TK_NODE_CAST = 6,
+  TK_NODE_QNN_ADD = 7,
+  TK_NODE_MAX_POOL2D = 8,
+  TK_NODE_AVG_POOL2D = 9,
+  TK_NODE_GLOBAL_AVG_POOL2D = 10,
+  TK_NODE_COPY = 11,       /* batch_flatten / reshape */
+  TK_NODE_SHADOW = 12,     /* NCHW→NHWC int8 shadow for a conv input (not traced) */
+};
+
+typedef struct {
+  int32_t kind;                 /* TK_NODE_* */
+  int32_t n_inputs;
+  const tk_tensor* inputs[3];
+  tk_tensor* output;
+  void* ext[4];                 /* kind-specific device pointers (see enum) */
+  union {
+    tk_conv2d_attrs conv2d;
+    tk_dense_attrs dense;
+    tk_requantize_attrs requantize;
+    tk_qnn_add_attrs qnn_add;
+    tk_pool2d_attrs pool2d;
+    struct { int64_t a_min, a_max; } clip;
+    struct { int32_t axis; } bias_add;
+  } attrs;
+} tk_node;
+
+typedef struct tk_module tk_module;
+
+int tk_module_create(const tk_node* nodes, int n_nodes, tk_module** out);
+int tk_module_destroy(tk_module* mod);
+int tk_module_num_nodes(const tk_module* mod);
+/* Runs every node in order on `stream`.  If `capture_stream` and `host_dst`
+ * are non-NULL, node i's output is copied device→host into host_dst[i]
+ * (NULL entries are skipped) on capture_stream, each copy gated by an event
+ * recorded after node i, so copies overlap the following nodes. */
+int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst);
+/* Runs nodes [begin, end) only (per-op record-and-run, Trace.calibrate analogue). */
+int tk_module_run_range(tk_module* mod, int begin, int end, void* stream);
+/* Runs once with a timing event after every node and returns per-node device time in
+ * milliseconds (GraphExecutorDebug::RunIndividual analogue, graph_executor_debug.cc:70-116). */
+int tk_module_run_profiled(tk_module* mod, void* stream, float* node_ms);
+/* Profiling mode: subsequent tk_module_run calls (traced or not) also record a timing
+ * event after every node on the compute stream; tk_module_node_times reads the last run. */
+int tk_module_set_profiling(tk_module* mod, int enable);
+int tk_module_node_times(tk_module* mod, float* node_ms);
+
+/* ---------------------------------------------------------------- trace format
+ * NDArray-list blob (src/runtime/file_utils.cc:184-236, include/tvm/runtime/ndarray.h:447-494):
+ *   u64 0xF7E58D4F05049CB7, u64 0, u64 n, n×(u64 len, bytes), u64 n,
+ *   n × { u64 0xDD5E40F096B4A13F, u64 0, i32 dev_type=1, i32 dev_id=0, i32 ndim,
+ *         u8 code, u8 bits, u16 lanes, i64 shape[ndim], i64 nbytes, bytes }.
+ * The writer lays out a blob so that array payloads can be DMA'd straight into
+ * their final positions.                                                   */
+
+typedef struct {
+  const char* name;
+  int32_t ndim;
+  const int64_t* shape;
+  tk_dtype dtype;
+} tk_array_meta;
+
+/* Total blob size; data_offsets[i] receives the byte offset of array i's payload. */
+int64_t tk_ndlist_layout(const tk_array_meta* arrays, int n, int64_t* data_offsets);
+/* Writes every header/name byte of the blob into `blob` (payload bytes untouched). */
+int tk_ndlist_write_headers(const tk_array_meta* arrays, int n, void* blob, int64_t blob_size);
+/* Parses a blob: fills up to `cap` entries.  Names are NOT NUL-terminated: `name` points
+ * at the name bytes inside the blob and their length is the u64 stored just before them
+ * (((const uint64_t*)name)[-1], unaligned).  Shapes are written to shapes_storage. */
+int tk_ndlist_parse(const void* blob, int64_t blob_size, int cap, tk_array_meta* arrays,
+                    int64_t* data_offsets, int64_t* shapes_storage, int shapes_cap, int* n_out);
+
+/* Trace container: "TKTRACE\0" | u64 version | u64 json_len | u64 params_off | u64 params_size |
+ * u64 records_off | u64 records_size | json | pad | params blob | pad | records blob. */
+#define TK_TRACE_MAGIC 0x0045434152544B54ULL /* "TKTRACE\0" little-endian */
+#define TK_TRACE_VERSION 1
+#define TK_TRACE_ALIGN 4096
+typedef struct {
+  uint64_t magic, version, json_len, params_off, params_size, records_off, records_size;
+} tk_trace_header;
+
+/* Sizes a trace image and fills the fixed header + json + blob headers into `image`
+ * (if non-NULL).  param/record payload offsets (absolute, within the image) are returned. */
+int64_t tk_trace_layout(const char* json, const tk_array_meta* params, int n_params,
+                        const tk_array_meta* records, int n_records, int64_t* param_offsets,
+                        int64_t* record_offsets);
+int tk_trace_write_headers(const char* json, const tk_array_meta* params, int n_params,
+                           const tk_array_meta* records, int n_records, void* image, int64_t image_size);
+/* Writes `size` bytes of `image` to `path` (O_TRUNC); large sequential writes. */
+int tk_write_file(const char* path, const void* image, int64_t size);
+
+/* ---------------------------------------------------------------- digest
+ * Order-aware 64-bit digest computed on the device: Σ_i mix64(w_i ^ i·0x9E3779B97F4A7C15)
+ * mod 2^64 over little-endian 8-byte words w_i (tail zero-padded), mix64 = the
+ * splitmix64 finaliser.  Used by digest-only trace mode and the RCCL digest
+ * all-gather.  Result written to *out_device. */
+int tk_digest_bytes(const void* data, int64_t nbytes, uint64_t* out_device, void* stream);
+
+#pragma GCC visibility pop
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TACHIKOMA_H_ */

@@ -1,0 +1,77 @@
+"""Build the in-tree HIP library ``tachikoma_amd/libtachikoma.so`` for gfx950.
+
+Plain hipcc, no cmake: each translation unit is compiled to an object in
+``tachikoma_amd/_build/`` (in parallel) and linked into one shared library whose
+exported symbols are exactly the ``extern "C"`` entry points of
+``include/tachikoma.h``.
+"""
+from __future__ import annotations
+
+import concurrent.futures
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libtachikoma.so")
+ARCH = os.environ.get("TK_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["tk_host.cc", "tk_format.cc", "tk_runtime.cc", "tk_elementwise.hip", "tk_gemm.hip"]
+HEADERS = ["tk_common.h"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the tachikoma HIP library cannot be built")
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def _compile(src: str, obj: str, extra) -> None:
+    hipcc = _hipcc()
+    cmd = [hipcc, "-std=c++17", "-O3", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}",
+           "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function", "-c", src, "-o", obj] + extra
+    if src.endswith(".cc"):
+        cmd[1:1] = ["-x", "hip"]
+    subprocess.run(cmd, check=True)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "tachikoma.h")]
+    jobs = []
+    objs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(BUILD, s + ".o")
+        objs.append(obj)
+        if force or not _newer(obj, [src] + hdrs + [__file__]):
+            jobs.append((src, obj))
+    if jobs:
+        workers = min(len(jobs), int(os.environ.get("MAX_JOBS", "8")))
+        with concurrent.futures.ThreadPoolExecutor(max_workers=workers) as ex:
+            futs = [ex.submit(_compile, s, o, []) for s, o in jobs]
+            for f in futs:
+                f.result()
+    if force or jobs or not _newer(LIB, objs):
+        tmp = LIB + ".tmp"
+        subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs, check=True)
+        os.replace(tmp, LIB)
+        if verbose:
+            print(f"[tachikoma] built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,212 @@
+"""``graph_executor.GraphModule`` surface (python/tvm/contrib/graph_executor.py:114-351)
+plus the trace capture the reference only sketches (README.md:6,16) and the debug
+executor's per-node dump (python/tvm/contrib/debugger/debug_executor.py:210-347).
+
+    lib = relay.build(mod, target="mi355x", params=params)
+    m = graph_executor.GraphModule(lib["default"](tachikoma_amd.rocm(0)))
+    m.set_input("data", x); m.run(); y = m.get_output(0).numpy()
+    m.dump_trace("model.tkt")             # every op output of the last run
+    m.run(trace=True)                     # run with overlapped D2H capture
+"""
+from __future__ import annotations
+
+import json
+import time
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from .. import _lib
+from .. import trace_format as tf
+from ..relay.device_module import DeviceModule
+
+
+class NDArrayView:
+    """What get_output returns: ``.numpy()`` like tvm.nd.NDArray."""
+
+    def __init__(self, t):
+        self._t = t
+
+    def numpy(self) -> np.ndarray:
+        return self._t.detach().cpu().numpy()
+
+    @property
+    def shape(self):
+        return tuple(self._t.shape)
+
+    @property
+    def dtype(self):
+        return str(self._t.dtype).replace("torch.", "")
+
+    def torch(self):
+        return self._t
+
+
+class TraceCapture:
+    """Pinned host image of one trace shard; device→host copies land at final offsets."""
+
+    def __init__(self, module: DeviceModule, meta: Dict[str, Any]):
+        import torch
+        self.module = module
+        plan = module.plan
+        params = [(t.name, t.shape, t.dtype) for t in plan.params]
+        records = [(t.name, t.shape, t.dtype) for t in plan.records]
+        self.meta = dict(meta)
+        self.layout = tf.TraceLayout.compute(tf.header_json(self.meta), params, records)
+        self.image = torch.empty(self.layout.total, dtype=torch.uint8, pin_memory=True)
+        self.ptr = self.image.data_ptr()
+        self.layout.write_headers(self.ptr, self.layout.total)
+        # params once, from the device copies
+        for (name, shape, dtype), off in zip(params, self.layout.param_offsets):
+            self._host_view(off, shape, dtype).copy_(module.buffers[name].reshape(shape))
+        self.record_offsets = dict(zip([r[0] for r in records], self.layout.record_offsets))
+        self.host_dst = [None if name is None else self.ptr + self.record_offsets[name] for name in module.node_names]
+        self.capture_stream = torch.cuda.Stream(device=module.device)
+
+    def _host_view(self, off: int, shape, dtype: str):
+        from ..relay.device_module import torch_dtype
+        nbytes = int(np.prod(shape, dtype=np.int64)) * np.dtype(dtype).itemsize
+        return self.image[off:off + nbytes].view(torch_dtype(dtype)).view(tuple(shape))
+
+    def update_meta(self, **kw) -> None:
+        self.meta.update(kw)
+        text = tf.header_json(self.meta)
+        old = self.layout.json_text
+        if len(text.rstrip()) > len(old):
+            raise _lib.TachikomaError("trace header grew beyond its reserved slack")
+        text = text.rstrip().ljust(len(old))
+        self.layout.json_text = text
+        self.image[56:56 + len(text)].copy_(__import__("torch").frombuffer(bytearray(text.encode()),
+                                                                           dtype=__import__("torch").uint8))
+
+    def capture_inputs(self, stream) -> None:
+        """Copy the graph inputs (recorded first) on the capture stream."""
+        import torch
+        self.capture_stream.wait_stream(stream)
+        with torch.cuda.stream(self.capture_stream):
+            for t in self.module.plan.inputs:
+                self._host_view(self.record_offsets[t.name], t.shape, t.dtype).copy_(
+                    self.module.buffers[t.name], non_blocking=True)
+
+    def synchronize(self) -> None:
+        self.capture_stream.synchronize()
+
+    def write(self, path: str) -> None:
+        tf.write_file(path, self.ptr, self.layout.total)
+
+    def bytes(self) -> memoryview:
+        return memoryview(self.image.numpy())
+
+
+class GraphModule:
+    def __init__(self, module: DeviceModule):
+        self.module = module
+        self.plan = module.plan
+        self._capture: Optional[TraceCapture] = None
+        self._meta = {"format": "tachikoma-trace", "version": tf.TRACE_VERSION, "model": "graph",
+                      "target": "mi355x", "sample_offset": 0, "rank": 0, "world": 1,
+                      "semantics": {"reference": "tvm llvm target without -mcpu", "requantize_compute_dtype":
+                                    "int64", "rounding_default": "UPWARD"},
+                      "inputs": [t.name for t in self.plan.inputs],
+                      "params": [t.name for t in self.plan.params],
+                      "outputs": list(self.plan.outputs),
+                      "ops": [o.describe() for o in self.plan.ops]}
+        if self.plan.inputs:
+            self._meta["n_samples"] = int(self.plan.inputs[0].shape[0]) if self.plan.inputs[0].shape else 1
+
+    # -- reference surface -------------------------------------------------
+    def set_input(self, key=None, value=None, **params):
+        if key is not None:
+            self.module.set_input(key, value)
+        for k, v in params.items():
+            self.module.set_input(k, v)
+
+    def run(self, trace: bool = False, **inputs):
+        import torch
+        if inputs:
+            self.set_input(**inputs)
+        stream = torch.cuda.current_stream(self.module.device)
+        if trace:
+            cap = self.trace_capture()
+            cap.capture_inputs(stream)
+            self.module.run(stream, cap.capture_stream, cap.host_dst)
+        else:
+            self.module.run(stream)
+
+    def get_num_outputs(self) -> int:
+        return len(self.plan.outputs)
+
+    def get_num_inputs(self) -> int:
+        return len(self.plan.inputs)
+
+    def get_input(self, key) -> NDArrayView:
+        if isinstance(key, int):
+            key = self.plan.inputs[key].name
+        return NDArrayView(self.module.buffers[key])
+
+    def get_output(self, index: int, out=None) -> NDArrayView:
+        t = self.module.buffers[self.plan.outputs[index]]
+        if out is not None:
+            out[...] = t.cpu().numpy()
+            return out
+        return NDArrayView(t)
+
+    def load_params(self, params_bytes: bytes) -> None:
+        """``GraphModule.load_params``: an NDArray-list blob (file_utils.cc:184-206)."""
+        for name, arr in tf.parse_ndarray_list(params_bytes).items():
+            if name in self.module.buffers:
+                self.module.set_input(name, arr)
+        raise_if_packed = [o.name for o in self.plan.ops if o.op == "qnn.conv2d"]
+        if raise_if_packed:
+            # packed conv weights were prepared at build time; rebuild to use new weights
+            raise _lib.TachikomaError("load_params after build: rebuild the module (conv weights are pre-packed)")
+
+    # -- trace / debug surface ---------------------------------------------
+    def get_node_output(self, name: str) -> NDArrayView:
+        return NDArrayView(self.module.buffers[name])
+
+    def node_names(self) -> List[str]:
+        return [o.name for o in self.plan.ops]
+
+    def trace_capture(self) -> TraceCapture:
+        if self._capture is None:
+            self._capture = TraceCapture(self.module, self._meta)
+        return self._capture
+
+    def set_trace_meta(self, **kw) -> None:
+        self._meta.update(kw)
+        if self._capture is not None:
+            self._capture.update_meta(**kw)
+
+    def dump_trace(self, path: str, sample_offset: Optional[int] = None) -> str:
+        """Write the trace of the last run (re-runs with capture if the last run was not traced)."""
+        import torch
+        if sample_offset is not None:
+            self.set_trace_meta(sample_offset=int(sample_offset))
+        stream = torch.cuda.current_stream(self.module.device)
+        cap = self.trace_capture()
+        cap.capture_inputs(stream)
+        self.module.run(stream, cap.capture_stream, cap.host_dst)
+        cap.synchronize()
+        cap.write(path)
+        return path
+
+    def profile(self) -> Dict[str, float]:
+        """Per-node device time in ms (GraphExecutorDebug::RunIndividual analogue)."""
+        return self.module.run_profiled()
+
+    def chrome_trace(self, path: str) -> None:
+        """Chrome trace JSON in the debug executor's schema (debug_result.py:151-189)."""
+        timings = self.profile()
+        events, t = [], 0.0
+        for name, ms in timings.items():
+            us = ms * 1e3
+            events.append({"name": name, "cat": "Op", "ph": "B", "ts": t * 1e3, "pid": 1, "tid": 1})
+            events.append({"name": name, "cat": "Op", "ph": "E", "ts": (t + us) * 1e3, "pid": 1, "tid": 1})
+            t += us
+        with open(path, "w") as f:
+            json.dump({"traceEvents": events, "displayTimeUnit": "ns"}, f)
+
+
+def create(lib_factory, dev=None) -> GraphModule:
+    return GraphModule(lib_factory["default"](dev))

@@ -1,0 +1,557 @@
+// Wavefront-level integer elementwise / pooling kernels for gfx950.
+//
+// All of these are HBM-bound streaming kernels: 16-byte vector loads per lane
+// where the element type allows, grid-stride loops sized to ~8 workgroups per CU.
+// Semantics follow the canonicalised Relay ops the reference runs on the CPU
+// (SURVEY.md Appendix A); every function cites the reference lowering it mirrors.
+#include <algorithm>
+#include <climits>
+
+#include "tk_common.h"
+
+namespace tk {
+
+constexpr int kBlock = 256;
+
+static inline int grid_for(int64_t work_items) {
+  int64_t g = (work_items + kBlock - 1) / kBlock;
+  if (g < 1) g = 1;
+  if (g > 256 * 8) g = 256 * 8;
+  return (int)g;
+}
+
+template <int D> struct DTT;
+template <> struct DTT<DT_I8> { using T = int8_t; };
+template <> struct DTT<DT_U8> { using T = uint8_t; };
+template <> struct DTT<DT_I16> { using T = int16_t; };
+template <> struct DTT<DT_U16> { using T = uint16_t; };
+template <> struct DTT<DT_I32> { using T = int32_t; };
+template <> struct DTT<DT_U32> { using T = uint32_t; };
+template <> struct DTT<DT_I64> { using T = int64_t; };
+template <> struct DTT<DT_U64> { using T = uint64_t; };
+
+template <typename T> __device__ __forceinline__ int64_t tmin() { return (int64_t)std::numeric_limits<T>::min(); }
+template <typename T> __device__ __forceinline__ int64_t tmax() { return (int64_t)std::numeric_limits<T>::max(); }
+
+// dispatch helper: calls f(DTT<D>{}) for the runtime dtype id (generic lambdas)
+template <typename F> static int dispatch_int(int dt, F&& f) {
+  switch (dt) {
+    case DT_I8: return f(DTT<DT_I8>{});
+    case DT_U8: return f(DTT<DT_U8>{});
+    case DT_I16: return f(DTT<DT_I16>{});
+    case DT_U16: return f(DTT<DT_U16>{});
+    case DT_I32: return f(DTT<DT_I32>{});
+    case DT_U32: return f(DTT<DT_U32>{});
+    case DT_I64: return f(DTT<DT_I64>{});
+    case DT_U64: return f(DTT<DT_U64>{});
+  }
+  set_error("unsupported integer dtype");
+  return TK_ERR_DTYPE;
+}
+
+// Position along a broadcast axis: element i sits in channel (i / inner) % C.
+struct AxisWalker {
+  int32_t inner, C;
+  int64_t q;
+  int32_t r, c;
+  __device__ __forceinline__ void seek(int64_t i) {
+    q = i / inner;
+    r = (int32_t)(i - q * inner);
+    c = (int32_t)(q % C);
+  }
+  __device__ __forceinline__ void next() {
+    if (++r == inner) {
+      r = 0;
+      if (++c == C) c = 0;
+    }
+  }
+};
+
+// ---------------------------------------------------------------- requantize
+// RequantizeLowerInt (src/relay/qnn/op/requantize.cc:195-273):
+//   t = int32(x) - zp_in;  t = FPM(t);  t = zp_out + t;  clip+cast unless out is int32.
+struct RqParams {
+  int32_t mode, multiplier, shift, zp_in, zp_out;
+  const int32_t* ms;
+  const int32_t* ss;
+  const int32_t* zps;
+  int32_t inner, C;
+  int64_t qmin, qmax;
+  int32_t clip_out;
+};
+
+__device__ __forceinline__ int32_t rq_apply(int32_t t, int c, const RqParams& p) {
+  int32_t zp = p.zps ? p.zps[c] : p.zp_in;
+  t = (int32_t)((uint32_t)t - (uint32_t)zp);
+  switch (p.mode) {
+    case TK_RQ_IDENTITY: break;
+    case TK_RQ_TENSOR_POW2: t = qms_pow2(t, p.shift); break;
+    case TK_RQ_TENSOR_UPWARD: t = qms_upward(t, p.multiplier, p.shift); break;
+    case TK_RQ_TENSOR_TONEAREST: t = qms_tonearest(t, p.multiplier, p.shift); break;
+    case TK_RQ_AXIS_UPWARD: t = qms_upward(t, p.ms[c], p.ss[c]); break;
+    case TK_RQ_AXIS_TONEAREST: t = qms_tonearest(t, p.ms[c], p.ss[c]); break;
+  }
+  t = (int32_t)((uint32_t)p.zp_out + (uint32_t)t);
+  return t;
+}
+
+template <typename Tin, typename Tout, int VEC>
+__global__ __launch_bounds__(kBlock) void requantize_kernel(const Tin* __restrict__ x, Tout* __restrict__ y,
+                                                            int64_t n, RqParams p) {
+  int64_t nvec = n / VEC;
+  int64_t stride = (int64_t)gridDim.x * kBlock;
+  AxisWalker w{p.inner, p.C};
+  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nvec; v += stride) {
+    Tin in[VEC];
+    Tout out[VEC];
+    __builtin_memcpy(in, x + v * VEC, sizeof(in));
+    w.seek(v * VEC);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      int32_t t = rq_apply((int32_t)in[j], w.c, p);
+      if (p.clip_out) t = (int32_t)min(max((int64_t)t, p.qmin), p.qmax);
+      out[j] = (Tout)t;
+      w.next();
+    }
+    __builtin_memcpy(y + v * VEC, out, sizeof(out));
+  }
+  // tail
+  int64_t tail0 = nvec * VEC;
+  for (int64_t i = tail0 + blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += stride) {
+    w.seek(i);
+    int32_t t = rq_apply((int32_t)x[i], w.c, p);
+    if (p.clip_out) t = (int32_t)min(max((int64_t)t, p.qmin), p.qmax);
+    y[i] = (Tout)t;
+  }
+}
+
+static int axis_geometry(const tk_tensor* t, int axis, int32_t* inner, int32_t* C) {
+  if (t->ndim == 0) {
+    *inner = 1;
+    *C = 1;
+    return TK_OK;
+  }
+  int ax = axis < 0 ? t->ndim + axis : axis;
+  if (ax < 0 || ax >= t->ndim) return TK_ERR_INVALID_ARG;
+  int64_t in = 1;
+  for (int i = ax + 1; i < t->ndim; ++i) in *= t->shape[i];
+  if (in > INT32_MAX) return TK_ERR_UNSUPPORTED;
+  *inner = (int32_t)in;
+  *C = (int32_t)t->shape[ax];
+  return TK_OK;
+}
+
+template <typename Tin, typename Tout>
+static int launch_requantize(const tk_tensor* x, tk_tensor* y, const RqParams& p, hipStream_t s) {
+  int64_t n = numel(x);
+  constexpr int VEC = 16 / sizeof(Tin) > 0 ? (int)(16 / sizeof(Tin)) : 1;
+  int64_t items = n / VEC + 1;
+  hipLaunchKernelGGL((requantize_kernel<Tin, Tout, VEC>), dim3(grid_for(items)), dim3(kBlock), 0, s,
+                     (const Tin*)ptr(x), (Tout*)ptr(y), n, p);
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
+int requantize_impl(const tk_tensor* x, tk_tensor* y, const tk_requantize_attrs* a, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y), "strided tensors are not supported");
+  TK_CHECK_ARG(numel(x) == numel(y), "shape mismatch");
+  TK_CHECK_ARG(is_integer(x) && is_integer(y), "integer tensors required");
+  RqParams p{};
+  p.mode = a->mode;
+  p.multiplier = a->multiplier;
+  p.shift = a->shift;
+  p.zp_in = a->input_zero_point;
+  p.zp_out = a->output_zero_point;
+  p.ms = a->multipliers;
+  p.ss = a->shifts;
+  p.zps = a->input_zero_points;
+  if (axis_geometry(x, a->axis, &p.inner, &p.C) != TK_OK) {
+    set_error("tk_requantize: bad axis");
+    return TK_ERR_INVALID_ARG;
+  }
+  if ((p.mode == TK_RQ_AXIS_UPWARD || p.mode == TK_RQ_AXIS_TONEAREST) && (!p.ms || !p.ss)) {
+    set_error("tk_requantize: per-axis mode needs device multipliers/shifts");
+    return TK_ERR_INVALID_ARG;
+  }
+  int dti = dt_of(x), dto = dt_of(y);
+  p.clip_out = !(dto == DT_I32);
+  switch (dto) {
+    case DT_I8: p.qmin = -128; p.qmax = 127; break;
+    case DT_U8: p.qmin = 0; p.qmax = 255; break;
+    case DT_I16: p.qmin = -32768; p.qmax = 32767; break;
+    case DT_U16: p.qmin = 0; p.qmax = 65535; break;
+    case DT_I32: p.qmin = INT32_MIN; p.qmax = INT32_MAX; break;
+    default: set_error("tk_requantize: unsupported out dtype"); return TK_ERR_DTYPE;
+  }
+#define RQ_OUT(TI)                                                   \
+  switch (dto) {                                                     \
+    case DT_I8: return launch_requantize<TI, int8_t>(x, y, p, s);    \
+    case DT_U8: return launch_requantize<TI, uint8_t>(x, y, p, s);   \
+    case DT_I16: return launch_requantize<TI, int16_t>(x, y, p, s);  \
+    case DT_U16: return launch_requantize<TI, uint16_t>(x, y, p, s); \
+    case DT_I32: return launch_requantize<TI, int32_t>(x, y, p, s);  \
+  }
+  switch (dti) {
+    case DT_I8: RQ_OUT(int8_t); break;
+    case DT_U8: RQ_OUT(uint8_t); break;
+    case DT_I16: RQ_OUT(int16_t); break;
+    case DT_U16: RQ_OUT(uint16_t); break;
+    case DT_I32: RQ_OUT(int32_t); break;
+  }
+#undef RQ_OUT
+  set_error("tk_requantize: unsupported dtype combination");
+  return TK_ERR_DTYPE;
+}
+
+// ---------------------------------------------------------------- bias_add
+// nn.bias_add / broadcast add of a vector along `axis` (int32 wraps like LLVM add).
+template <typename T, int VEC>
+__global__ __launch_bounds__(kBlock) void bias_add_kernel(const T* __restrict__ x, const T* __restrict__ b,
+                                                          T* __restrict__ y, int64_t n, int32_t inner, int32_t C) {
+  int64_t nvec = n / VEC;
+  int64_t stride = (int64_t)gridDim.x * kBlock;
+  AxisWalker w{inner, C};
+  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nvec; v += stride) {
+    T in[VEC], out[VEC];
+    __builtin_memcpy(in, x + v * VEC, sizeof(in));
+    w.seek(v * VEC);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      using U = typename std::make_unsigned<T>::type;
+      out[j] = (T)((U)in[j] + (U)b[w.c]);
+      w.next();
+    }
+    __builtin_memcpy(y + v * VEC, out, sizeof(out));
+  }
+  for (int64_t i = nvec * VEC + blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += stride) {
+    w.seek(i);
+    using U = typename std::make_unsigned<T>::type;
+    y[i] = (T)((U)x[i] + (U)b[w.c]);
+  }
+}
+
+int bias_add_impl(const tk_tensor* x, const tk_tensor* b, tk_tensor* y, int axis, hipStream_t s) {
+  TK_CHECK_ARG(x && b && y, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y) && compact(b), "strided tensors are not supported");
+  TK_CHECK_ARG(dt_of(x) == dt_of(b) && dt_of(x) == dt_of(y), "dtype mismatch");
+  TK_CHECK_ARG(numel(x) == numel(y), "shape mismatch");
+  int32_t inner, C;
+  if (axis_geometry(x, axis, &inner, &C) != TK_OK || numel(b) != C) {
+    set_error("tk_bias_add: bias length does not match the axis");
+    return TK_ERR_SHAPE;
+  }
+  int64_t n = numel(x);
+  return dispatch_int(dt_of(x), [&](auto tag) -> int {
+    using T = typename decltype(tag)::T;
+    constexpr int VEC = 16 / sizeof(T);
+    hipLaunchKernelGGL((bias_add_kernel<T, VEC>), dim3(grid_for(n / VEC + 1)), dim3(kBlock), 0, s,
+                       (const T*)ptr(x), (const T*)ptr(b), (T*)ptr(y), n, inner, C);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  });
+}
+
+// ---------------------------------------------------------------- clip
+template <typename T, int VEC>
+__global__ __launch_bounds__(kBlock) void clip_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n, T lo,
+                                                      T hi) {
+  int64_t nvec = n / VEC;
+  int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nvec; v += stride) {
+    T in[VEC];
+    __builtin_memcpy(in, x + v * VEC, sizeof(in));
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) in[j] = max(min(in[j], hi), lo);
+    __builtin_memcpy(y + v * VEC, in, sizeof(in));
+  }
+  for (int64_t i = nvec * VEC + blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += stride)
+    y[i] = max(min(x[i], hi), lo);
+}
+
+int clip_impl(const tk_tensor* x, tk_tensor* y, int64_t lo, int64_t hi, hipStream_t s) {
+  TK_CHECK_ARG(x && y, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y) && dt_of(x) == dt_of(y) && numel(x) == numel(y), "bad tensors");
+  int64_t n = numel(x);
+  return dispatch_int(dt_of(x), [&](auto tag) -> int {
+    using T = typename decltype(tag)::T;
+    constexpr int VEC = 16 / sizeof(T);
+    hipLaunchKernelGGL((clip_kernel<T, VEC>), dim3(grid_for(n / VEC + 1)), dim3(kBlock), 0, s, (const T*)ptr(x),
+                       (T*)ptr(y), n, (T)lo, (T)hi);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  });
+}
+
+// ---------------------------------------------------------------- cast
+template <typename Ti, typename To>
+__global__ __launch_bounds__(kBlock) void cast_kernel(const Ti* __restrict__ x, To* __restrict__ y, int64_t n) {
+  int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += stride) y[i] = (To)x[i];
+}
+
+int cast_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s) {
+  TK_CHECK_ARG(x && y && compact(x) && compact(y) && numel(x) == numel(y), "bad tensors");
+  TK_CHECK_ARG(is_integer(x) && is_integer(y), "integer cast only");
+  int64_t n = numel(x);
+  return dispatch_int(dt_of(x), [&](auto ti) -> int {
+    return dispatch_int(dt_of(y), [&](auto to) -> int {
+      using Ti = typename decltype(ti)::T;
+      using To = typename decltype(to)::T;
+      hipLaunchKernelGGL((cast_kernel<Ti, To>), dim3(grid_for(n)), dim3(kBlock), 0, s, (const Ti*)ptr(x),
+                         (To*)ptr(y), n);
+      TK_LAUNCH_CHECK();
+      return TK_OK;
+    });
+  });
+}
+
+// ---------------------------------------------------------------- qnn.add
+// QnnAddCanonicalize (src/relay/qnn/op/add.cc:40-96): a' = RQ(a) or int32(a), b' likewise,
+// o = a' + b' - zp_c (int32), clip to the input dtype, cast.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void qnn_add_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                         T* __restrict__ y, int64_t n, RqParams pa, RqParams pb,
+                                                         int32_t zp_c, int32_t up_a, int32_t up_b) {
+  int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += stride) {
+    int32_t x0 = (int32_t)a[i], x1 = (int32_t)b[i];
+    int32_t ra = up_a ? x0 : rq_apply(x0, 0, pa);
+    int32_t rb = up_b ? x1 : rq_apply(x1, 0, pb);
+    int32_t o = (int32_t)((uint32_t)ra + (uint32_t)rb);
+    o = (int32_t)((uint32_t)o - (uint32_t)zp_c);
+    int64_t c = min(max((int64_t)o, tmin<T>()), tmax<T>());
+    y[i] = (T)c;
+  }
+}
+
+static RqParams rq_from_attrs(const tk_requantize_attrs& a) {
+  RqParams p{};
+  p.mode = a.mode;
+  p.multiplier = a.multiplier;
+  p.shift = a.shift;
+  p.zp_in = a.input_zero_point;
+  p.zp_out = a.output_zero_point;
+  p.inner = 1;
+  p.C = 1;
+  return p;
+}
+
+int qnn_add_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* y, const tk_qnn_add_attrs* at, hipStream_t s) {
+  TK_CHECK_ARG(a && b && y && at, "null argument");
+  TK_CHECK_ARG(numel(a) == numel(b) && numel(a) == numel(y), "qnn.add: only same-shape operands are supported");
+  TK_CHECK_ARG(dt_of(a) == dt_of(b) && dt_of(a) == dt_of(y), "dtype mismatch");
+  TK_CHECK_ARG(at->lhs.mode <= TK_RQ_TENSOR_TONEAREST && at->rhs.mode <= TK_RQ_TENSOR_TONEAREST,
+               "qnn.add: per-tensor parameters only");
+  int64_t n = numel(a);
+  RqParams pa = rq_from_attrs(at->lhs), pb = rq_from_attrs(at->rhs);
+  return dispatch_int(dt_of(a), [&](auto tag) -> int {
+    using T = typename decltype(tag)::T;
+    hipLaunchKernelGGL((qnn_add_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, s, (const T*)ptr(a), (const T*)ptr(b),
+                       (T*)ptr(y), n, pa, pb, at->output_zero_point, at->lhs_upcast, at->rhs_upcast);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  });
+}
+
+// ---------------------------------------------------------------- pooling (NCHW)
+struct PoolGeom {
+  int32_t N, C, H, W, OH, OW, kh, kw, sh, sw, pt, pl, pb, pr, dh, dw, include_pad;
+};
+
+// nn.max_pool2d: padded taps are the dtype minimum (include/tvm/topi/nn/pooling.h:123).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void max_pool_kernel(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
+  int64_t n = (int64_t)g.N * g.C * g.OH * g.OW;
+  int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += stride) {
+    int ow = (int)(i % g.OW);
+    int64_t t = i / g.OW;
+    int oh = (int)(t % g.OH);
+    int64_t nc = t / g.OH;
+    const T* plane = x + nc * (int64_t)g.H * g.W;
+    T m = (T)tmin<T>();
+    for (int r = 0; r < g.kh; ++r) {
+      int ih = oh * g.sh - g.pt + r * g.dh;
+      if (ih < 0 || ih >= g.H) continue;
+      for (int c = 0; c < g.kw; ++c) {
+        int iw = ow * g.sw - g.pl + c * g.dw;
+        if (iw < 0 || iw >= g.W) continue;
+        T v = plane[ih * g.W + iw];
+        m = v > m ? v : m;
+      }
+    }
+    y[i] = m;
+  }
+}
+
+__device__ __forceinline__ int64_t truncdiv64(int64_t a, int64_t b) { return a / b; }  // C++ '/' truncates
+
+// nn.avg_pool2d on integers: window sum in the input dtype (wraps), truncdiv by the count
+// (include/tvm/topi/nn/pooling.h:560-650).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void avg_pool_kernel(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
+  int64_t n = (int64_t)g.N * g.C * g.OH * g.OW;
+  int64_t stride = (int64_t)gridDim.x * kBlock;
+  using U = typename std::make_unsigned<T>::type;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += stride) {
+    int ow = (int)(i % g.OW);
+    int64_t t = i / g.OW;
+    int oh = (int)(t % g.OH);
+    int64_t nc = t / g.OH;
+    const T* plane = x + nc * (int64_t)g.H * g.W;
+    U sum = 0;
+    for (int r = 0; r < g.kh; ++r) {
+      int ih = oh * g.sh - g.pt + r * g.dh;
+      if (ih < 0 || ih >= g.H) continue;
+      for (int c = 0; c < g.kw; ++c) {
+        int iw = ow * g.sw - g.pl + c * g.dw;
+        if (iw < 0 || iw >= g.W) continue;
+        sum = (U)(sum + (U)plane[ih * g.W + iw]);
+      }
+    }
+    int64_t cnt = 1;
+    int dims[2][6] = {{oh, g.sh, g.kh, g.dh, g.H, g.pt}, {ow, g.sw, g.kw, g.dw, g.W, g.pl}};
+    int tails[2] = {g.pb, g.pr};
+    for (int d = 0; d < 2; ++d) {
+      int o = dims[d][0], st = dims[d][1], k = dims[d][2], dl = dims[d][3], dim = dims[d][4], ph = dims[d][5];
+      int start = o * st - ph;
+      int end = start + (k - 1) * dl;
+      if (g.include_pad) {
+        end = min(end, dim + tails[d] - 1);
+        cnt *= (end - start) / dl + 1;
+      } else {
+        int jumps = (dl - 1 - start) / dl;
+        jumps = max(jumps, 0);
+        end = min(end, dim - 1);
+        cnt *= (end - (start + dl * jumps)) / dl + 1;
+      }
+    }
+    if (!g.include_pad) cnt = max(cnt, (int64_t)1);
+    int64_t sv = (int64_t)(T)sum;
+    y[i] = (T)truncdiv64(sv, (int64_t)(T)cnt);
+  }
+}
+
+// global_avg_pool2d: one wave per (n, c) plane (adaptive pool 1x1, pooling.h:366-389).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void global_avg_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                            int64_t planes, int32_t hw) {
+  using U = typename std::make_unsigned<T>::type;
+  int lane = threadIdx.x & 63;
+  int64_t wave = (blockIdx.x * (int64_t)kBlock + threadIdx.x) >> 6;
+  int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t p = wave; p < planes; p += nwaves) {
+    const T* plane = x + p * hw;
+    U s = 0;
+    for (int i = lane; i < hw; i += 64) s = (U)(s + (U)plane[i]);
+    for (int off = 32; off > 0; off >>= 1) s = (U)(s + (U)__shfl_xor(s, off));
+    if (lane == 0) {
+      int64_t sv = (int64_t)(T)s;
+      y[p] = (T)truncdiv64(sv, (int64_t)(T)hw);
+    }
+  }
+}
+
+static int pool_geom(const tk_tensor* x, const tk_tensor* y, const tk_pool2d_attrs* a, PoolGeom* g) {
+  if (x->ndim != 4 || y->ndim != 4) return TK_ERR_SHAPE;
+  g->N = (int32_t)x->shape[0];
+  g->C = (int32_t)x->shape[1];
+  g->H = (int32_t)x->shape[2];
+  g->W = (int32_t)x->shape[3];
+  g->kh = a->pool_size[0]; g->kw = a->pool_size[1];
+  g->sh = a->strides[0]; g->sw = a->strides[1];
+  g->pt = a->padding[0]; g->pl = a->padding[1]; g->pb = a->padding[2]; g->pr = a->padding[3];
+  g->dh = a->dilation[0] ? a->dilation[0] : 1; g->dw = a->dilation[1] ? a->dilation[1] : 1;
+  g->include_pad = a->count_include_pad;
+  g->OH = (g->H + g->pt + g->pb - g->dh * (g->kh - 1) - 1) / g->sh + 1;
+  g->OW = (g->W + g->pl + g->pr - g->dw * (g->kw - 1) - 1) / g->sw + 1;
+  if (y->shape[0] != g->N || y->shape[1] != g->C || y->shape[2] != g->OH || y->shape[3] != g->OW) return TK_ERR_SHAPE;
+  return TK_OK;
+}
+
+int max_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a && dt_of(x) == dt_of(y), "bad arguments");
+  PoolGeom g;
+  if (pool_geom(x, y, a, &g)) { set_error("tk_max_pool2d: shape mismatch"); return TK_ERR_SHAPE; }
+  int64_t n = (int64_t)g.N * g.C * g.OH * g.OW;
+  return dispatch_int(dt_of(x), [&](auto tag) -> int {
+    using T = typename decltype(tag)::T;
+    hipLaunchKernelGGL((max_pool_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, s, (const T*)ptr(x), (T*)ptr(y), g);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  });
+}
+
+int avg_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a && dt_of(x) == dt_of(y), "bad arguments");
+  PoolGeom g;
+  if (pool_geom(x, y, a, &g)) { set_error("tk_avg_pool2d: shape mismatch"); return TK_ERR_SHAPE; }
+  int64_t n = (int64_t)g.N * g.C * g.OH * g.OW;
+  return dispatch_int(dt_of(x), [&](auto tag) -> int {
+    using T = typename decltype(tag)::T;
+    hipLaunchKernelGGL((avg_pool_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, s, (const T*)ptr(x), (T*)ptr(y), g);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  });
+}
+
+int global_avg_pool_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s) {
+  TK_CHECK_ARG(x && y && x->ndim == 4 && y->ndim == 4 && dt_of(x) == dt_of(y), "bad arguments");
+  TK_CHECK_ARG(y->shape[0] == x->shape[0] && y->shape[1] == x->shape[1] && y->shape[2] == 1 && y->shape[3] == 1,
+               "output must be [N,C,1,1]");
+  int64_t planes = x->shape[0] * x->shape[1];
+  int32_t hw = (int32_t)(x->shape[2] * x->shape[3]);
+  return dispatch_int(dt_of(x), [&](auto tag) -> int {
+    using T = typename decltype(tag)::T;
+    hipLaunchKernelGGL((global_avg_kernel<T>), dim3(grid_for(planes * 64)), dim3(kBlock), 0, s, (const T*)ptr(x),
+                       (T*)ptr(y), planes, hw);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  });
+}
+
+int copy_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s) {
+  TK_CHECK_ARG(x && y && nbytes(x) == nbytes(y), "size mismatch");
+  TK_HIP(hipMemcpyAsync(ptr(y), ptr(x), nbytes(x), hipMemcpyDeviceToDevice, s));
+  return TK_OK;
+}
+
+// ---------------------------------------------------------------- digest
+// Order-aware, parallel 64-bit digest: Σ_i mix(word_i ^ (i · φ)) mod 2^64 over
+// little-endian 8-byte words (tail zero-padded), finalised with the byte length.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void digest_kernel(const uint8_t* __restrict__ p, int64_t nbytes,
+                                                         unsigned long long* out) {
+  int64_t nw = (nbytes + 7) / 8;
+  int64_t stride = (int64_t)gridDim.x * kBlock;
+  uint64_t acc = 0;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < nw; i += stride) {
+    uint64_t w = 0;
+    if ((i + 1) * 8 <= nbytes) {
+      __builtin_memcpy(&w, p + i * 8, 8);
+    } else {
+      for (int b = 0; i * 8 + b < nbytes; ++b) w |= (uint64_t)p[i * 8 + b] << (8 * b);
+    }
+    acc += mix64(w ^ ((uint64_t)i * 0x9E3779B97F4A7C15ULL));
+  }
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
+int digest_impl(const void* data, int64_t nbytes, uint64_t* out, hipStream_t s) {
+  TK_CHECK_ARG(out && (data || nbytes == 0), "null argument");
+  TK_HIP(hipMemsetAsync(out, 0, 8, s));
+  if (nbytes == 0) return TK_OK;
+  hipLaunchKernelGGL(digest_kernel, dim3(grid_for((nbytes + 7) / 8)), dim3(kBlock), 0, s, (const uint8_t*)data, nbytes,
+                     (unsigned long long*)out);
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
+}  // namespace tk

@@ -1,0 +1,322 @@
+// extern "C" entry points + the native node executor.
+//
+// tk_module is the MI355X analogue of the reference's GraphExecutor
+// (src/runtime/graph_executor/graph_executor.cc:61-66 Run, :466-572 op execs)
+// fused with the debug executor's per-node copy-out
+// (src/runtime/graph_executor/debug/graph_executor_debug.cc:249-284): it walks a
+// flat node list on one HIP stream and, when asked, copies every node output to
+// host memory on a second stream, each copy gated by an event recorded right
+// after the node, so the PCIe transfer of node i overlaps the kernels of nodes > i.
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "tk_common.h"
+
+namespace tk {
+int requantize_impl(const tk_tensor* x, tk_tensor* y, const tk_requantize_attrs* a, hipStream_t s);
+int bias_add_impl(const tk_tensor* x, const tk_tensor* b, tk_tensor* y, int axis, hipStream_t s);
+int clip_impl(const tk_tensor* x, tk_tensor* y, int64_t lo, int64_t hi, hipStream_t s);
+int cast_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
+int qnn_add_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* y, const tk_qnn_add_attrs* at, hipStream_t s);
+int max_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s);
+int avg_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s);
+int global_avg_pool_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
+int copy_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
+int digest_impl(const void* data, int64_t nbytes, uint64_t* out, hipStream_t s);
+int64_t conv_packed_weight_bytes(const tk_tensor* weight, int groups);
+int conv_pack_weight(const tk_tensor* weight, int groups, void* packed, int32_t* sums, hipStream_t s);
+int64_t conv_shadow_bytes(const tk_tensor* data);
+int nchw_to_nhwc_impl(const tk_tensor* data, void* shadow, hipStream_t s);
+int conv2d_prepared_impl(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
+                         const int32_t* sums, tk_tensor* out, const tk_conv2d_attrs* a, void* patch, hipStream_t s);
+int64_t conv2d_workspace_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* a);
+int conv2d_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_conv2d_attrs* a,
+                void* workspace, hipStream_t s);
+int64_t dense_workspace_bytes(const tk_tensor* data, const tk_tensor* weight);
+int dense_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_dense_attrs* a,
+               void* workspace, hipStream_t s);
+
+// A tensor descriptor owned by the module (shape copied).
+struct OwnedTensor {
+  tk_tensor t{};
+  std::vector<int64_t> shape;
+  void assign(const tk_tensor* src) {
+    t = *src;
+    shape.assign(src->shape, src->shape + src->ndim);
+    t.shape = shape.data();
+    t.strides = nullptr;
+  }
+  OwnedTensor() = default;
+  OwnedTensor(const OwnedTensor& o) { assign(&o.t); }
+  OwnedTensor& operator=(const OwnedTensor& o) {
+    assign(&o.t);
+    return *this;
+  }
+};
+
+struct Node {
+  tk_node desc{};
+  OwnedTensor in[3];
+  OwnedTensor out;
+};
+
+static int run_node(Node& n, hipStream_t s) {
+  const tk_node& d = n.desc;
+  const tk_tensor* i0 = &n.in[0].t;
+  const tk_tensor* i1 = &n.in[1].t;
+  tk_tensor* o = &n.out.t;
+  switch (d.kind) {
+    case TK_NODE_CONV2D:
+      return conv2d_prepared_impl(i0, d.ext[0], i1, d.ext[1], (const int32_t*)d.ext[2], o, &d.attrs.conv2d, d.ext[3], s);
+    case TK_NODE_DENSE:
+      return dense_impl(i0, i1, o, &d.attrs.dense, d.ext[0], s);
+    case TK_NODE_REQUANTIZE:
+      return requantize_impl(i0, o, &d.attrs.requantize, s);
+    case TK_NODE_BIAS_ADD:
+      return bias_add_impl(i0, i1, o, d.attrs.bias_add.axis, s);
+    case TK_NODE_CLIP:
+      return clip_impl(i0, o, d.attrs.clip.a_min, d.attrs.clip.a_max, s);
+    case TK_NODE_CAST:
+      return cast_impl(i0, o, s);
+    case TK_NODE_QNN_ADD:
+      return qnn_add_impl(i0, i1, o, &d.attrs.qnn_add, s);
+    case TK_NODE_MAX_POOL2D:
+      return max_pool_impl(i0, o, &d.attrs.pool2d, s);
+    case TK_NODE_AVG_POOL2D:
+      return avg_pool_impl(i0, o, &d.attrs.pool2d, s);
+    case TK_NODE_GLOBAL_AVG_POOL2D:
+      return global_avg_pool_impl(i0, o, s);
+    case TK_NODE_COPY:
+      return copy_impl(i0, o, s);
+    case TK_NODE_SHADOW:
+      return nchw_to_nhwc_impl(i0, d.ext[0], s);
+  }
+  set_error("tk_module: unknown node kind " + std::to_string(d.kind));
+  return TK_ERR_INVALID_ARG;
+}
+
+}  // namespace tk
+
+struct tk_module {
+  std::vector<tk::Node> nodes;
+  std::vector<hipEvent_t> done;  // one per node, recorded after it on the compute stream
+  std::vector<hipEvent_t> prof;  // n+1 timing events for run_profiled / profiling mode
+  bool profiling = false;
+  bool have_times = false;
+  ~tk_module() {
+    for (auto e : done) (void)hipEventDestroy(e);
+    for (auto e : prof) (void)hipEventDestroy(e);
+  }
+};
+
+extern "C" {
+
+// ---------------------------------------------------------------- per-op API
+int64_t tk_conv2d_packed_weight_bytes(const tk_tensor* weight, int groups) {
+  return tk::conv_packed_weight_bytes(weight, groups);
+}
+int tk_conv2d_pack_weight(const tk_tensor* weight, int groups, void* packed, int32_t* weight_sums, void* stream) {
+  return tk::conv_pack_weight(weight, groups, packed, weight_sums, tk::as_stream(stream));
+}
+int64_t tk_conv2d_shadow_bytes(const tk_tensor* data) { return tk::conv_shadow_bytes(data); }
+int tk_nchw_to_nhwc_i8(const tk_tensor* data, void* shadow, void* stream) {
+  return tk::nchw_to_nhwc_impl(data, shadow, tk::as_stream(stream));
+}
+int tk_qnn_conv2d_prepared(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
+                           const int32_t* weight_sums, tk_tensor* out, const tk_conv2d_attrs* attrs, void* patch_sums,
+                           void* stream) {
+  return tk::conv2d_prepared_impl(data, shadow, weight, packed, weight_sums, out, attrs, patch_sums,
+                                  tk::as_stream(stream));
+}
+int64_t tk_qnn_conv2d_workspace_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* attrs) {
+  return tk::conv2d_workspace_bytes(data, weight, attrs);
+}
+int tk_qnn_conv2d(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_conv2d_attrs* attrs,
+                  void* workspace, void* stream) {
+  return tk::conv2d_impl(data, weight, out, attrs, workspace, tk::as_stream(stream));
+}
+int64_t tk_qnn_dense_workspace_bytes(const tk_tensor* data, const tk_tensor* weight) {
+  return tk::dense_workspace_bytes(data, weight);
+}
+int tk_qnn_dense(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_dense_attrs* attrs,
+                 void* workspace, void* stream) {
+  return tk::dense_impl(data, weight, out, attrs, workspace, tk::as_stream(stream));
+}
+int tk_requantize(const tk_tensor* data, tk_tensor* out, const tk_requantize_attrs* attrs, void* stream) {
+  return tk::requantize_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_add(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const tk_qnn_add_attrs* attrs,
+               void* stream) {
+  return tk::qnn_add_impl(lhs, rhs, out, attrs, tk::as_stream(stream));
+}
+int tk_bias_add(const tk_tensor* data, const tk_tensor* bias, tk_tensor* out, int axis, void* stream) {
+  return tk::bias_add_impl(data, bias, out, axis, tk::as_stream(stream));
+}
+int tk_clip(const tk_tensor* data, tk_tensor* out, int64_t a_min, int64_t a_max, void* stream) {
+  return tk::clip_impl(data, out, a_min, a_max, tk::as_stream(stream));
+}
+int tk_cast(const tk_tensor* data, tk_tensor* out, void* stream) {
+  return tk::cast_impl(data, out, tk::as_stream(stream));
+}
+int tk_max_pool2d(const tk_tensor* data, tk_tensor* out, const tk_pool2d_attrs* attrs, void* stream) {
+  return tk::max_pool_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_avg_pool2d(const tk_tensor* data, tk_tensor* out, const tk_pool2d_attrs* attrs, void* stream) {
+  return tk::avg_pool_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_global_avg_pool2d(const tk_tensor* data, tk_tensor* out, void* stream) {
+  return tk::global_avg_pool_impl(data, out, tk::as_stream(stream));
+}
+int tk_copy(const tk_tensor* data, tk_tensor* out, void* stream) {
+  return tk::copy_impl(data, out, tk::as_stream(stream));
+}
+int tk_digest_bytes(const void* data, int64_t nbytes, uint64_t* out_device, void* stream) {
+  return tk::digest_impl(data, nbytes, out_device, tk::as_stream(stream));
+}
+
+// ---------------------------------------------------------------- executor
+int tk_module_create(const tk_node* nodes, int n_nodes, tk_module** out) {
+  if (!out || n_nodes < 0 || (n_nodes > 0 && !nodes)) {
+    tk::set_error("tk_module_create: invalid argument");
+    return TK_ERR_INVALID_ARG;
+  }
+  auto mod = std::make_unique<tk_module>();
+  mod->nodes.resize(n_nodes);
+  for (int i = 0; i < n_nodes; ++i) {
+    const tk_node& src = nodes[i];
+    tk::Node& dst = mod->nodes[i];
+    dst.desc = src;
+    if (src.n_inputs < 0 || src.n_inputs > 3) {
+      tk::set_error("tk_module_create: node " + std::to_string(i) + " has a bad input count");
+      return TK_ERR_INVALID_ARG;
+    }
+    for (int k = 0; k < src.n_inputs; ++k) {
+      if (!src.inputs[k]) {
+        tk::set_error("tk_module_create: node " + std::to_string(i) + " has a null input");
+        return TK_ERR_INVALID_ARG;
+      }
+      dst.in[k].assign(src.inputs[k]);
+    }
+    if (src.kind != TK_NODE_SHADOW) {
+      if (!src.output) {
+        tk::set_error("tk_module_create: node " + std::to_string(i) + " has no output");
+        return TK_ERR_INVALID_ARG;
+      }
+      dst.out.assign(src.output);
+    }
+    for (int k = 0; k < 3; ++k) dst.desc.inputs[k] = nullptr;  // resolved through dst.in
+    dst.desc.output = nullptr;
+  }
+  mod->done.resize(n_nodes);
+  for (int i = 0; i < n_nodes; ++i) {
+    hipError_t e = hipEventCreateWithFlags(&mod->done[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+      mod->done.resize(i);
+      tk::set_error(std::string("tk_module_create: hipEventCreate failed: ") + hipGetErrorString(e));
+      return TK_ERR_HIP;
+    }
+  }
+  *out = mod.release();
+  return TK_OK;
+}
+
+int tk_module_destroy(tk_module* mod) {
+  delete mod;
+  return TK_OK;
+}
+
+int tk_module_num_nodes(const tk_module* mod) { return mod ? (int)mod->nodes.size() : 0; }
+
+static int ensure_prof_events(tk_module* mod) {
+  while (mod->prof.size() < mod->nodes.size() + 1) {
+    hipEvent_t e;
+    TK_HIP(hipEventCreate(&e));
+    mod->prof.push_back(e);
+  }
+  return TK_OK;
+}
+
+int tk_module_set_profiling(tk_module* mod, int enable) {
+  if (!mod) {
+    tk::set_error("tk_module_set_profiling: null module");
+    return TK_ERR_INVALID_ARG;
+  }
+  mod->profiling = enable != 0;
+  mod->have_times = false;
+  return mod->profiling ? ensure_prof_events(mod) : TK_OK;
+}
+
+int tk_module_node_times(tk_module* mod, float* node_ms) {
+  if (!mod || !node_ms || !mod->have_times) {
+    tk::set_error("tk_module_node_times: no profiled run recorded");
+    return TK_ERR_INVALID_ARG;
+  }
+  size_t n = mod->nodes.size();
+  TK_HIP(hipEventSynchronize(mod->prof[n]));
+  for (size_t i = 0; i < n; ++i) TK_HIP(hipEventElapsedTime(&node_ms[i], mod->prof[i], mod->prof[i + 1]));
+  return TK_OK;
+}
+
+int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst) {
+  if (!mod) {
+    tk::set_error("tk_module_run: null module");
+    return TK_ERR_INVALID_ARG;
+  }
+  hipStream_t s = tk::as_stream(stream);
+  hipStream_t cs = tk::as_stream(capture_stream);
+  bool capture = capture_stream && host_dst;
+  if (mod->profiling) TK_HIP(hipEventRecord(mod->prof[0], s));
+  for (size_t i = 0; i < mod->nodes.size(); ++i) {
+    tk::Node& n = mod->nodes[i];
+    int rc = tk::run_node(n, s);
+    if (rc) {
+      tk::set_error("node " + std::to_string(i) + ": " + tk_last_error());
+      return rc;
+    }
+    if (mod->profiling) TK_HIP(hipEventRecord(mod->prof[i + 1], s));
+    if (capture && host_dst[i] && n.desc.kind != TK_NODE_SHADOW) {
+      TK_HIP(hipEventRecord(mod->done[i], s));
+      TK_HIP(hipStreamWaitEvent(cs, mod->done[i], 0));
+      TK_HIP(hipMemcpyAsync(host_dst[i], tk::ptr(&n.out.t), tk::nbytes(&n.out.t), hipMemcpyDeviceToHost, cs));
+    }
+  }
+  mod->have_times = mod->profiling;
+  return TK_OK;
+}
+
+int tk_module_run_range(tk_module* mod, int begin, int end, void* stream) {
+  if (!mod || begin < 0 || end > (int)mod->nodes.size() || begin > end) {
+    tk::set_error("tk_module_run_range: bad range");
+    return TK_ERR_INVALID_ARG;
+  }
+  hipStream_t s = tk::as_stream(stream);
+  for (int i = begin; i < end; ++i) {
+    int rc = tk::run_node(mod->nodes[i], s);
+    if (rc) return rc;
+  }
+  return TK_OK;
+}
+
+int tk_module_run_profiled(tk_module* mod, void* stream, float* node_ms) {
+  if (!mod || !node_ms) {
+    tk::set_error("tk_module_run_profiled: invalid argument");
+    return TK_ERR_INVALID_ARG;
+  }
+  size_t n = mod->nodes.size();
+  int rc0 = ensure_prof_events(mod);
+  if (rc0) return rc0;
+  hipStream_t s = tk::as_stream(stream);
+  TK_HIP(hipEventRecord(mod->prof[0], s));
+  for (size_t i = 0; i < n; ++i) {
+    int rc = tk::run_node(mod->nodes[i], s);
+    if (rc) return rc;
+    TK_HIP(hipEventRecord(mod->prof[i + 1], s));
+  }
+  TK_HIP(hipEventSynchronize(mod->prof[n]));
+  for (size_t i = 0; i < n; ++i) TK_HIP(hipEventElapsedTime(&node_ms[i], mod->prof[i], mod->prof[i + 1]));
+  return TK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,31 @@
+"""Relay-compatible front door: ``relay.var/const``, ``relay.qnn.op.*``, ``relay.nn.*`` and
+``relay.build`` (python/tvm/relay/build_module.py:409) targeting the MI355X engine."""
+from . import qnn  # noqa: F401
+from .expr import (Call, Constant, Expr, Function, IRModule, TensorType, Var, const, free_vars,  # noqa: F401
+                   post_order, var)
+from .op import (avg_pool2d, batch_flatten, bias_add, cast, clip, global_avg_pool2d, max_pool2d,  # noqa: F401
+                 relu, reshape)
+from . import op as _op
+
+
+class _NN:
+    bias_add = staticmethod(_op.bias_add)
+    relu = staticmethod(_op.relu)
+    max_pool2d = staticmethod(_op.max_pool2d)
+    avg_pool2d = staticmethod(_op.avg_pool2d)
+    global_avg_pool2d = staticmethod(_op.global_avg_pool2d)
+    batch_flatten = staticmethod(_op.batch_flatten)
+
+
+nn = _NN()
+
+
+class analysis:  # noqa: N801  (mirrors relay.analysis)
+    free_vars = staticmethod(free_vars)
+    post_order = staticmethod(post_order)
+
+
+def build(mod, target: str = "mi355x", params=None, mod_name: str = "default"):
+    """``relay.build``: lower a QNN module to the MI355X engine (see build_module.py)."""
+    from .build_module import build as _build
+    return _build(mod, target=target, params=params, mod_name=mod_name)

@@ -1,0 +1,326 @@
+"""``relay.build`` for the MI355X engine.
+
+Reference surface: ``relay.build(ir_mod, target, params)``
+(python/tvm/relay/build_module.py:409-419) → ``lib["default"](dev)`` →
+``graph_executor.GraphModule`` (python/tvm/contrib/graph_executor.py:114-351).
+
+Lowering is split in two:
+  * ``lower(mod, params)`` → ``Plan``: topologically ordered ops named the way
+    MRT names symbols (``%N`` in post-order, python/tvm/mrt/symbol.py:212-253,
+    utils.py:29-67), with every QNN constant folded the way the reference's
+    canonicalisation folds it.  Pure host code (no GPU needed).
+  * ``ExecutorFactory(plan, params)["default"](dev)`` → a device module: one HBM
+    buffer per op output (no storage reuse, so every output stays traceable),
+    weights uploaded/packed once, and a native ``tk_module`` node list.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from .. import _lib
+from .expr import Call, Constant, Expr, IRModule, Var, post_order
+from .op import INT_DTYPES
+
+TARGETS = ("mi355x", "rocm", "hip", "gfx950")
+
+
+class UnsupportedError(NotImplementedError):
+    pass
+
+
+@dataclass
+class PlanTensor:
+    name: str
+    shape: Tuple[int, ...]
+    dtype: str
+
+    @property
+    def nbytes(self) -> int:
+        return int(np.prod(self.shape, dtype=np.int64)) * np.dtype(self.dtype).itemsize
+
+
+@dataclass
+class PlanOp:
+    index: int
+    name: str
+    op: str
+    inputs: List[str]
+    attrs: Dict[str, Any]
+    out: PlanTensor
+    consts: Dict[str, np.ndarray] = field(default_factory=dict)
+
+    def describe(self) -> Dict[str, Any]:
+        def py(v):
+            if isinstance(v, np.ndarray):
+                return v.tolist()
+            if isinstance(v, (np.integer,)):
+                return int(v)
+            if isinstance(v, (np.floating,)):
+                return float(v)
+            if isinstance(v, tuple):
+                return list(v)
+            return v
+        d = {"id": self.index, "name": self.name, "op": self.op, "inputs": list(self.inputs),
+             "shape": list(self.out.shape), "dtype": self.out.dtype,
+             "attrs": {k: py(v) for k, v in self.attrs.items()}}
+        if self.consts:
+            d["consts"] = {k: py(v) for k, v in self.consts.items()}
+        return d
+
+
+@dataclass
+class Plan:
+    inputs: List[PlanTensor]
+    params: List[PlanTensor]
+    ops: List[PlanOp]
+    outputs: List[str]
+
+    def tensor(self, name: str) -> PlanTensor:
+        for t in self.inputs + self.params:
+            if t.name == name:
+                return t
+        for o in self.ops:
+            if o.name == name:
+                return o.out
+        raise KeyError(name)
+
+    @property
+    def records(self) -> List[PlanTensor]:
+        """Traced tensors in file order: graph inputs, then every op output (topo order)."""
+        return list(self.inputs) + [o.out for o in self.ops]
+
+
+def _scalar(c: Expr, what: str):
+    if not isinstance(c, Constant):
+        raise UnsupportedError(f"{what} must be a relay.const")
+    return c.data
+
+
+def _resolve_rounding(attrs) -> Tuple[str, str]:
+    """SelectRequntizeParameter (src/relay/qnn/utils.cc:218-229) with the pinned defaults
+    (requantize_config.h:53-72: rounding UPWARD, compute_dtype int64 for llvm w/o -mcpu)."""
+    r = attrs.get("rounding", "None")
+    if r in (None, "None"):
+        r = attrs.get("cfg_rounding") or "UPWARD"
+    cd = attrs.get("compute_dtype", "None")
+    if cd in (None, "None"):
+        cd = attrs.get("cfg_compute_dtype") or "int64"
+    if r not in ("UPWARD", "TONEAREST"):
+        raise ValueError(f"qnn.requantize: rounding must be UPWARD or TONEAREST, got {r}")
+    if cd != "int64":
+        raise UnsupportedError(
+            f"qnn.requantize compute_dtype={cd}: the reference selects the float path only for llvm "
+            "targets with an SSE4.1 -mcpu; this engine implements the pinned integer (int64) path")
+    return r, cd
+
+
+def requantize_plan(input_scale: np.ndarray, output_scale, rounding: str):
+    """Fold scales into (mode, multipliers, shifts) through the library's host port of
+    RequantizeLowerInt's constant folding (tk_requantize_prepare)."""
+    lib = _lib.load()
+    s_in = np.asarray(input_scale, dtype=np.float32)
+    per_axis = s_in.ndim != 0
+    vals = s_in.reshape(-1) if per_axis else s_in.reshape(1)
+    n = len(vals) if per_axis else 0
+    cap = max(1, len(vals))
+    ms = (ctypes.c_int32 * cap)()
+    ss = (ctypes.c_int32 * cap)()
+    mode = ctypes.c_int()
+    arr = (ctypes.c_float * len(vals))(*[float(v) for v in vals])
+    rnd = _lib.TK_ROUND_UPWARD if rounding == "UPWARD" else _lib.TK_ROUND_TONEAREST
+    _lib.check(lib.tk_requantize_prepare(arr, n, ctypes.c_float(float(np.float32(output_scale))), rnd, ms, ss,
+                                         ctypes.byref(mode)), "tk_requantize_prepare")
+    return int(mode.value), np.array(ms[:cap], dtype=np.int32), np.array(ss[:cap], dtype=np.int32)
+
+
+def _clip_bound(v: float, dtype: str) -> int:
+    info = np.iinfo(np.dtype(dtype))
+    if not np.isfinite(v):
+        return int(info.max) if v > 0 else int(info.min)
+    iv = int(np.trunc(v))
+    return max(min(iv, int(info.max)), int(info.min))
+
+
+def lower(mod, params: Optional[Dict[str, Any]] = None) -> Plan:
+    """Topologically order the graph, name ops MRT-style and fold QNN constants."""
+    func = mod["main"] if isinstance(mod, IRModule) else IRModule.from_expr(mod)["main"]
+    params = {k: np.asarray(v.numpy() if hasattr(v, "numpy") else v) for k, v in (params or {}).items()}
+    nodes = post_order(func.body)
+    names: Dict[int, str] = {}
+    inputs: List[PlanTensor] = []
+    plist: List[PlanTensor] = []
+    ops: List[PlanOp] = []
+    counter = 0
+    for v in func.params:
+        if not isinstance(v, Var):
+            continue
+    for node in nodes:
+        if isinstance(node, Var):
+            names[id(node)] = node.name_hint
+            t = PlanTensor(node.name_hint, node.shape, node.dtype)
+            if node.name_hint in params:
+                p = params[node.name_hint]
+                if tuple(p.shape) != node.shape:
+                    raise TypeError(f"param {node.name_hint}: shape {p.shape} vs {node.shape}")
+                plist.append(t)
+            else:
+                inputs.append(t)
+        elif isinstance(node, Constant):
+            continue
+        elif isinstance(node, Call):
+            name = f"%{counter}"
+            counter += 1
+            names[id(node)] = name
+            ops.append(_lower_call(len(ops), name, node, names))
+        else:
+            raise UnsupportedError(f"expression type {type(node).__name__}")
+    # free vars not reachable from the body are ignored like Relay does for unused params
+    out = names[id(func.body)]
+    return Plan(inputs, plist, ops, [out])
+
+
+def _tensor_args(call: Call, k: int, names) -> List[str]:
+    out = []
+    for a in call.args[:k]:
+        if isinstance(a, Constant):
+            raise UnsupportedError(f"{call.op}: constant tensor operands must be passed as params (MRT symbols)")
+        out.append(names[id(a)])
+    return out
+
+
+def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
+    op = call.op
+    out = PlanTensor(name, call.shape, call.dtype)
+    a = dict(call.attrs)
+    consts: Dict[str, np.ndarray] = {}
+    if op == "qnn.conv2d":
+        ins = _tensor_args(call, 2, names)
+        za = _scalar(call.args[2], "qnn.conv2d input_zero_point")
+        zw = _scalar(call.args[3], "qnn.conv2d kernel_zero_point")
+        if np.ndim(za) != 0:
+            raise UnsupportedError("qnn.conv2d: per-channel input zero point")
+        a["input_zero_point"] = int(za)
+        if np.ndim(zw) == 0:
+            a["kernel_zero_point"] = int(zw)
+        else:
+            a["kernel_zero_point"] = 0
+            consts["kernel_zero_points"] = np.asarray(zw, np.int32).reshape(-1)
+        a["input_scale"] = _scalar(call.args[4], "scale").tolist()
+        a["kernel_scale"] = _scalar(call.args[5], "scale").tolist()
+    elif op == "qnn.dense":
+        ins = _tensor_args(call, 2, names)
+        za = _scalar(call.args[2], "qnn.dense input_zero_point")
+        zw = _scalar(call.args[3], "qnn.dense kernel_zero_point")
+        if np.ndim(za) != 0:
+            raise UnsupportedError("qnn.dense: per-channel input zero point")
+        a["input_zero_point"] = int(za)
+        if np.ndim(zw) == 0:
+            a["kernel_zero_point"] = int(zw)
+        else:
+            a["kernel_zero_point"] = 0
+            consts["kernel_zero_points"] = np.asarray(zw, np.int32).reshape(-1)
+        a["input_scale"] = _scalar(call.args[4], "scale").tolist()
+        a["kernel_scale"] = _scalar(call.args[5], "scale").tolist()
+    elif op == "qnn.requantize":
+        ins = _tensor_args(call, 1, names)
+        s_in = _scalar(call.args[1], "qnn.requantize input_scale")
+        zp_in = _scalar(call.args[2], "qnn.requantize input_zero_point")
+        s_out = _scalar(call.args[3], "qnn.requantize output_scale")
+        zp_out = _scalar(call.args[4], "qnn.requantize output_zero_point")
+        if np.ndim(zp_out) != 0:
+            raise UnsupportedError("qnn.requantize: per-axis output zero point")
+        rounding, cd = _resolve_rounding(a)
+        mode, ms, ss = requantize_plan(s_in, s_out, rounding)
+        nd = len(call.args[0].shape)
+        axis = a["axis"]
+        ax = axis if axis >= 0 else (nd + axis if nd > 0 else 0)
+        a.update(rounding=rounding, compute_dtype=cd, mode=mode, channel_axis=ax,
+                 input_scale=np.asarray(s_in, np.float32).tolist(), output_scale=float(np.float32(s_out)),
+                 output_zero_point=int(zp_out))
+        for k in ("cfg_rounding", "cfg_compute_dtype"):
+            a.pop(k, None)
+        if mode >= _lib.TK_RQ_AXIS_UPWARD:
+            consts["multipliers"] = ms
+            consts["shifts"] = ss
+        else:
+            a["multiplier"] = int(ms[0])
+            a["shift"] = int(ss[0])
+        if np.ndim(zp_in) == 0:
+            a["input_zero_point"] = int(zp_in)
+        else:
+            a["input_zero_point"] = 0
+            consts["input_zero_points"] = np.asarray(zp_in, np.int32).reshape(-1)
+    elif op == "qnn.add":
+        ins = _tensor_args(call, 2, names)
+        vals = [_scalar(call.args[i], "qnn.add param") for i in range(2, 8)]
+        if any(np.ndim(v) != 0 for v in vals):
+            raise UnsupportedError("qnn.add: per-tensor scales/zero points only")
+        ls, lz, rs, rz, os_, oz = vals
+        a.update(lhs_scale=float(np.float32(ls)), lhs_zero_point=int(lz), rhs_scale=float(np.float32(rs)),
+                 rhs_zero_point=int(rz), output_scale=float(np.float32(os_)), output_zero_point=int(oz))
+        for side, s, z in (("lhs", ls, lz), ("rhs", rs, rz)):
+            # RequantizeOrUpcast (op_common.h:186-200): cast when scale AND zero point match
+            up = np.float32(s).tobytes() == np.float32(os_).tobytes() and int(z) == int(oz)
+            a[f"{side}_upcast"] = int(up)
+            if not up:
+                mode, ms, ss = requantize_plan(np.float32(s), np.float32(os_), "UPWARD")
+                a[f"{side}_mode"], a[f"{side}_multiplier"], a[f"{side}_shift"] = mode, int(ms[0]), int(ss[0])
+            else:
+                a[f"{side}_mode"], a[f"{side}_multiplier"], a[f"{side}_shift"] = 0, 0, 0
+    elif op == "nn.bias_add":
+        ins = _tensor_args(call, 2, names)
+        nd = len(call.args[0].shape)
+        a["axis"] = a["axis"] if a["axis"] >= 0 else nd + a["axis"]
+    elif op == "clip":
+        ins = _tensor_args(call, 1, names)
+        a["lo"] = _clip_bound(a["a_min"], call.dtype)
+        a["hi"] = _clip_bound(a["a_max"], call.dtype)
+    elif op == "nn.relu":
+        ins = _tensor_args(call, 1, names)
+        a["lo"] = 0
+        a["hi"] = int(np.iinfo(np.dtype(call.dtype)).max)
+    elif op in ("cast", "nn.max_pool2d", "nn.avg_pool2d", "nn.global_avg_pool2d", "nn.batch_flatten", "reshape"):
+        ins = _tensor_args(call, 1, names)
+        if op == "cast" and (call.args[0].dtype not in INT_DTYPES or call.dtype not in INT_DTYPES):
+            raise UnsupportedError("cast: integer types only")
+    else:
+        raise UnsupportedError(f"operator {op} is not on the integer trace path")
+    return PlanOp(index, name, op, ins, a, out, consts)
+
+
+class ExecutorFactory:
+    """What ``relay.build`` returns (backend/executor_factory.py:148-211 analogue)."""
+
+    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], target: str, mod_name: str = "default"):
+        self.plan = plan
+        self.params = params
+        self.target = target
+        self.mod_name = mod_name
+
+    def __getitem__(self, key: str):
+        if key != self.mod_name:
+            raise KeyError(key)
+        return self._create
+
+    def get_params(self) -> Dict[str, np.ndarray]:
+        return dict(self.params)
+
+    def _create(self, dev=None):
+        from .device_module import DeviceModule
+        return DeviceModule(self.plan, self.params, dev)
+
+
+def build(mod, target: str = "mi355x", params=None, mod_name: str = "default") -> ExecutorFactory:
+    t = str(target).split()[0].lower()
+    if t not in TARGETS:
+        raise UnsupportedError(
+            f"target {target!r}: this engine builds for MI355X only ({', '.join(TARGETS)}); "
+            "the reference's CPU llvm path is not part of it")
+    params = {k: np.ascontiguousarray(np.asarray(v.numpy() if hasattr(v, "numpy") else v))
+              for k, v in (params or {}).items()}
+    plan = lower(mod, params)
+    return ExecutorFactory(plan, params, t, mod_name)

@@ -1,0 +1,265 @@
+"""Device-side module: HBM buffers + the native node list (tk_module).
+
+Memory layout in HBM (one GPU, one batch shard):
+  * params: uploaded once; MFMA convs additionally hold a packed
+    [Cout_pad][KH][KW][Cin_pad] int8 copy and int32 per-channel weight sums;
+  * graph inputs and EVERY op output get their own buffer (no storage-pool
+    reuse as in graph_executor.cc:356-464), so each output stays addressable
+    for the trace copy-out until the step ends — ResNet-50 at 64 samples is
+    ~7 GB, nothing next to 288 GB;
+  * conv inputs have an NHWC int8 shadow (channels padded to 16) produced by a
+    shadow node right before the first conv that reads them.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from .. import _lib
+from .build_module import Plan, PlanOp
+
+
+def _torch():
+    import torch
+    return torch
+
+
+_TORCH_DT = None
+
+
+def torch_dtype(name: str):
+    torch = _torch()
+    return {"int8": torch.int8, "uint8": torch.uint8, "int16": torch.int16, "int32": torch.int32,
+            "int64": torch.int64, "float32": torch.float32}[name]
+
+
+class DeviceModule:
+    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], dev=None):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise _lib.TachikomaError("no MI355X visible: the engine runs on the GPU only (no CPU fallback)")
+        self.lib = _lib.load()
+        self.plan = plan
+        self.device = torch.device("cuda", 0) if dev is None else _as_torch_device(dev)
+        self.buffers: Dict[str, "torch.Tensor"] = {}
+        self._keep: List[object] = []
+        self.node_names: List[Optional[str]] = []  # tk node index -> record name (None for shadows)
+        with torch.cuda.device(self.device):
+            self._alloc(params)
+            self._build_nodes()
+
+    # ------------------------------------------------------------ setup
+    def _alloc(self, params):
+        torch = _torch()
+        for t in self.plan.inputs:
+            self.buffers[t.name] = torch.zeros(t.shape, dtype=torch_dtype(t.dtype), device=self.device)
+        for t in self.plan.params:
+            self.buffers[t.name] = torch.from_numpy(np.ascontiguousarray(params[t.name])).to(self.device)
+        for op in self.plan.ops:
+            self.buffers[op.name] = torch.empty(op.out.shape, dtype=torch_dtype(op.out.dtype), device=self.device)
+
+    def _ref(self, name: str) -> _lib.TensorRef:
+        r = _lib.TensorRef.from_torch(self.buffers[name])
+        self._keep.append(r)
+        return r
+
+    def _dev_i32(self, arr: np.ndarray):
+        torch = _torch()
+        t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int32)).to(self.device)
+        self._keep.append(t)
+        return t
+
+    def _scratch(self, nbytes: int):
+        torch = _torch()
+        t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
+        self._keep.append(t)
+        return t
+
+    def _build_nodes(self):
+        torch = _torch()
+        nodes: List[_lib.tk_node] = []
+        shadows: Dict[str, object] = {}
+        stream = _lib.stream_handle()
+        for op in self.plan.ops:
+            kind = op.op
+            n = _lib.tk_node()
+            ins = [self._ref(x) for x in op.inputs]
+            out = self._ref(op.name)
+            a = op.attrs
+            if kind == "qnn.conv2d":
+                n.kind = _lib.NODE_KINDS["qnn.conv2d"]
+                ca = n.attrs.conv2d
+                ca.strides[:] = list(a["strides"])
+                ca.padding[:] = list(a["padding"])
+                ca.dilation[:] = list(a["dilation"])
+                ca.groups = a["groups"]
+                ca.input_zero_point = a["input_zero_point"]
+                ca.kernel_zero_point = a["kernel_zero_point"]
+                if "kernel_zero_points" in op.consts:
+                    ca.kernel_zero_points = self._dev_i32(op.consts["kernel_zero_points"]).data_ptr()
+                ws = self.lib.tk_qnn_conv2d_workspace_bytes(ins[0].ptr, ins[1].ptr, ctypes.byref(ca))
+                if ws < 0:
+                    _lib.check(-3, f"{op.name} qnn.conv2d workspace")
+                if ws > 0:  # MFMA implicit-GEMM path: shadow + packed weight
+                    src = op.inputs[0]
+                    if src not in shadows:
+                        sh = self._scratch(self.lib.tk_conv2d_shadow_bytes(ins[0].ptr))
+                        shadows[src] = sh
+                        sn = _lib.tk_node()
+                        sn.kind = _lib.NODE_KINDS["shadow"]
+                        sn.n_inputs = 1
+                        sn.inputs[0] = ins[0].ptr
+                        sn.ext[0] = sh.data_ptr()
+                        nodes.append(sn)
+                        self.node_names.append(None)
+                    packed = self._scratch(self.lib.tk_conv2d_packed_weight_bytes(ins[1].ptr, 1))
+                    o = op.out.shape[1]
+                    sums = self._scratch(((o + 127) // 128 * 128) * 4)
+                    _lib.check(self.lib.tk_conv2d_pack_weight(ins[1].ptr, 1, ctypes.c_void_p(packed.data_ptr()),
+                                                              ctypes.c_void_p(sums.data_ptr()), stream),
+                               f"{op.name} pack weight")
+                    n.ext[0] = shadows[src].data_ptr()
+                    n.ext[1] = packed.data_ptr()
+                    n.ext[2] = sums.data_ptr()
+                    if a["kernel_zero_point"] != 0 or "kernel_zero_points" in op.consts:
+                        p = int(np.prod(op.out.shape)) // op.out.shape[1]
+                        n.ext[3] = self._scratch(p * 4).data_ptr()
+            elif kind == "qnn.dense":
+                n.kind = _lib.NODE_KINDS["qnn.dense"]
+                da = n.attrs.dense
+                da.input_zero_point = a["input_zero_point"]
+                da.kernel_zero_point = a["kernel_zero_point"]
+                if "kernel_zero_points" in op.consts:
+                    da.kernel_zero_points = self._dev_i32(op.consts["kernel_zero_points"]).data_ptr()
+                ws = self.lib.tk_qnn_dense_workspace_bytes(ins[0].ptr, ins[1].ptr)
+                n.ext[0] = self._scratch(ws).data_ptr()
+            elif kind == "qnn.requantize":
+                n.kind = _lib.NODE_KINDS["qnn.requantize"]
+                self._fill_rq(n.attrs.requantize, op)
+            elif kind == "qnn.add":
+                n.kind = _lib.NODE_KINDS["qnn.add"]
+                qa = n.attrs.qnn_add
+                for side in ("lhs", "rhs"):
+                    r = getattr(qa, side)
+                    r.mode = a[f"{side}_mode"]
+                    r.axis = -1
+                    r.multiplier = a[f"{side}_multiplier"]
+                    r.shift = a[f"{side}_shift"]
+                    r.input_zero_point = a[f"{side}_zero_point"]
+                    r.output_zero_point = a["output_zero_point"]
+                qa.output_zero_point = a["output_zero_point"]
+                qa.lhs_upcast = a["lhs_upcast"]
+                qa.rhs_upcast = a["rhs_upcast"]
+            elif kind == "nn.bias_add":
+                n.kind = _lib.NODE_KINDS["nn.bias_add"]
+                n.attrs.bias_add.axis = a["axis"]
+            elif kind in ("clip", "nn.relu"):
+                n.kind = _lib.NODE_KINDS["clip"]
+                n.attrs.clip.a_min = a["lo"]
+                n.attrs.clip.a_max = a["hi"]
+            elif kind == "cast":
+                n.kind = _lib.NODE_KINDS["cast"]
+            elif kind in ("nn.max_pool2d", "nn.avg_pool2d"):
+                n.kind = _lib.NODE_KINDS[kind]
+                pa = n.attrs.pool2d
+                pa.pool_size[:] = list(a["pool_size"])
+                pa.strides[:] = list(a["strides"])
+                pa.padding[:] = list(a["padding"])
+                pa.dilation[:] = list(a["dilation"])
+                pa.count_include_pad = int(a.get("count_include_pad", False))
+            elif kind == "nn.global_avg_pool2d":
+                n.kind = _lib.NODE_KINDS[kind]
+            elif kind in ("nn.batch_flatten", "reshape"):
+                n.kind = _lib.NODE_KINDS["copy"]
+            else:
+                raise _lib.TachikomaError(f"no device lowering for {kind}")
+            n.n_inputs = len(ins)
+            for k, r in enumerate(ins):
+                n.inputs[k] = r.ptr
+            n.output = out.ptr
+            nodes.append(n)
+            self.node_names.append(op.name)
+        torch.cuda.current_stream().synchronize()
+        arr = (_lib.tk_node * max(1, len(nodes)))(*nodes)
+        handle = ctypes.c_void_p()
+        _lib.check(self.lib.tk_module_create(arr, len(nodes), ctypes.byref(handle)), "tk_module_create")
+        self.handle = handle
+        self.n_nodes = len(nodes)
+
+    def _fill_rq(self, r, op: PlanOp):
+        a = op.attrs
+        r.mode = a["mode"]
+        r.axis = a["channel_axis"]
+        r.multiplier = a.get("multiplier", 0)
+        r.shift = a.get("shift", 0)
+        if "multipliers" in op.consts:
+            r.multipliers = self._dev_i32(op.consts["multipliers"]).data_ptr()
+            r.shifts = self._dev_i32(op.consts["shifts"]).data_ptr()
+        r.input_zero_point = a["input_zero_point"]
+        if "input_zero_points" in op.consts:
+            r.input_zero_points = self._dev_i32(op.consts["input_zero_points"]).data_ptr()
+        r.output_zero_point = a["output_zero_point"]
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.lib.tk_module_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    # ------------------------------------------------------------ execution
+    def set_input(self, name: str, value) -> None:
+        torch = _torch()
+        buf = self.buffers[name]
+        if isinstance(value, torch.Tensor):
+            buf.copy_(value.to(buf.dtype).reshape(buf.shape), non_blocking=True)
+        else:
+            v = np.asarray(value.numpy() if hasattr(value, "numpy") else value)
+            if tuple(v.shape) != tuple(buf.shape):
+                raise ValueError(f"set_input {name}: shape {v.shape} vs {tuple(buf.shape)}")
+            buf.copy_(torch.from_numpy(np.ascontiguousarray(v.astype(np.dtype(str(buf.dtype).replace("torch.", ""))))))
+
+    def run(self, stream=None, capture_stream=None, host_dst=None) -> None:
+        s = _lib.stream_handle(stream)
+        if host_dst is not None:
+            arr = (ctypes.c_void_p * self.n_nodes)(*host_dst)
+            _lib.check(self.lib.tk_module_run(self.handle, ctypes.c_void_p(s),
+                                              ctypes.c_void_p(_lib.stream_handle(capture_stream)), arr),
+                       "tk_module_run")
+        else:
+            _lib.check(self.lib.tk_module_run(self.handle, ctypes.c_void_p(s), None, None), "tk_module_run")
+
+    def run_profiled(self, stream=None) -> Dict[str, float]:
+        ms = (ctypes.c_float * self.n_nodes)()
+        _lib.check(self.lib.tk_module_run_profiled(self.handle, ctypes.c_void_p(_lib.stream_handle(stream)), ms),
+                   "tk_module_run_profiled")
+        out = {}
+        for i, name in enumerate(self.node_names):
+            out[name if name is not None else f"<shadow:{i}>"] = float(ms[i])
+        return out
+
+    def set_profiling(self, enable: bool) -> None:
+        _lib.check(self.lib.tk_module_set_profiling(self.handle, int(enable)), "tk_module_set_profiling")
+
+    def node_times(self) -> List[float]:
+        ms = (ctypes.c_float * self.n_nodes)()
+        _lib.check(self.lib.tk_module_node_times(self.handle, ms), "tk_module_node_times")
+        return [float(v) for v in ms]
+
+    def output(self, name: str):
+        return self.buffers[name]
+
+
+def _as_torch_device(dev):
+    torch = _torch()
+    if isinstance(dev, torch.device):
+        return dev
+    if isinstance(dev, int):
+        return torch.device("cuda", dev)
+    if hasattr(dev, "device_id"):
+        return torch.device("cuda", int(dev.device_id))
+    return torch.device(dev)

@@ -1,0 +1,139 @@
+"""Minimal Relay-style expression IR for integer QNN graphs.
+
+Mirrors the subset of ``tvm.relay`` the reference's trace path consumes
+(``python/tvm/relay/expr.py`` Var/Constant/Call, ``python/tvm/ir/module.py``
+IRModule) — enough to write the same graph-building code as the reference's
+tests and MRT driver, with eager type inference on construction.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+
+@dataclass(frozen=True)
+class TensorType:
+    shape: Tuple[int, ...]
+    dtype: str
+
+    @property
+    def concrete_shape(self):
+        return self.shape
+
+
+class Expr:
+    checked_type: TensorType
+
+    @property
+    def shape(self) -> Tuple[int, ...]:
+        return self.checked_type.shape
+
+    @property
+    def dtype(self) -> str:
+        return self.checked_type.dtype
+
+
+class Var(Expr):
+    def __init__(self, name_hint: str, shape: Sequence[int], dtype: str = "float32"):
+        self.name_hint = name_hint
+        self.checked_type = TensorType(tuple(int(s) for s in shape), str(np.dtype(dtype)))
+
+    def __repr__(self):
+        return f"%{self.name_hint}: Tensor[{self.shape}, {self.dtype}]"
+
+
+class Constant(Expr):
+    def __init__(self, data: np.ndarray):
+        self.data = np.asarray(data)
+        self.checked_type = TensorType(tuple(self.data.shape), str(self.data.dtype))
+
+    def is_scalar(self) -> bool:
+        return self.data.ndim == 0
+
+    def numpy(self) -> np.ndarray:
+        return self.data
+
+    def __repr__(self):
+        return f"const({self.data.tolist()}, {self.dtype})"
+
+
+class Call(Expr):
+    def __init__(self, op: str, args: List[Expr], attrs: Dict[str, Any], ret: TensorType):
+        self.op = op
+        self.args = list(args)
+        self.attrs = dict(attrs)
+        self.checked_type = ret
+
+    def __repr__(self):
+        return f"{self.op}({', '.join(type(a).__name__ for a in self.args)})"
+
+
+class Function:
+    def __init__(self, params: List[Var], body: Expr):
+        self.params = list(params)
+        self.body = body
+
+
+class IRModule:
+    def __init__(self, main: Function):
+        self.functions = {"main": main}
+
+    @staticmethod
+    def from_expr(expr) -> "IRModule":
+        if isinstance(expr, Function):
+            return IRModule(expr)
+        return IRModule(Function(free_vars(expr), expr))
+
+    def __getitem__(self, name: str) -> Function:
+        return self.functions[name]
+
+
+def var(name_hint: str, shape: Sequence[int] = (), dtype: str = "float32") -> Var:
+    return Var(name_hint, shape, dtype)
+
+
+def const(value, dtype: Optional[str] = None) -> Constant:
+    """``relay.const``: python floats default to float32, ints to int32 (python/tvm/relay/expr.py)."""
+    if isinstance(value, Constant):
+        return value
+    if dtype is None:
+        if isinstance(value, float):
+            dtype = "float32"
+        elif isinstance(value, (bool, np.bool_)):
+            dtype = "bool"
+        elif isinstance(value, int):
+            dtype = "int32"
+    arr = np.asarray(value)
+    if dtype is not None:
+        arr = arr.astype(dtype)
+    elif arr.dtype == np.float64:
+        arr = arr.astype(np.float32)
+    elif arr.dtype == np.int64:
+        arr = arr.astype(np.int32)
+    return Constant(arr)
+
+
+def post_order(expr: Expr) -> List[Expr]:
+    """Post-order DFS over args (``relay.analysis.post_order_visit``); each node once."""
+    out: List[Expr] = []
+    seen = set()
+    stack = [(expr, False)]
+    while stack:
+        node, expanded = stack.pop()
+        if id(node) in seen:
+            continue
+        if expanded or not isinstance(node, Call):
+            seen.add(id(node))
+            out.append(node)
+            continue
+        stack.append((node, True))
+        for a in reversed(node.args):
+            if id(a) not in seen:
+                stack.append((a, False))
+    return out
+
+
+def free_vars(expr: Expr) -> List[Var]:
+    return [n for n in post_order(expr) if isinstance(n, Var)]

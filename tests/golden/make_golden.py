@@ -1,0 +1,227 @@
+"""Generate tests/golden/qnn_kats.json: the reference's literal known-answer vectors.
+
+The reference (a TVM 0.11.dev0 fork) cannot be imported or built in this image
+(``import tvm`` fails, submodules empty, no LLVM dev libs), so
+these fixtures are *transcriptions of the literal input/expected-output data*
+that the reference's own unit tests assert with ``np.testing.assert_equal`` on
+target ``llvm``.  Each case records the test file:line it comes from.  Only
+data (inputs, attributes, expected outputs) is stored — no reference source.
+
+Run:  python tests/golden/make_golden.py   (rewrites qnn_kats.json)
+"""
+import json
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+RQ = "tests/python/relay/test_op_qnn_requantize.py"
+DENSE = "tests/python/relay/test_op_qnn_dense.py"
+CONV = "tests/python/relay/test_op_qnn_conv2d.py"
+ADD = "tests/python/relay/test_op_qnn_add.py"
+
+
+def arr(a, dtype):
+    a = np.asarray(a).astype(dtype)
+    flat = a.reshape(-1)
+    if flat.size > 64 and np.all(flat == flat[0]):
+        return {"dtype": dtype, "shape": list(a.shape), "fill": flat[0].item()}
+    return {"dtype": dtype, "shape": list(a.shape), "data": flat.tolist()}
+
+
+def rq_case(src, name, data, data_dtype, out_dtype, s_in, s_out, expect, rounding,
+            zp_in=0, zp_out=0, axis=0, shape=None):
+    d = np.asarray(data)
+    if shape is not None:
+        d = d.reshape(shape)
+    e = np.asarray(expect).reshape(d.shape)
+    return {
+        "op": "qnn.requantize", "source": src, "name": name,
+        "inputs": {"data": arr(d, data_dtype)},
+        "attrs": {"input_scale": s_in, "input_zero_point": zp_in, "output_scale": s_out,
+                  "output_zero_point": zp_out, "axis": axis, "rounding": rounding,
+                  "out_dtype": out_dtype},
+        "expected": arr(e, out_dtype),
+    }
+
+
+def requantize_cases():
+    cases = []
+    for rounding in ("UPWARD", "TONEAREST"):
+        d = np.arange(-100, 100)
+        cases.append(rq_case(f"{RQ}:81-98", "same_scale", d, "int32", "int8", 0.5, 0.5, d, rounding))
+        cases.append(rq_case(f"{RQ}:101-117", "scalar_same_scale", np.array(-10), "int32", "int8",
+                             0.5, 0.5, np.array(-10), rounding))
+        # test_downscale (:120-204)
+        pos = np.arange(0, 32)
+        neg = np.arange(0, -32, -1)
+        cases.append(rq_case(f"{RQ}:133-136", "downscale_16_pos", pos, "int32", "int8", 1.0, 16.0,
+                             np.repeat([0, 1, 2], [8, 16, 8]), rounding))
+        exp = np.repeat([0, -1, -2], [9, 16, 7]) if rounding == "UPWARD" else np.repeat([0, -1, -2], [8, 16, 8])
+        cases.append(rq_case(f"{RQ}:138-144", "downscale_16_neg", neg, "int32", "int8", 1.0, 16.0, exp, rounding))
+        cases.append(rq_case(f"{RQ}:156-160", "downscale_4_pos", pos, "int32", "int8", 1.0, 4.0,
+                             np.repeat([0, 1, 2, 3, 4, 5, 6, 7, 8], [2, 4, 4, 4, 4, 4, 4, 4, 2]), rounding))
+        if rounding == "UPWARD":
+            exp = np.repeat([0, -1, -2, -3, -4, -5, -6, -7, -8], [3, 4, 4, 4, 4, 4, 4, 4, 1])
+        else:
+            exp = np.repeat([0, -1, -2, -3, -4, -5, -6, -7, -8], [2, 4, 4, 4, 4, 4, 4, 4, 2])
+        cases.append(rq_case(f"{RQ}:162-173", "downscale_4_neg", neg, "int32", "int8", 1.0, 4.0, exp, rounding))
+        cases.append(rq_case(f"{RQ}:175-189", "downscale_16_uint8_out", pos, "int32", "uint8", 1.0, 16.0,
+                             np.repeat([0, 1, 2], [8, 16, 8]), rounding))
+        cases.append(rq_case(f"{RQ}:191-204", "downscale_16_uint8_in_out", pos, "uint8", "uint8", 1.0, 16.0,
+                             np.repeat([0, 1, 2], [8, 16, 8]), rounding))
+        # test_upscale (:207-230)
+        cases.append(rq_case(f"{RQ}:220-224", "upscale_pos", pos, "int32", "int8", 2.0, 1.0, 2 * pos, rounding))
+        cases.append(rq_case(f"{RQ}:226-230", "upscale_neg", neg, "int32", "int8", 2.0, 1.0, 2 * neg, rounding))
+        # test_non_power_of_two (:233-275)
+        cases.append(rq_case(f"{RQ}:246-249", "npot_div3_pos", 3 * pos, "int32", "int8", 1.0, 3.0, pos, rounding))
+        cases.append(rq_case(f"{RQ}:251-254", "npot_div3_neg", 3 * neg, "int32", "int8", 1.0, 3.0, neg, rounding))
+        cases.append(rq_case(f"{RQ}:266-269", "npot_mul3_pos", pos, "int32", "int8", 3.0, 1.0, 3 * pos, rounding))
+        cases.append(rq_case(f"{RQ}:271-274", "npot_mul3_neg", neg, "int32", "int8", 3.0, 1.0, 3 * neg, rounding))
+        # test_saturation (:278-322)
+        cases.append(rq_case(f"{RQ}:290-296", "saturation_pos", 120 + np.arange(16), "int32", "int8", 0.5, 0.5,
+                             [120, 121, 122, 123, 124, 125, 126, 127] + [127] * 8, rounding))
+        cases.append(rq_case(f"{RQ}:298-321", "saturation_neg", -120 - np.arange(16), "int32", "int8", 0.5, 0.5,
+                             [-120, -121, -122, -123, -124, -125, -126, -127] + [-128] * 8, rounding))
+        # test_zero_point (:325-384)
+        cases.append(rq_case(f"{RQ}:340-344", "out_zp_pos", pos, "int32", "int8", 1.0, 16.0,
+                             1 + np.repeat([0, 1, 2], [8, 16, 8]), rounding, zp_out=1))
+        exp = np.repeat([-2, -3, -4], [9, 16, 7]) if rounding == "UPWARD" else np.repeat([-2, -3, -4], [8, 16, 8])
+        cases.append(rq_case(f"{RQ}:346-353", "out_zp_neg", np.arange(-32, -64, -1), "int32", "int8", 1.0, 16.0,
+                             1 + exp, rounding, zp_out=1))
+        cases.append(rq_case(f"{RQ}:369-372", "in_zp_pos", np.arange(32, 64), "int32", "int8", 1.0, 16.0,
+                             np.repeat([2, 3, 4], [8, 16, 8]) - 1, rounding, zp_in=16))
+        cases.append(rq_case(f"{RQ}:374-381", "in_zp_neg", np.arange(-32, -64, -1), "int32", "int8", 1.0, 16.0,
+                             exp - 1, rounding, zp_in=16))
+        # per-channel (:387-479)
+        d = np.arange(-5, 5).reshape(5, 2)
+        cases.append(rq_case(f"{RQ}:389-403", "per_channel_same_scale_2d", d, "int32", "int8", [0.5, 0.5], 0.5,
+                             d, rounding, axis=1))
+        d = np.arange(-10, 10).reshape(2, 2, 5)
+        cases.append(rq_case(f"{RQ}:405-420", "per_channel_same_scale_3d", d, "int32", "int8", [0.5, 0.5], 0.5,
+                             d, rounding, axis=1))
+        d = np.arange(-5, 5).reshape(5, 2)
+        cases.append(rq_case(f"{RQ}:424-441", "per_channel_diff_scale_2d", d, "int32", "int8", [0.5, 0.25], 0.5,
+                             [-5, -2, -3, -1, -1, 0, 1, 1, 3, 2], rounding, axis=1))
+        d = np.arange(-20, 20, 2).reshape(2, 2, 5)
+        cases.append(rq_case(f"{RQ}:443-460", "per_channel_diff_scale_3d", d, "int32", "int8", [0.5, 0.25], 0.5,
+                             [-20, -18, -16, -14, -12, -5, -4, -3, -2, -1, 0, 2, 4, 6, 8, 5, 6, 7, 8, 9],
+                             rounding, axis=1))
+        d = np.arange(-5, 5).reshape(5, 2)
+        cases.append(rq_case(f"{RQ}:462-479", "per_channel_in_gt_out_2d", d, "int32", "int8", [1.0, 0.25], 0.5,
+                             [-10, -2, -6, -1, -2, 0, 2, 1, 6, 2], rounding, axis=1))
+    # test_default_cfg_and_no_args (:482-492): default rounding is UPWARD
+    cases.append(rq_case(f"{RQ}:482-492", "default_cfg", np.arange(0, -32, -1), "int32", "int8", 1.0, 16.0,
+                         np.repeat([0, -1, -2], [9, 16, 7]), "UPWARD"))
+    return cases
+
+
+def dense_cases():
+    data = np.array([1, 3, 5, 7, 9, 11, 13, 15, -19, -21, 1, 3, 5, 7, 9, 11, 13, -17, 17, -21]).reshape(2, 10)
+    kernel = np.tile(np.array([1, 3, 5, 7, 9, 11, 13, 15, 17, 19]), 3).reshape(3, 10)
+    base = {"op": "qnn.dense", "inputs": {"data": arr(data, "int8"), "weight": arr(kernel, "int8")},
+            "attrs": {"input_zero_point": -1, "kernel_zero_point": -1, "input_scale": 0.5,
+                      "kernel_scale": 0.5, "units": 3}}
+    cases = []
+    c = json.loads(json.dumps(base))
+    c.update(source=f"{DENSE}:81-145,223-228", name="dense_no_bias",
+             expected=arr(np.array([92, 92, 92, 228, 228, 228]).reshape(2, 3), "int32"))
+    cases.append(c)
+    c = json.loads(json.dumps(base))
+    c.update(source=f"{DENSE}:81-145,231-236", name="dense_bias", bias=arr([4, 8, 12], "int32"),
+             expected=arr(np.array([96, 100, 104, 232, 236, 240]).reshape(2, 3), "int32"))
+    cases.append(c)
+    c = json.loads(json.dumps(base))
+    c.update(source=f"{DENSE}:81-145,239-245", name="dense_bias_requantize", bias=arr([4, 8, 12], "int32"),
+             requantize={"input_scale": 0.25, "output_scale": 1.0, "output_zero_point": -1, "out_dtype": "int8"},
+             expected=arr(np.array([23, 24, 25, 57, 58, 59]).reshape(2, 3), "int8"))
+    cases.append(c)
+    # per-channel: requantize input_scale = 0.5 * float32([0.5, 0.3, 0.4]) computed in float32
+    pc = (0.5 * np.array([0.5, 0.3, 0.4], dtype=np.float32)).astype(np.float32)
+    c = json.loads(json.dumps(base))
+    c.update(source=f"{DENSE}:131-133,248-252", name="dense_per_channel", bias=arr([4, 8, 12], "int32"),
+             requantize={"input_scale": [float(v) for v in pc], "output_scale": 1.0, "output_zero_point": -1,
+                         "out_dtype": "int8"},
+             expected=arr(np.array([23, 14, 20, 57, 34, 47]).reshape(2, 3), "int8"))
+    cases.append(c)
+    return cases
+
+
+def conv_cases():
+    cases = []
+    cases.append({
+        "op": "qnn.conv2d", "source": f"{CONV}:766-803", "name": "tflite_large_irregular",
+        "inputs": {"data": arr(np.full((1, 1024, 1, 1), 127), "uint8"),
+                   "weight": arr(np.full((1001, 1024, 1, 1), 127), "uint8")},
+        "attrs": {"input_zero_point": 127, "kernel_zero_point": 127, "strides": [1, 1], "padding": [0, 0, 0, 0],
+                  "dilation": [1, 1], "groups": 1},
+        "expected": arr(np.zeros((1, 1001, 1, 1)), "int32"),
+    })
+    data = 128 + np.array((1, 1, 1, 1, 2, 2, 2, 2, 1, 2, 3, 4, 1, 2, 3, 4)).reshape(2, 1, 2, 4)
+    weight = 128 + np.array((1, 2, 3, 4, -1, 1, -1, 1, -1, -1, 1, 1)).reshape(3, 1, 2, 2)
+    cases.append({
+        "op": "qnn.conv2d", "source": f"{CONV}:806-848", "name": "tflite_output_multiplier_greater_than_one",
+        "inputs": {"data": arr(data, "uint8"), "weight": arr(weight, "uint8")},
+        "attrs": {"input_zero_point": 128, "kernel_zero_point": 128, "strides": [2, 2], "padding": [0, 0, 0, 0],
+                  "dilation": [1, 1], "groups": 1},
+        "expected": arr(np.array((17, 17, 0, 0, 2, 2, 16, 36, 2, 2, 0, 0)).reshape(2, 3, 1, 2), "int32"),
+    })
+    data = np.array((133, 131, 129, 125, 123, 121, 135, 133, 131, 123, 121, 119, 137, 135, 133, 121, 119,
+                     117)).reshape(1, 1, 3, 6)
+    weight = np.array((129, 131, 133, 135)).reshape(1, 1, 2, 2)
+    cases.append({
+        "op": "qnn.conv2d", "source": f"{CONV}:851-911", "name": "tflite_anisotropic_strides",
+        "inputs": {"data": arr(data, "uint8"), "weight": arr(weight, "uint8")},
+        "attrs": {"input_zero_point": 127, "kernel_zero_point": 127, "strides": [1, 3], "padding": [0, 0, 0, 0],
+                  "dilation": [1, 1], "groups": 1},
+        "expected": arr(np.array((124, -92, 164, -132)).reshape(1, 1, 2, 2), "int32"),
+    })
+    return cases
+
+
+def add_case(src, name, x, y, ls, lz, rs, rz, os_, oz, expect):
+    return {"op": "qnn.add", "source": src, "name": name,
+            "inputs": {"lhs": arr(np.array(x).reshape(1, 4), "uint8"), "rhs": arr(np.array(y).reshape(1, 4), "uint8")},
+            "attrs": {"lhs_scale": ls, "lhs_zero_point": lz, "rhs_scale": rs, "rhs_zero_point": rz,
+                      "output_scale": os_, "output_zero_point": oz},
+            "expected": arr(np.array(expect).reshape(1, 4), "uint8")}
+
+
+def add_cases():
+    c = []
+    xs = [(140, 153, 165, 178), (25, 153, 178, 216), (25, 153, 216, 165)]
+    ys = [(204, 178, 165, 140), (204, 178, 191, 25), (204, 178, 25, 191)]
+    gs = [(217, 204, 203, 191), (102, 204, 242, 114), (102, 204, 114, 229)]
+    for i in range(3):
+        c.append(add_case(f"{ADD}:23-69", f"same_io_params_{i}", xs[i], ys[i], 0.00784314, 127, 0.00784314, 127,
+                          0.00784314, 127, gs[i]))
+    xs = [(76, 140, 153, 172), (133, 140, 146, 153), (76, 140, 172, 146)]
+    ys = [(136, 119, 128, 17), (136, 119, 111, 94), (136, 119, 17, 128)]
+    gs = [(120, 154, 167, 124), (158, 154, 154, 150), (120, 154, 124, 163)]
+    for i in range(3):
+        c.append(add_case(f"{ADD}:72-118", f"different_io_params_{i}", xs[i], ys[i], 0.0156863, 127, 0.0117647, 85,
+                          0.0235294, 128, gs[i]))
+    c.append(add_case(f"{ADD}:121-150", "saturation_same", (255, 1, 1, 0), (255, 255, 128, 0), 0.125, 0, 0.125, 0,
+                      0.125, 0, (255, 255, 129, 0)))
+    c.append(add_case(f"{ADD}:152-177", "saturation_out_scale", (255, 1, 1, 0), (255, 255, 127, 0), 0.125, 0, 0.125,
+                      0, 0.25, 0, (255, 129, 65, 0)))
+    c.append(add_case(f"{ADD}:205-232", "saturation_all_diff", (255, 0, 1, 0), (0, 128, 64, 0), 0.5, 0, 0.25, 0,
+                      0.125, 0, (255, 255, 132, 0)))
+    return c
+
+
+def main():
+    doc = {
+        "about": "Literal known-answer vectors transcribed from the reference's unit tests "
+                 "(CortexFoundation/tachikoma @ /root/reference). Generated by make_golden.py.",
+        "pinned_config": {"target": "llvm (no -mcpu)", "compute_dtype": "int64", "rounding_default": "UPWARD"},
+        "cases": requantize_cases() + dense_cases() + conv_cases() + add_cases(),
+    }
+    path = os.path.join(HERE, "qnn_kats.json")
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=None, separators=(",", ":"))
+    print(f"wrote {len(doc['cases'])} cases to {path}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,107 @@
+"""C-ABI library: loads without a GPU, exports every declared symbol, ctypes layouts match C,
+and the host-side constant folding equals the oracle's restatement."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import qnn_ref as ref
+from tachikoma_amd import _lib
+from tachikoma_amd.relay.build_module import requantize_plan
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "tachikoma.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tk_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) > 30
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
+    assert lib.tk_abi_version() == 1
+    assert lib.tk_build_arch() == b"gfx950"
+
+
+LAYOUT_C = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "tachikoma.h"
+#define P(T) printf(#T " %zu\n", sizeof(T));
+#define O(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  P(tk_tensor) P(tk_requantize_attrs) P(tk_conv2d_attrs) P(tk_dense_attrs) P(tk_qnn_add_attrs)
+  P(tk_pool2d_attrs) P(tk_node) P(tk_array_meta) P(tk_trace_header)
+  O(tk_tensor, shape) O(tk_tensor, byte_offset) O(tk_node, inputs) O(tk_node, output) O(tk_node, ext)
+  O(tk_node, attrs) O(tk_qnn_add_attrs, rhs) O(tk_qnn_add_attrs, lhs_upcast) O(tk_requantize_attrs, output_zero_point)
+  O(tk_conv2d_attrs, kernel_zero_points) O(tk_array_meta, dtype)
+  return 0;
+}
+"""
+
+
+def test_ctypes_layout_matches_c(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(LAYOUT_C)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.check_output([str(exe)]).decode().split("\n") if line)
+    py = {
+        "tk_tensor": ctypes.sizeof(_lib.tk_tensor), "tk_requantize_attrs": ctypes.sizeof(_lib.tk_requantize_attrs),
+        "tk_conv2d_attrs": ctypes.sizeof(_lib.tk_conv2d_attrs), "tk_dense_attrs": ctypes.sizeof(_lib.tk_dense_attrs),
+        "tk_qnn_add_attrs": ctypes.sizeof(_lib.tk_qnn_add_attrs), "tk_pool2d_attrs": ctypes.sizeof(_lib.tk_pool2d_attrs),
+        "tk_node": ctypes.sizeof(_lib.tk_node), "tk_array_meta": ctypes.sizeof(_lib.tk_array_meta),
+        "tk_trace_header": 56,
+        "tk_tensor.shape": _lib.tk_tensor.shape.offset, "tk_tensor.byte_offset": _lib.tk_tensor.byte_offset.offset,
+        "tk_node.inputs": _lib.tk_node.inputs.offset, "tk_node.output": _lib.tk_node.output.offset,
+        "tk_node.ext": _lib.tk_node.ext.offset, "tk_node.attrs": _lib.tk_node.attrs.offset,
+        "tk_qnn_add_attrs.rhs": _lib.tk_qnn_add_attrs.rhs.offset,
+        "tk_qnn_add_attrs.lhs_upcast": _lib.tk_qnn_add_attrs.lhs_upcast.offset,
+        "tk_requantize_attrs.output_zero_point": _lib.tk_requantize_attrs.output_zero_point.offset,
+        "tk_conv2d_attrs.kernel_zero_points": _lib.tk_conv2d_attrs.kernel_zero_points.offset,
+        "tk_array_meta.dtype": _lib.tk_array_meta.dtype.offset,
+    }
+    for k, v in py.items():
+        assert int(got[k]) == v, (k, got[k], v)
+
+
+def test_fixed_point_multiplier_shift_matches_oracle():
+    lib = _lib.load()
+    rng = np.random.default_rng(0)
+    vals = list(rng.uniform(1e-6, 10, size=2000)) + [0.0, 1.0, 0.5, 0.25, 1 / 3, 2.0, 3.0, 1e-9,
+                                                      float(np.nextafter(1.0, 0.0)), 123456.789]
+    vals += list(np.float64(rng.uniform(1e-4, 1, size=500).astype(np.float32)) /
+                 np.float64(rng.uniform(1e-4, 1, size=500).astype(np.float32)))
+    m, s = ctypes.c_int32(), ctypes.c_int32()
+    for v in vals:
+        _lib.check(lib.tk_fixed_point_multiplier_shift(float(v), ctypes.byref(m), ctypes.byref(s)))
+        assert (m.value, s.value) == ref.get_fixed_point_multiplier_shift(float(v)), v
+
+
+def test_requantize_prepare_modes():
+    # equal scales skip FPM (requantize.cc:226); power of two → int32 path; per-axis always general
+    assert requantize_plan(np.float32(0.5), np.float32(0.5), "UPWARD")[0] == _lib.TK_RQ_IDENTITY
+    mode, ms, ss = requantize_plan(np.float32(1.0), np.float32(16.0), "UPWARD")
+    assert mode == _lib.TK_RQ_TENSOR_POW2 and ms[0] == 1 << 30 and ss[0] == -3
+    assert requantize_plan(np.float32(1.0), np.float32(16.0), "TONEAREST")[0] == _lib.TK_RQ_TENSOR_TONEAREST
+    assert requantize_plan(np.float32(1.0), np.float32(3.0), "UPWARD")[0] == _lib.TK_RQ_TENSOR_UPWARD
+    mode, ms, ss = requantize_plan(np.array([0.5, 0.5], np.float32), np.float32(0.5), "UPWARD")
+    assert mode == _lib.TK_RQ_AXIS_UPWARD and list(ms) == [1 << 30, 1 << 30] and list(ss) == [1, 1]
+    with pytest.raises(_lib.TachikomaError):
+        requantize_plan(np.float32(1e-30), np.float32(1.0), "UPWARD")  # shift out of range
+
+
+def test_no_gpu_needed_for_host_calls():
+    # loading the library and host-only calls must not require a visible GPU
+    lib = _lib.load()
+    assert lib.tk_last_error() is not None

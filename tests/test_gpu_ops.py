@@ -1,0 +1,182 @@
+"""Per-op parity through the C ABI on the MI355X vs the CPU oracle (bit-exact).
+
+Covers the reference's literal KATs (tests/golden/qnn_kats.json) and seeded random
+sweeps over the edge cases the reference tests: zero points (scalar / per-channel),
+uint8 operands, strides, padding, dilation, groups/depthwise, ragged K and M,
+saturation, per-axis requantize, both rounding modes.
+"""
+import numpy as np
+import pytest
+
+from oracle import qnn_ref as ref
+from tests.golden_util import load_array, load_cases, scale_const
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tk(device):
+    from tests import tk_gpu
+    return tk_gpu
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.requantize"), ids=lambda c: f"{c['name']}-{c['attrs']['rounding']}")
+def test_requantize_kat(tk, case):
+    a = case["attrs"]
+    x = load_array(case["inputs"]["data"])
+    out = tk.requantize(x, scale_const(a["input_scale"]), np.int32(a["input_zero_point"]), np.float32(a["output_scale"]),
+                        a["output_zero_point"], axis=a["axis"], rounding=a["rounding"], out_dtype=a["out_dtype"])
+    np.testing.assert_array_equal(out, load_array(case["expected"]))
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.dense"), ids=lambda c: c["name"])
+def test_dense_kat(tk, case):
+    a = case["attrs"]
+    out = tk.dense(load_array(case["inputs"]["data"]), load_array(case["inputs"]["weight"]), a["input_zero_point"],
+                   a["kernel_zero_point"])
+    if "bias" in case:
+        out = tk.bias_add(out, load_array(case["bias"]), axis=1)
+    if "requantize" in case:
+        r = case["requantize"]
+        out = tk.requantize(out, scale_const(r["input_scale"]), np.int32(0), np.float32(r["output_scale"]),
+                            r["output_zero_point"], axis=-1, out_dtype=r["out_dtype"])
+    np.testing.assert_array_equal(out, load_array(case["expected"]))
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.conv2d"), ids=lambda c: c["name"])
+def test_conv2d_kat(tk, case):
+    a = case["attrs"]
+    out = tk.conv2d(load_array(case["inputs"]["data"]), load_array(case["inputs"]["weight"]), a["input_zero_point"],
+                    a["kernel_zero_point"], strides=a["strides"], padding=a["padding"], dilation=a["dilation"],
+                    groups=a["groups"])
+    np.testing.assert_array_equal(out, load_array(case["expected"]))
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.add"), ids=lambda c: c["name"])
+def test_add_kat(tk, case):
+    a = case["attrs"]
+    out = tk.qnn_add(load_array(case["inputs"]["lhs"]), load_array(case["inputs"]["rhs"]), a["lhs_scale"],
+                     a["lhs_zero_point"], a["rhs_scale"], a["rhs_zero_point"], a["output_scale"],
+                     a["output_zero_point"])
+    np.testing.assert_array_equal(out, load_array(case["expected"]))
+
+
+def _rand(rng, shape, dtype):
+    info = np.iinfo(dtype)
+    return rng.integers(info.min, int(info.max) + 1, size=shape, dtype=np.int64).astype(dtype)
+
+
+CONV_CASES = [
+    # (N, C, H, W, O, K, stride, pad, dilation, groups, dtype_x, dtype_w, za, zw)
+    (2, 16, 9, 9, 32, 3, 1, 1, 1, 1, "int8", "int8", -3, 0),
+    (1, 3, 17, 19, 64, 7, 2, 3, 1, 1, "int8", "int8", 5, 0),        # stem: Cin 3 (channel padding)
+    (2, 64, 14, 14, 128, 1, 1, 0, 1, 1, "int8", "int8", 0, 0),      # 1x1
+    (2, 64, 15, 15, 128, 1, 2, 0, 1, 1, "int8", "int8", 7, 0),      # strided 1x1 (downsample)
+    (1, 24, 10, 11, 48, 3, 2, (0, 1, 1, 0), 1, 1, "int8", "int8", -8, 0),  # asymmetric pad
+    (1, 32, 12, 12, 40, 3, 1, 2, 2, 1, "int8", "int8", 2, 0),       # dilation, ragged Cout
+    (1, 32, 8, 8, 64, 3, 1, 1, 1, 1, "uint8", "uint8", 128, 127),   # uint8 both, zw != 0
+    (1, 20, 7, 7, 33, 3, 1, 1, 1, 1, "int8", "int8", 1, -2),        # zw != 0, ragged C and O
+    (2, 32, 10, 10, 32, 3, 1, 1, 1, 32, "int8", "int8", 3, 0),      # depthwise
+    (1, 32, 9, 9, 64, 3, 2, 1, 1, 4, "uint8", "int8", 100, 1),      # grouped, mixed dtypes
+    (1, 1, 28, 28, 6, 5, 1, 2, 1, 1, "int8", "int8", -4, 0),        # LeNet conv1 (direct path)
+    (3, 256, 7, 7, 512, 3, 1, 1, 1, 1, "int8", "int8", -1, 0),      # K = 2304, image-straddling tiles
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[f"conv{i}" for i in range(len(CONV_CASES))])
+def test_conv2d_random(tk, case):
+    n, c, h, w, o, k, s, p, d, g, dx, dw_, za, zw = case
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    x = _rand(rng, (n, c, h, w), dx)
+    wt = _rand(rng, (o, c // g, k, k), dw_)
+    pad = (p, p, p, p) if isinstance(p, int) else p
+    got = tk.conv2d(x, wt, za, zw, strides=(s, s), padding=pad, dilation=(d, d), groups=g)
+    exp = ref.qnn_conv2d(x, wt, za, zw, strides=(s, s), padding=pad, dilation=(d, d), groups=g)
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_conv2d_per_channel_kernel_zp(tk):
+    rng = np.random.default_rng(7)
+    x = _rand(rng, (2, 16, 8, 8), "int8")
+    w = _rand(rng, (48, 16, 3, 3), "int8")
+    zw = rng.integers(-5, 6, size=48).astype(np.int32)
+    got = tk.conv2d(x, w, 3, 0, padding=(1, 1, 1, 1), zw_vec=zw)
+    exp = ref.qnn_conv2d(x, w, 3, zw, padding=(1, 1, 1, 1))
+    np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("m,k,n,dx,dw_,za,zw", [
+    (128, 128, 128, "int8", "int8", -3, 0),
+    (1, 400, 120, "int8", "int8", 4, 0),
+    (64, 2048, 1000, "int8", "int8", -7, 0),
+    (5, 77, 13, "uint8", "uint8", 120, 131),
+    (130, 70, 129, "int8", "uint8", 0, 128),
+])
+def test_dense_random(tk, m, k, n, dx, dw_, za, zw):
+    rng = np.random.default_rng(m * 1000 + k)
+    x = _rand(rng, (m, k), dx)
+    w = _rand(rng, (n, k), dw_)
+    np.testing.assert_array_equal(tk.dense(x, w, za, zw), ref.qnn_dense(x, w, za, zw))
+
+
+@pytest.mark.parametrize("rounding", ["UPWARD", "TONEAREST"])
+@pytest.mark.parametrize("out_dtype", ["int8", "uint8", "int32"])
+def test_requantize_random(tk, rounding, out_dtype):
+    rng = np.random.default_rng(11)
+    x = rng.integers(-2**31, 2**31, size=(3, 17, 5, 7), dtype=np.int64).astype(np.int32)
+    x[0, 0, 0, :4] = [2**31 - 1, -2**31, 0, -1]
+    # per-axis scales incl. a power of two and an equal-to-output one
+    s_in = rng.uniform(1e-4, 2.0, size=17).astype(np.float32)
+    s_in[0] = 0.125
+    s_in[1] = 0.5
+    for axis_scale, s_out in ((s_in, np.float32(0.5)), (np.float32(0.0625), np.float32(1.0)),
+                              (np.float32(0.3), np.float32(0.7)), (np.float32(3.0), np.float32(1.5))):
+        got = tk.requantize(x, axis_scale, np.int32(3), s_out, -2, axis=1, rounding=rounding, out_dtype=out_dtype)
+        exp = ref.requantize(x, axis_scale, np.int32(3), s_out, np.int32(-2), axis=1, rounding=rounding,
+                             out_dtype=out_dtype)
+        np.testing.assert_array_equal(got, exp)
+
+
+def test_requantize_int8_input_and_vector_zp(tk):
+    rng = np.random.default_rng(5)
+    x = _rand(rng, (4, 6, 9), "int8")
+    zp = rng.integers(-10, 10, size=6).astype(np.int32)
+    s = rng.uniform(0.01, 0.1, size=6).astype(np.float32)
+    got = tk.requantize(x, s, zp, np.float32(0.05), 7, axis=1)
+    exp = ref.requantize(x, s, zp, np.float32(0.05), np.int32(7), axis=1)
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_qnn_add_random(tk):
+    rng = np.random.default_rng(3)
+    a = _rand(rng, (2, 64, 9, 9), "int8")
+    b = _rand(rng, (2, 64, 9, 9), "int8")
+    for params in ((0.05, 3, 0.07, -2, 0.09, 1), (0.05, 3, 0.05, 3, 0.05, 3), (0.125, 0, 0.5, 0, 0.25, -5)):
+        np.testing.assert_array_equal(tk.qnn_add(a, b, *params), ref.qnn_add(a, b, *params))
+
+
+def test_elementwise_random(tk):
+    rng = np.random.default_rng(9)
+    x32 = rng.integers(-2**31, 2**31, size=(3, 5, 7, 3), dtype=np.int64).astype(np.int32)
+    bias = rng.integers(-2**31, 2**31, size=(5,), dtype=np.int64).astype(np.int32)
+    np.testing.assert_array_equal(tk.bias_add(x32, bias, 1), ref.bias_add(x32, bias, 1))
+    x8 = _rand(rng, (2, 3, 33, 5), "int8")
+    np.testing.assert_array_equal(tk.unary("tk_clip", x8, None, -3, 100), ref.clip(x8, -3, 100))
+    for dst in ("int32", "uint8", "int16"):
+        np.testing.assert_array_equal(tk.unary("tk_cast", x32, dst), ref.cast(x32, dst))
+    np.testing.assert_array_equal(tk.unary("tk_cast", x8, "int32"), ref.cast(x8, "int32"))
+
+
+def test_pools(tk):
+    rng = np.random.default_rng(4)
+    x8 = _rand(rng, (2, 5, 13, 11), "int8")
+    np.testing.assert_array_equal(tk.pool("tk_max_pool2d", x8, (3, 3), (2, 2), (1, 1, 1, 1)),
+                                  ref.max_pool2d(x8, (3, 3), (2, 2), (1, 1, 1, 1)))
+    np.testing.assert_array_equal(tk.pool("tk_max_pool2d", x8, (2, 2), (2, 2), (0, 0, 0, 0)),
+                                  ref.max_pool2d(x8, (2, 2), (2, 2), (0, 0, 0, 0)))
+    x32 = rng.integers(-10**6, 10**6, size=(2, 5, 13, 11)).astype(np.int32)
+    for cip in (False, True):
+        np.testing.assert_array_equal(tk.pool("tk_avg_pool2d", x32, (3, 3), (2, 2), (1, 1, 1, 1), count_include_pad=cip),
+                                      ref.avg_pool2d(x32, (3, 3), (2, 2), (1, 1, 1, 1), count_include_pad=cip))
+    x32 = rng.integers(-10**6, 10**6, size=(3, 7, 7, 7)).astype(np.int32)
+    np.testing.assert_array_equal(tk.global_avg_pool(x32), ref.global_avg_pool2d(x32))
