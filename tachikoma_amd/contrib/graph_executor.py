@@ -42,6 +42,11 @@ class NDArrayView:
         return self._t
 
 
+def _as_bytes(t):
+    import torch
+    return t.reshape(-1).view(torch.uint8)
+
+
 class TraceCapture:
     """Pinned host image of one trace shard; device→host copies land at final offsets."""
 
@@ -58,15 +63,15 @@ class TraceCapture:
         self.layout.write_headers(self.ptr, self.layout.total)
         # params once, from the device copies
         for (name, shape, dtype), off in zip(params, self.layout.param_offsets):
-            self._host_view(off, shape, dtype).copy_(module.buffers[name].reshape(shape))
+            self._host_bytes(off, shape, dtype).copy_(_as_bytes(module.buffers[name]))
         self.record_offsets = dict(zip([r[0] for r in records], self.layout.record_offsets))
         self.host_dst = [None if name is None else self.ptr + self.record_offsets[name] for name in module.node_names]
         self.capture_stream = torch.cuda.Stream(device=module.device)
 
-    def _host_view(self, off: int, shape, dtype: str):
-        from ..relay.device_module import torch_dtype
+    def _host_bytes(self, off: int, shape, dtype: str):
+        """Byte view of a payload (NDArray-list payloads are not element-aligned)."""
         nbytes = int(np.prod(shape, dtype=np.int64)) * np.dtype(dtype).itemsize
-        return self.image[off:off + nbytes].view(torch_dtype(dtype)).view(tuple(shape))
+        return self.image[off:off + nbytes]
 
     def update_meta(self, **kw) -> None:
         self.meta.update(kw)
@@ -85,8 +90,8 @@ class TraceCapture:
         self.capture_stream.wait_stream(stream)
         with torch.cuda.stream(self.capture_stream):
             for t in self.module.plan.inputs:
-                self._host_view(self.record_offsets[t.name], t.shape, t.dtype).copy_(
-                    self.module.buffers[t.name], non_blocking=True)
+                self._host_bytes(self.record_offsets[t.name], t.shape, t.dtype).copy_(
+                    _as_bytes(self.module.buffers[t.name]), non_blocking=True)
 
     def synchronize(self) -> None:
         self.capture_stream.synchronize()
