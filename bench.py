@@ -26,6 +26,7 @@ if ROOT not in sys.path:
 import numpy as np  # noqa: E402
 
 INT8_MFMA_PEAK_OPS = 5.0e15  # gfx950 dense int8 (2x the 2.5 PF dense bf16 peak), MI355X_MICROARCH.md
+HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (6.3 TB/s measured streaming copy), MI355X_MICROARCH.md
 
 
 def _log(msg: str) -> None:
@@ -44,6 +45,7 @@ def parse():
     p.add_argument("--sink", choices=["memory", "file"], default="memory",
                    help="memory: trace image complete in pinned host RAM; file: also write each step to disk")
     p.add_argument("--out-dir", default="/tmp")
+    p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
     return p.parse_args()
 
 
@@ -102,6 +104,10 @@ def main():
             dist.barrier()
 
     def step(i):
+        if args.no_trace:
+            m.run(trace=False)
+            torch.cuda.synchronize(device)
+            return
         m.run(trace=True)
         cap.synchronize()
         if args.sink == "file":
@@ -139,25 +145,32 @@ def main():
     torch.cuda.synchronize(device)
     compute_ms = (time.perf_counter() - tc) / max(args.steps, 1) * 1e3
 
-    # ---- roofline of the dominant kernel family: the MFMA conv/dense contractions
-    names = m.module.node_names
-    conv_ops, conv_ms, n_launch = 0.0, 0.0, 0
-    for i, name in enumerate(names):
-        if name is None:
+    # ---- roofline of the dominant kernel: the fused MFMA conv/dense layer block
+    # (qnn.conv2d|dense -> bias_add -> requantize [-> clip] in one kernel).  It is bound by
+    # HBM: every op output of the block is a trace record that must be written
+    # (int32 conv + int32 bias_add + int8 requantize + int8 clip per output element).
+    blk_ops, blk_bytes, blk_ms, n_launch = 0.0, 0.0, 0.0, 0
+    ops_by_name = {o.name: o for o in m.plan.ops}
+    for i, recs in enumerate(m.module.node_records):
+        if not recs or m.module.node_kinds[i] not in ("conv_block", "dense_block", "qnn.conv2d", "qnn.dense"):
             continue
-        op = next(o for o in m.plan.ops if o.name == name)
-        if op.op in ("qnn.conv2d", "qnn.dense"):
-            w = m.plan.tensor(op.inputs[1])
-            if op.op == "qnn.conv2d":
-                o, cg, kh, kw = w.shape
-                nb, _, oh, ow = op.out.shape
-                macs = nb * o * oh * ow * cg * kh * kw
-            else:
-                macs = op.out.shape[0] * w.shape[0] * w.shape[1]
-            conv_ops += 2.0 * macs
-            conv_ms += node_ms[i]
-            n_launch += 1
-    achieved = conv_ops / (conv_ms * 1e-3) if conv_ms > 0 else 0.0
+        op = ops_by_name[recs[0]]
+        x = m.plan.tensor(op.inputs[0])
+        w = m.plan.tensor(op.inputs[1])
+        out_elems = int(np.prod(op.out.shape))
+        if op.op == "qnn.conv2d":
+            o, cg, kh, kw = w.shape
+            nb, _, oh, ow = op.out.shape
+            macs = nb * o * oh * ow * cg * kh * kw
+        else:
+            macs = op.out.shape[0] * w.shape[0] * w.shape[1]
+        rec_bytes = sum(ops_by_name[r].out.nbytes for r in recs)
+        blk_bytes += x.nbytes + w.nbytes + (4 * op.out.shape[1] if len(recs) > 1 else 0) + rec_bytes
+        blk_ops += 2.0 * macs
+        blk_ms += node_ms[i]
+        n_launch += 1
+    achieved_bw = blk_bytes / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
+    achieved_ops = blk_ops / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
     total_ms = float(node_ms.sum())
 
     # ---- optional trace-digest all-gather (RCCL over xGMI): one 8-byte digest per rank
@@ -195,11 +208,13 @@ def main():
                                    f"full per-op trace to pinned host memory",
                        "model": args.model, "global_batch": B * world, "samples_per_gpu": B, "seq_len": None,
                        "parallelism": f"batch-shard x{world}", "sink": args.sink},
-            "roofline": {"bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": INT8_MFMA_PEAK_OPS / 1e12,
-                         "unit": "TOPS", "frac": round(achieved / INT8_MFMA_PEAK_OPS, 4), "traffic": None,
-                         "kernel": "gemm_i8_kernel (MFMA i32_32x32x32_i8 implicit-GEMM conv/dense)",
-                         "launches_per_step": n_launch, "kernel_ms_per_step": round(conv_ms, 3),
-                         "ops_per_step": conv_ops},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_bw / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved_bw / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "gemm_i8_kernel<*,*,block> fused conv/dense layer block (v_mfma_i32_32x32x32_i8)",
+                         "launches_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
+                         "algorithmic_bytes_per_step": int(blk_bytes),
+                         "mfma_tops": round(achieved_ops / 1e12, 1),
+                         "mfma_frac": round(achieved_ops / INT8_MFMA_PEAK_OPS, 4)},
             "cpu_baseline": cpu,
             "extra": {
                 "compute_only_ms_per_step": round(compute_ms, 3),

@@ -143,6 +143,19 @@ typedef struct {
   int32_t rhs_upcast;
 } tk_qnn_add_attrs;
 
+/* A fused layer "block": qnn.conv2d|qnn.dense → nn.bias_add → qnn.requantize [→ clip].
+ * One kernel computes the contraction and writes EVERY op output of the chain from
+ * registers (each stays a separate trace record), so the int32 intermediates are never
+ * re-read from HBM.  Requantize/bias must run along the channel axis (NCHW axis 1 /
+ * dense units). */
+typedef struct {
+  tk_conv2d_attrs conv;         /* conv blocks */
+  tk_dense_attrs dense;         /* dense blocks */
+  tk_requantize_attrs requantize;
+  int32_t has_clip;
+  int64_t clip_min, clip_max;
+} tk_block_attrs;
+
 typedef struct {
   int32_t pool_size[2];
   int32_t strides[2];
@@ -177,10 +190,20 @@ int64_t tk_qnn_conv2d_workspace_bytes(const tk_tensor* data, const tk_tensor* we
 int tk_qnn_conv2d(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
                   const tk_conv2d_attrs* attrs, void* workspace, void* stream);
 
+/* Fused conv block: outs = {conv int32, bias_add int32, requantize int8/uint8, clip (if has_clip)}.
+ * `shadow_out` (optional): NHWC int8 copy of the block's last output, channels padded to
+ * 16, for a following MFMA conv (same layout as tk_nchw_to_nhwc_i8). */
+int tk_qnn_conv2d_block(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
+                        const int32_t* weight_sums, const tk_tensor* bias, tk_tensor* const* outs, int n_outs,
+                        const tk_block_attrs* attrs, void* patch_sums, void* shadow_out, void* stream);
+
 /* qnn.dense (src/relay/qnn/op/dense.cc:87-206). */
 int64_t tk_qnn_dense_workspace_bytes(const tk_tensor* data, const tk_tensor* weight);
 int tk_qnn_dense(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
                  const tk_dense_attrs* attrs, void* workspace, void* stream);
+/* Fused dense block (outs as for tk_qnn_conv2d_block). */
+int tk_qnn_dense_block(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,
+                       int n_outs, const tk_block_attrs* attrs, void* workspace, void* stream);
 
 int tk_requantize(const tk_tensor* data, tk_tensor* out, const tk_requantize_attrs* attrs, void* stream);
 int tk_qnn_add(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const tk_qnn_add_attrs* attrs,
@@ -216,20 +239,26 @@ enum {
   TK_NODE_GLOBAL_AVG_POOL2D = 10,
   TK_NODE_COPY = 11,       /* batch_flatten / reshape */
   TK_NODE_SHADOW = 12,     /* NCHW→NHWC int8 shadow for a conv input (not traced) */
+  TK_NODE_CONV_BLOCK = 13, /* in: data, weight, bias; outs: 3-4; ext: shadow, packed, weight_sums, patch_sums, shadow_out */
+  TK_NODE_DENSE_BLOCK = 14,/* in: data, weight, bias; outs: 3-4; ext: workspace */
 };
+
+#define TK_MAX_NODE_OUTPUTS 4
 
 typedef struct {
   int32_t kind;                 /* TK_NODE_* */
   int32_t n_inputs;
   const tk_tensor* inputs[3];
-  tk_tensor* output;
-  void* ext[4];                 /* kind-specific device pointers (see enum) */
+  int32_t n_outputs;            /* traced outputs (0 for SHADOW) */
+  tk_tensor* outputs[TK_MAX_NODE_OUTPUTS];
+  void* ext[5];                 /* kind-specific device pointers (see enum) */
   union {
     tk_conv2d_attrs conv2d;
     tk_dense_attrs dense;
     tk_requantize_attrs requantize;
     tk_qnn_add_attrs qnn_add;
     tk_pool2d_attrs pool2d;
+    tk_block_attrs block;
     struct { int64_t a_min, a_max; } clip;
     struct { int32_t axis; } bias_add;
   } attrs;
@@ -241,9 +270,10 @@ int tk_module_create(const tk_node* nodes, int n_nodes, tk_module** out);
 int tk_module_destroy(tk_module* mod);
 int tk_module_num_nodes(const tk_module* mod);
 /* Runs every node in order on `stream`.  If `capture_stream` and `host_dst`
- * are non-NULL, node i's output is copied device→host into host_dst[i]
- * (NULL entries are skipped) on capture_stream, each copy gated by an event
- * recorded after node i, so copies overlap the following nodes. */
+ * are non-NULL, output k of node i is copied device→host into
+ * host_dst[i * TK_MAX_NODE_OUTPUTS + k] (NULL entries are skipped) on
+ * capture_stream, the copies gated by an event recorded after node i, so they
+ * overlap the following nodes. */
 int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst);
 /* Runs nodes [begin, end) only (per-op record-and-run, Trace.calibrate analogue). */
 int tk_module_run_range(tk_module* mod, int begin, int end, void* stream);

@@ -85,6 +85,17 @@ class tk_qnn_add_attrs(ctypes.Structure):
     ]
 
 
+class tk_block_attrs(ctypes.Structure):
+    _fields_ = [
+        ("conv", tk_conv2d_attrs),
+        ("dense", tk_dense_attrs),
+        ("requantize", tk_requantize_attrs),
+        ("has_clip", ctypes.c_int32),
+        ("clip_min", ctypes.c_int64),
+        ("clip_max", ctypes.c_int64),
+    ]
+
+
 class tk_pool2d_attrs(ctypes.Structure):
     _fields_ = [
         ("pool_size", ctypes.c_int32 * 2),
@@ -110,6 +121,7 @@ class tk_node_attrs(ctypes.Union):
         ("requantize", tk_requantize_attrs),
         ("qnn_add", tk_qnn_add_attrs),
         ("pool2d", tk_pool2d_attrs),
+        ("block", tk_block_attrs),
         ("clip", _clip),
         ("bias_add", _bias_add),
     ]
@@ -120,8 +132,9 @@ class tk_node(ctypes.Structure):
         ("kind", ctypes.c_int32),
         ("n_inputs", ctypes.c_int32),
         ("inputs", ctypes.POINTER(tk_tensor) * 3),
-        ("output", ctypes.POINTER(tk_tensor)),
-        ("ext", ctypes.c_void_p * 4),
+        ("n_outputs", ctypes.c_int32),
+        ("outputs", ctypes.POINTER(tk_tensor) * 4),
+        ("ext", ctypes.c_void_p * 5),
         ("attrs", tk_node_attrs),
     ]
 
@@ -144,7 +157,9 @@ TK_ROUND_UPWARD, TK_ROUND_TONEAREST = 0, 1
 NODE_KINDS = {
     "qnn.conv2d": 1, "qnn.dense": 2, "qnn.requantize": 3, "nn.bias_add": 4, "clip": 5, "cast": 6,
     "qnn.add": 7, "nn.max_pool2d": 8, "nn.avg_pool2d": 9, "nn.global_avg_pool2d": 10, "copy": 11, "shadow": 12,
+    "conv_block": 13, "dense_block": 14,
 }
+MAX_NODE_OUTPUTS = 4
 
 # Every symbol declared in include/tachikoma.h, with its ctypes signature.
 _VP, _I32, _I64, _F32, _F64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double
@@ -166,6 +181,10 @@ SIGNATURES = {
     "tk_qnn_conv2d": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_conv2d_attrs), _VP, _VP]),
     "tk_qnn_dense_workspace_bytes": (_I64, [_PT, _PT]),
     "tk_qnn_dense": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_dense_attrs), _VP, _VP]),
+    "tk_qnn_conv2d_block": (ctypes.c_int, [_PT, _VP, _PT, _VP, _VP, _PT, ctypes.POINTER(_PT), ctypes.c_int,
+                                           ctypes.POINTER(tk_block_attrs), _VP, _VP, _VP]),
+    "tk_qnn_dense_block": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(_PT), ctypes.c_int,
+                                          ctypes.POINTER(tk_block_attrs), _VP, _VP]),
     "tk_requantize": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_requantize_attrs), _VP]),
     "tk_qnn_add": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_qnn_add_attrs), _VP]),
     "tk_bias_add": (ctypes.c_int, [_PT, _PT, _PT, ctypes.c_int, _VP]),

@@ -65,7 +65,7 @@ class TraceCapture:
         for (name, shape, dtype), off in zip(params, self.layout.param_offsets):
             self._host_bytes(off, shape, dtype).copy_(_as_bytes(module.buffers[name]))
         self.record_offsets = dict(zip([r[0] for r in records], self.layout.record_offsets))
-        self.host_dst = [None if name is None else self.ptr + self.record_offsets[name] for name in module.node_names]
+        self.host_dst = module.host_dst_array({n: self.ptr + off for n, off in self.record_offsets.items()})
         self.capture_stream = torch.cuda.Stream(device=module.device)
 
     def _host_bytes(self, off: int, shape, dtype: str):

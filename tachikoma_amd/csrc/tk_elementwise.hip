@@ -68,32 +68,7 @@ struct AxisWalker {
 };
 
 // ---------------------------------------------------------------- requantize
-// RequantizeLowerInt (src/relay/qnn/op/requantize.cc:195-273):
-//   t = int32(x) - zp_in;  t = FPM(t);  t = zp_out + t;  clip+cast unless out is int32.
-struct RqParams {
-  int32_t mode, multiplier, shift, zp_in, zp_out;
-  const int32_t* ms;
-  const int32_t* ss;
-  const int32_t* zps;
-  int32_t inner, C;
-  int64_t qmin, qmax;
-  int32_t clip_out;
-};
-
-__device__ __forceinline__ int32_t rq_apply(int32_t t, int c, const RqParams& p) {
-  int32_t zp = p.zps ? p.zps[c] : p.zp_in;
-  t = (int32_t)((uint32_t)t - (uint32_t)zp);
-  switch (p.mode) {
-    case TK_RQ_IDENTITY: break;
-    case TK_RQ_TENSOR_POW2: t = qms_pow2(t, p.shift); break;
-    case TK_RQ_TENSOR_UPWARD: t = qms_upward(t, p.multiplier, p.shift); break;
-    case TK_RQ_TENSOR_TONEAREST: t = qms_tonearest(t, p.multiplier, p.shift); break;
-    case TK_RQ_AXIS_UPWARD: t = qms_upward(t, p.ms[c], p.ss[c]); break;
-    case TK_RQ_AXIS_TONEAREST: t = qms_tonearest(t, p.ms[c], p.ss[c]); break;
-  }
-  t = (int32_t)((uint32_t)p.zp_out + (uint32_t)t);
-  return t;
-}
+// (RqParams / rq_apply live in tk_common.h: the fused conv epilogue uses them too)
 
 template <typename Tin, typename Tout, int VEC>
 __global__ __launch_bounds__(kBlock) void requantize_kernel(const Tin* __restrict__ x, Tout* __restrict__ y,

@@ -16,6 +16,7 @@
 // The epilogue writes int32 NCHW directly (lanes run along pixels: coalesced).
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 
 #include "tk_common.h"
@@ -27,6 +28,8 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 
 constexpr int kBK = 64;          // bytes of K per stage
 constexpr int kGemmThreads = 256;
+constexpr int kEpiRows = 32;     // epilogue chunk: 32 rows x 128 columns of int32 in LDS
+constexpr int kEpiStride = 132;  // dwords per LDS row (128 + 4: breaks the 64-bank period)
 
 struct GemmArgs {
   const int8_t* A;     // [rowsA_pad][lda]
@@ -49,19 +52,57 @@ struct GemmArgs {
   // output addressing
   int32_t out_nchw;    // 1: C[(p/HW)*M*HW + i*HW + p%HW]; 0: C[i*N + j]
   int32_t ldc;         // row-major pitch (elements) when !out_nchw
+  // fused block epilogue (bias_add -> requantize -> clip), see BlockEpi
+  int32_t* bias_out;
+  uint8_t* rq_out;
+  uint8_t* clip_out;
+  uint8_t* shadow_out;  // NHWC copy of the last output (conv blocks), channels padded to shadow_cpad
+  const int32_t* bias;
+  RqParams rq;
+  int32_t has_clip, clip_lo, clip_hi, shadow_cpad;
+  uint32_t shadow_xor;  // 0x80 when the block output is uint8 (shadow stores int8 = u8 ^ 0x80)
+  int32_t ch_is_row;    // channel index = row (conv: Cout) or column (dense: units)
+  int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue
 };
+
+// Writes one element of every output of a fused block.  Mirrors, per element:
+// nn.bias_add (int32 wrap), RequantizeLowerInt + clip/cast to the out dtype
+// (src/relay/qnn/op/requantize.cc:195-273), then clip (python/tvm/topi/math.py:615-640).
+template <bool kBlock>
+__device__ __forceinline__ void epilogue_store(const GemmArgs& g, int64_t off, int ch, int64_t pix, uint32_t v) {
+  g.C[off] = (int32_t)v;
+  if (!kBlock) return;
+  int32_t b = (int32_t)(v + (uint32_t)g.bias[ch]);
+  g.bias_out[off] = b;
+  int32_t q = rq_apply(b, ch, g.rq);
+  q = (int32_t)min(max((int64_t)q, g.rq.qmin), g.rq.qmax);
+  g.rq_out[off] = (uint8_t)q;
+  int32_t last = q;
+  if (g.has_clip) {
+    last = min(max(q, g.clip_lo), g.clip_hi);
+    g.clip_out[off] = (uint8_t)last;
+  }
+  if (g.shadow_out) g.shadow_out[pix * g.shadow_cpad + ch] = (uint8_t)((uint32_t)last ^ g.shadow_xor);
+}
+
+// Workgroup barrier that only drains this wave's LDS traffic.  __syncthreads() also waits
+// vmcnt(0), i.e. for every outstanding global store of the epilogue to complete, which
+// serialises the store latency once per barrier; the epilogue's barriers only order LDS.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // LDS tile [rows][64 B], 16-byte chunk c of row r stored at chunk c ^ ((r >> 2) & 3):
 // the 16-lane groups of ds_read_b128 then hit 16 distinct bank slots.
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * kBK + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int MT, bool kIm2col>
+template <int MT, bool kIm2col, bool kBlock>
 __global__ __launch_bounds__(kGemmThreads) void gemm_i8_kernel(GemmArgs g) {
   constexpr int BM = 64 * MT;   // rows of A per block (2 waves along M, MT 32-row tiles each)
   constexpr int BN = 128;       // rows of B per block (2 waves along N, 2 32-col tiles each)
   constexpr int A_CHUNKS = BM * kBK / 16 / kGemmThreads;  // 16-byte loads per thread per stage
   constexpr int B_CHUNKS = BN * kBK / 16 / kGemmThreads;
-  __shared__ __attribute__((aligned(16))) int8_t smem[2 * (BM + BN) * kBK];
+  constexpr int kStage = 2 * (BM + BN) * kBK;
+  constexpr int kEpi = kEpiRows * kEpiStride * 4;
+  __shared__ __attribute__((aligned(16))) int8_t smem[kStage > kEpi ? kStage : kEpi];
   int8_t* As = smem;
   int8_t* Bs = smem + 2 * BM * kBK;
 
@@ -188,36 +229,203 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_i8_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  // ---- epilogue: zero-point folding + store
+  // ---- epilogue, staged through LDS 32 rows at a time:
+  //  (1) the two waves owning the chunk dump their raw accumulators to LDS [row][col]
+  //      (no loads, no branches: everything per-row/per-column happens in (2));
+  //  (2) every thread takes 4 consecutive columns of one row: zero-point folding, then
+  //      16-byte int32 stores for the conv / bias_add records and 4-byte stores for
+  //      requantize / clip (NCHW: consecutive pixels of one channel are contiguous); it
+  //      overwrites its LDS slot with the block's final int8 values;
+  //  (3) the NHWC shadow for the next conv: each thread gathers 16 channels of one pixel
+  //      (a wave reads 64 consecutive columns per row: conflict-free) into one 16-byte store.
+  // Per-row constants are loaded at the top of each chunk (latency hidden by (1)); all
+  // optional operands are guarded by uniform flags so the waitcnt pass sees straight code.
+  if (g.ablate & 4) return;
+  lds_barrier();  // staging buffers are free
+  int32_t* tileI = reinterpret_cast<int32_t*>(smem);
   const int hw = g.OH * g.OW;
+  const bool has_ra = g.RA != nullptr, has_rb = g.RB != nullptr;
+  const bool za_vec = g.zA_vec != nullptr, zb_vec = g.zB_vec != nullptr;
+  const uint32_t keff = (uint32_t)g.k_eff;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn * 64 + j * 32 + (lane & 31);
-    if (col >= g.N) continue;
-    const uint32_t zb = g.zB_vec ? (uint32_t)g.zB_vec[col] : (uint32_t)g.zB;
-    const uint32_t rbj = g.RB ? (uint32_t)g.RB[col] : 0u;
-    int64_t base;
-    if (g.out_nchw) {
-      int img = col / hw;
-      int pix = col - img * hw;
-      base = (int64_t)img * g.M * hw + pix;
-    } else {
-      base = col;
-    }
+  for (int c = 0; c < MT * 2; ++c) {
+    // per-row constants of the 4 rows this thread processes in this chunk
+    uint32_t kra[4], kza[4];
+    int32_t kb[4], km[4], ks[4], kz[4];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 32 * MT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= g.M) continue;
-        const uint32_t za = g.zA_vec ? (uint32_t)g.zA_vec[row] : (uint32_t)g.zA;
-        const uint32_t rai = g.RA ? (uint32_t)g.RA[row] : 0u;
-        uint32_t v = (uint32_t)acc[i][j][r];
-        v = v - zb * rai - za * rbj + (uint32_t)g.k_eff * za * zb;
-        int64_t off = g.out_nchw ? base + (int64_t)row * hw : (int64_t)row * g.ldc + base;
-        g.C[off] = (int32_t)v;
+    for (int k = 0; k < 4; ++k) {
+      const int row = m0 + c * 32 + ((tid + kGemmThreads * k) >> 5);
+      const int rowc = row < g.M ? row : 0;
+      kra[k] = has_ra ? (uint32_t)g.RA[rowc] : 0u;
+      kza[k] = za_vec ? (uint32_t)g.zA_vec[rowc] : (uint32_t)g.zA;
+      kb[k] = km[k] = ks[k] = kz[k] = 0;
+      if (kBlock && g.ch_is_row) {
+        kb[k] = g.bias[rowc];
+        const bool axis = g.rq.mode >= TK_RQ_AXIS_UPWARD;
+        km[k] = axis ? g.rq.ms[rowc] : g.rq.multiplier;
+        ks[k] = axis ? g.rq.ss[rowc] : g.rq.shift;
+        kz[k] = g.rq.zps ? g.rq.zps[rowc] : g.rq.zp_in;
       }
     }
+    if (wm == c / MT) {
+      const int i = c % MT;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int lc = wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lr = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          tileI[lr * kEpiStride + lc] = acc[i][j][r];
+        }
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int item = tid + kGemmThreads * k;
+      const int lr = item >> 5;
+      const int lc4 = (item & 31) * 4;
+      const int row = m0 + c * 32 + lr;
+      const int col0 = n0 + lc4;
+      if (row >= g.M || col0 >= g.N) continue;
+      const bool full = col0 + 3 < g.N;
+      v4i vv = *reinterpret_cast<const v4i*>(tileI + lr * kEpiStride + lc4);
+      // zero-point folding: acc - zB[col]*RA[row] - zA[row]*RB[col] + K*zA[row]*zB[col]
+      uint32_t zb[4], rb[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int colq = full ? col0 + q : min(col0 + q, g.N - 1);
+        zb[q] = zb_vec ? (uint32_t)g.zB_vec[colq] : (uint32_t)g.zB;
+        rb[q] = has_rb ? (uint32_t)g.RB[colq] : 0u;
+      }
+      int32_t conv[4];
+      {
+        const int32_t a4[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          conv[q] = (int32_t)((uint32_t)a4[q] - zb[q] * kra[k] - kza[k] * rb[q] + keff * kza[k] * zb[q]);
+      }
+      vv = v4i{conv[0], conv[1], conv[2], conv[3]};
+      // output offsets of the 4 elements
+      int64_t off0;
+      bool vec = full;
+      if (g.out_nchw) {
+        const int img = col0 / hw;
+        const int pix = col0 - img * hw;
+        off0 = ((int64_t)img * g.M + row) * hw + pix;
+        vec = vec && (pix + 3 < hw) && ((off0 & 3) == 0);
+      } else {
+        off0 = (int64_t)row * g.ldc + col0;
+        vec = vec && ((off0 & 3) == 0);
+      }
+      if (!kBlock) {
+        if (vec) {
+          *reinterpret_cast<v4i*>(g.C + off0) = vv;
+        } else {
+          for (int q = 0; q < 4 && col0 + q < g.N; ++q) {
+            const int col = col0 + q;
+            int64_t off = off0 + q;
+            if (g.out_nchw) {
+              const int img = col / hw;
+              off = ((int64_t)img * g.M + row) * hw + (col - img * hw);
+            }
+            g.C[off] = conv[q];
+          }
+        }
+        continue;
+      }
+      int32_t badd[4], rqv[4], last[4];
+      if (g.ch_is_row) {
+        // one channel for the 4 elements: constants from registers, mode branch hoisted
+        const int32_t bch = kb[k], mch = km[k], sch = ks[k], zch = kz[k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) badd[q] = (int32_t)((uint32_t)conv[q] + (uint32_t)bch);
+        const int mode = g.rq.mode;
+        if (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rqv[q] = qms_upward((int32_t)((uint32_t)badd[q] - (uint32_t)zch), mch, sch);
+        } else if (mode == TK_RQ_TENSOR_POW2) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rqv[q] = qms_pow2((int32_t)((uint32_t)badd[q] - (uint32_t)zch), sch);
+        } else if (mode == TK_RQ_IDENTITY) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rqv[q] = (int32_t)((uint32_t)badd[q] - (uint32_t)zch);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rqv[q] = qms_tonearest((int32_t)((uint32_t)badd[q] - (uint32_t)zch), mch, sch);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          int32_t t = (int32_t)((uint32_t)g.rq.zp_out + (uint32_t)rqv[q]);
+          t = (int32_t)min(max((int64_t)t, g.rq.qmin), g.rq.qmax);
+          rqv[q] = t;
+          last[q] = g.has_clip ? min(max(t, g.clip_lo), g.clip_hi) : t;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ch = full ? col0 + q : min(col0 + q, g.N - 1);
+          badd[q] = (int32_t)((uint32_t)conv[q] + (uint32_t)g.bias[ch]);
+          int32_t t = rq_apply(badd[q], ch, g.rq);
+          t = (int32_t)min(max((int64_t)t, g.rq.qmin), g.rq.qmax);
+          rqv[q] = t;
+          last[q] = g.has_clip ? min(max(t, g.clip_lo), g.clip_hi) : t;
+        }
+      }
+      if (g.shadow_out)
+        *reinterpret_cast<v4i*>(tileI + lr * kEpiStride + lc4) = v4i{last[0], last[1], last[2], last[3]};
+      if (g.ablate & 2) {
+        if (badd[0] == 0x7fffffff && rqv[0] == 3 && last[0] == 5) g.C[0] = 1;  // keep values live
+      } else if (vec) {
+        *reinterpret_cast<v4i*>(g.C + off0) = vv;
+        *reinterpret_cast<v4i*>(g.bias_out + off0) = v4i{badd[0], badd[1], badd[2], badd[3]};
+        uint32_t pr = (rqv[0] & 0xFF) | ((rqv[1] & 0xFF) << 8) | ((rqv[2] & 0xFF) << 16) | ((uint32_t)rqv[3] << 24);
+        *reinterpret_cast<uint32_t*>(g.rq_out + off0) = pr;
+        if (g.has_clip) {
+          uint32_t pc = (last[0] & 0xFF) | ((last[1] & 0xFF) << 8) | ((last[2] & 0xFF) << 16) |
+                        ((uint32_t)last[3] << 24);
+          *reinterpret_cast<uint32_t*>(g.clip_out + off0) = pc;
+        }
+      } else {
+        for (int q = 0; q < 4 && col0 + q < g.N; ++q) {
+          const int col = col0 + q;
+          int64_t off = off0 + q;
+          if (g.out_nchw) {
+            const int img = col / hw;
+            off = ((int64_t)img * g.M + row) * hw + (col - img * hw);
+          }
+          g.C[off] = conv[q];
+          g.bias_out[off] = badd[q];
+          g.rq_out[off] = (uint8_t)rqv[q];
+          if (g.has_clip) g.clip_out[off] = (uint8_t)last[q];
+        }
+      }
+    }
+    if (kBlock && g.shadow_out && !(g.ablate & 1)) {
+      lds_barrier();
+      const int lc = tid & 127;
+      const int half = tid >> 7;
+      const int col = n0 + lc;
+      const int ch0 = m0 + c * 32 + half * 16;
+      if (col < g.N && ch0 < g.shadow_cpad) {
+        uint32_t w[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          uint32_t word = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int ch = ch0 + d * 4 + q;
+            uint32_t b = (uint32_t)tileI[(half * 16 + d * 4 + q) * kEpiStride + lc] ^ g.shadow_xor;
+            if (ch >= g.M) b = 0;  // padded channels of a partial group stay zero
+            word |= (b & 0xFFu) << (8 * q);
+          }
+          w[d] = word;
+        }
+        *reinterpret_cast<v4i*>(g.shadow_out + (int64_t)col * g.shadow_cpad + ch0) =
+            v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+      }
+    }
+    lds_barrier();
   }
 }
 
@@ -334,12 +542,12 @@ __global__ __launch_bounds__(256) void patch_sum_kernel(const int8_t* __restrict
 
 // Direct (VALU) grouped / depthwise / tiny-channel convolution on NCHW int8/uint8.
 // out[n][o][oh][ow] = Σ_{c in group(o), r, s} (a - za)(w - zw[o]); padded taps contribute 0.
-template <typename Tx, typename Tw>
+template <typename Tx, typename Tw, bool kBlock>
 __global__ __launch_bounds__(256) void direct_conv_kernel(const Tx* __restrict__ x, const Tw* __restrict__ w,
-                                                          int32_t* __restrict__ y, int N, int C, int H, int W, int O,
+                                                          int N, int C, int H, int W, int O,
                                                           int OH, int OW, int KH, int KW, int sh, int sw, int pt, int pl,
                                                           int dh, int dw, int groups, int32_t za, int32_t zw,
-                                                          const int32_t* __restrict__ zw_vec) {
+                                                          const int32_t* __restrict__ zw_vec, GemmArgs g) {
   int64_t total = (int64_t)N * O * OH * OW;
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int cg = C / groups, og = O / groups;
@@ -350,11 +558,11 @@ __global__ __launch_bounds__(256) void direct_conv_kernel(const Tx* __restrict__
     t /= OH;
     int o = (int)(t % O);
     int n = (int)(t / O);
-    int g = o / og;
+    int grp = o / og;
     int32_t zwo = zw_vec ? zw_vec[o] : zw;
     uint32_t acc = 0;
     for (int c = 0; c < cg; ++c) {
-      int ci = g * cg + c;
+      int ci = grp * cg + c;
       const Tx* plane = x + ((int64_t)n * C + ci) * H * W;
       const Tw* wk = w + (((int64_t)o * cg + c) * KH) * KW;
       for (int r = 0; r < KH; ++r) {
@@ -369,7 +577,8 @@ __global__ __launch_bounds__(256) void direct_conv_kernel(const Tx* __restrict__
         }
       }
     }
-    y[i] = (int32_t)acc;
+    int64_t pix = (int64_t)n * OH * OW + (int64_t)oh * OW + ow;
+    epilogue_store<kBlock>(g, i, o, pix, acc);
   }
 }
 
@@ -450,9 +659,78 @@ static inline uint32_t rep4(int v) {
   return b | (b << 8) | (b << 16) | (b << 24);
 }
 
-int conv2d_prepared_impl(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
-                         const int32_t* sums, tk_tensor* out, const tk_conv2d_attrs* a, void* workspace_patch,
-                         hipStream_t s) {
+// Block outputs (NULL `b` = plain conv/dense writing only the int32 contraction).
+struct BlockIO {
+  const tk_tensor* bias;
+  tk_tensor* const* outs;  // conv, bias_add, requantize, [clip]
+  int n_outs;
+  const tk_block_attrs* attrs;
+  void* shadow_out;
+};
+
+// Validates a fused block and fills the epilogue part of GemmArgs.
+static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out, int channels, int ch_axis) {
+  if (!b) return TK_OK;
+  const tk_block_attrs* at = b->attrs;
+  TK_CHECK_ARG(at && b->outs && b->bias && (b->n_outs == 3 || b->n_outs == 4), "block needs bias, attrs, 3-4 outs");
+  TK_CHECK_ARG((b->n_outs == 4) == (at->has_clip != 0), "clip output count mismatch");
+  TK_CHECK_ARG(is_int(b->bias, 32) && numel(b->bias) == channels, "bias must be int32 [channels]");
+  const tk_tensor* bo = b->outs[1];
+  const tk_tensor* rq = b->outs[2];
+  TK_CHECK_ARG(is_int(bo, 32) && numel(bo) == numel(conv_out), "bias_add output must be int32, conv shaped");
+  TK_CHECK_ARG(is_int8ish(rq) && numel(rq) == numel(conv_out), "requantize output must be int8/uint8, conv shaped");
+  int rq_axis = at->requantize.axis;
+  TK_CHECK_ARG(rq_axis == ch_axis || at->requantize.mode <= TK_RQ_TENSOR_TONEAREST,
+               "requantize must run along the channel axis to fuse");
+  if (b->n_outs == 4) {
+    TK_CHECK_ARG(b->outs[3]->dtype.code == rq->dtype.code && b->outs[3]->dtype.bits == 8 &&
+                     numel(b->outs[3]) == numel(conv_out),
+                 "clip output must match the requantize output");
+  }
+  ga.bias = (const int32_t*)ptr(b->bias);
+  ga.bias_out = (int32_t*)ptr(bo);
+  ga.rq_out = (uint8_t*)ptr(rq);
+  ga.clip_out = b->n_outs == 4 ? (uint8_t*)ptr(b->outs[3]) : nullptr;
+  ga.has_clip = at->has_clip;
+  bool u8 = is_uint(rq, 8);
+  int64_t lo = u8 ? 0 : -128, hi = u8 ? 255 : 127;
+  ga.clip_lo = (int32_t)std::max(at->clip_min, lo);
+  ga.clip_hi = (int32_t)std::min(at->clip_max, hi);
+  RqParams& p = ga.rq;
+  p.mode = at->requantize.mode;
+  p.multiplier = at->requantize.multiplier;
+  p.shift = at->requantize.shift;
+  p.zp_in = at->requantize.input_zero_point;
+  p.zp_out = at->requantize.output_zero_point;
+  p.ms = at->requantize.multipliers;
+  p.ss = at->requantize.shifts;
+  p.zps = at->requantize.input_zero_points;
+  p.inner = 1;
+  p.C = channels;
+  p.qmin = lo;
+  p.qmax = hi;
+  p.clip_out = 1;
+  if ((p.mode == TK_RQ_AXIS_UPWARD || p.mode == TK_RQ_AXIS_TONEAREST) && (!p.ms || !p.ss)) {
+    set_error("block: per-axis requantize needs device multipliers/shifts");
+    return TK_ERR_INVALID_ARG;
+  }
+  ga.shadow_out = (uint8_t*)b->shadow_out;
+  ga.shadow_cpad = (channels + 15) / 16 * 16;
+  ga.shadow_xor = u8 ? 0x80u : 0u;
+  return TK_OK;
+}
+
+static int ablate_flags() {
+  static int v = [] {
+    const char* e = getenv("TK_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
+                      const int32_t* sums, tk_tensor* out, const tk_conv2d_attrs* a, void* workspace_patch,
+                      const BlockIO* blk, hipStream_t s) {
   TK_CHECK_ARG(data && weight && out && a, "null argument");
   TK_CHECK_ARG(is_int8ish(data) && is_int8ish(weight) && is_int(out, 32), "dtypes: int8/uint8 in, int32 out");
   ConvGeom g;
@@ -466,20 +744,33 @@ int conv2d_prepared_impl(const tk_tensor* data, const void* shadow, const tk_ten
   TK_CHECK_ARG(a->strides[0] > 0 && a->strides[1] > 0 && a->dilation[0] > 0 && a->dilation[1] > 0, "bad strides");
   int64_t P = (int64_t)g.N * g.OH * g.OW;
   TK_CHECK_ARG(P < INT32_MAX && (int64_t)g.N * g.O * g.OH * g.OW < INT32_MAX * 2LL, "tensor too large");
+  GemmArgs ga{};
+  ga.C = (int32_t*)ptr(out);
+  ga.M = g.O;
+  ga.N = (int32_t)P;
+  ga.OH = g.OH;
+  ga.OW = g.OW;
+  ga.ch_is_row = 1;
+  ga.ablate = ablate_flags();
+  int rc = setup_block(ga, blk, out, g.O, 1);
+  if (rc) return rc;
   if (!use_mfma_conv(g, a->groups)) {
     // grouped / depthwise / tiny channel counts: direct VALU kernel on NCHW
     int64_t total = (int64_t)g.N * g.O * g.OH * g.OW;
     int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
-#define TK_DIRECT(TX, TW)                                                                                      \
-  hipLaunchKernelGGL((direct_conv_kernel<TX, TW>), dim3(grid), dim3(256), 0, s, (const TX*)ptr(data),               \
-                     (const TW*)ptr(weight), (int32_t*)ptr(out), g.N, g.C, g.H, g.W, g.O, g.OH, g.OW, g.KH, g.KW,    \
-                     a->strides[0], a->strides[1], a->padding[0], a->padding[1], a->dilation[0], a->dilation[1],     \
-                     a->groups, a->input_zero_point, a->kernel_zero_point, a->kernel_zero_points)
+#define TK_DIRECT(TX, TW, BLK)                                                                                   \
+  hipLaunchKernelGGL((direct_conv_kernel<TX, TW, BLK>), dim3(grid), dim3(256), 0, s, (const TX*)ptr(data),        \
+                     (const TW*)ptr(weight), g.N, g.C, g.H, g.W, g.O, g.OH, g.OW, g.KH, g.KW, a->strides[0],          \
+                     a->strides[1], a->padding[0], a->padding[1], a->dilation[0], a->dilation[1], a->groups,         \
+                     a->input_zero_point, a->kernel_zero_point, a->kernel_zero_points, ga)
+#define TK_DIRECT_B(TX, TW) \
+  if (blk) TK_DIRECT(TX, TW, true); else TK_DIRECT(TX, TW, false)
     bool du = is_uint(data, 8), wu = is_uint(weight, 8);
-    if (du && wu) TK_DIRECT(uint8_t, uint8_t);
-    else if (du) TK_DIRECT(uint8_t, int8_t);
-    else if (wu) TK_DIRECT(int8_t, uint8_t);
-    else TK_DIRECT(int8_t, int8_t);
+    if (du && wu) { TK_DIRECT_B(uint8_t, uint8_t); }
+    else if (du) { TK_DIRECT_B(uint8_t, int8_t); }
+    else if (wu) { TK_DIRECT_B(int8_t, uint8_t); }
+    else { TK_DIRECT_B(int8_t, int8_t); }
+#undef TK_DIRECT_B
 #undef TK_DIRECT
     TK_LAUNCH_CHECK();
     return TK_OK;
@@ -489,30 +780,22 @@ int conv2d_prepared_impl(const tk_tensor* data, const void* shadow, const tk_ten
   TK_CHECK_ARG(!(wu && a->kernel_zero_points), "per-channel zero points with uint8 weights are not supported");
   int32_t za = a->input_zero_point - (du ? 128 : 0);
   int32_t zw = a->kernel_zero_point - (wu ? 128 : 0);
-  GemmArgs ga{};
   ga.A = (const int8_t*)packed;
   ga.B = (const int8_t*)shadow;
-  ga.C = (int32_t*)ptr(out);
-  ga.M = g.O;
-  ga.N = (int32_t)P;
   ga.lda = g.k_pad;
   ga.ldb = g.cin_pad;
   ga.k_pad = g.k_pad;
   ga.k_eff = g.k_eff;
   // operand A = weights (zero point zw), operand B = activations (zero point za)
   ga.zA = zw;
-  ga.zA_vec = nullptr;
   ga.zB = za;
-  ga.zB_vec = nullptr;
   ga.RA = sums;
-  ga.RB = nullptr;
   ga.H = g.H; ga.W = g.W; ga.cin_pad = g.cin_pad; ga.KH = g.KH; ga.KW = g.KW;
   ga.sh = a->strides[0]; ga.sw = a->strides[1]; ga.pt = a->padding[0]; ga.pl = a->padding[1];
-  ga.dh = a->dilation[0]; ga.dw = a->dilation[1]; ga.OH = g.OH; ga.OW = g.OW;
+  ga.dh = a->dilation[0]; ga.dw = a->dilation[1];
   ga.taps = g.KH * g.KW;
   ga.fill = rep4(za);
   ga.out_nchw = 1;
-  ga.ldc = 0;
   if (zw != 0 || a->kernel_zero_points) {
     TK_CHECK_ARG(workspace_patch, "non-zero kernel zero point needs a patch-sum workspace");
     int32_t* ps = (int32_t*)workspace_patch;
@@ -523,14 +806,30 @@ int conv2d_prepared_impl(const tk_tensor* data, const void* shadow, const tk_ten
     ga.zA_vec = a->kernel_zero_points;
   }
   dim3 grid((unsigned)((P + 127) / 128), (unsigned)((g.O + 127) / 128));
-  if (g.O <= 64) {
+#define TK_GEMM(MT, BLK) hipLaunchKernelGGL((gemm_i8_kernel<MT, true, BLK>), grid, dim3(kGemmThreads), 0, s, ga)
+  if (g.O <= 64 || (blk && !getenv("TK_MT2"))) {
     grid.y = (unsigned)((g.O + 63) / 64);
-    hipLaunchKernelGGL((gemm_i8_kernel<1, true>), grid, dim3(kGemmThreads), 0, s, ga);
+    if (blk) TK_GEMM(1, true); else TK_GEMM(1, false);
   } else {
-    hipLaunchKernelGGL((gemm_i8_kernel<2, true>), grid, dim3(kGemmThreads), 0, s, ga);
+    if (blk) TK_GEMM(2, true); else TK_GEMM(2, false);
   }
+#undef TK_GEMM
   TK_LAUNCH_CHECK();
   return TK_OK;
+}
+
+int conv2d_prepared_impl(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
+                         const int32_t* sums, tk_tensor* out, const tk_conv2d_attrs* a, void* workspace_patch,
+                         hipStream_t s) {
+  return conv2d_run(data, shadow, weight, packed, sums, out, a, workspace_patch, nullptr, s);
+}
+
+int conv2d_block_impl(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
+                      const int32_t* sums, const tk_tensor* bias, tk_tensor* const* outs, int n_outs,
+                      const tk_block_attrs* attrs, void* patch, void* shadow_out, hipStream_t s) {
+  TK_CHECK_ARG(outs && n_outs >= 3 && outs[0], "block needs outputs");
+  BlockIO b{bias, outs, n_outs, attrs, shadow_out};
+  return conv2d_run(data, shadow, weight, packed, sums, outs[0], attrs ? &attrs->conv : nullptr, patch, &b, s);
 }
 
 int64_t conv2d_workspace_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* a) {
@@ -555,7 +854,7 @@ int conv2d_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, 
     return TK_ERR_SHAPE;
   }
   if (!use_mfma_conv(g, a->groups))
-    return conv2d_prepared_impl(data, nullptr, weight, nullptr, nullptr, out, a, nullptr, s);
+    return conv2d_run(data, nullptr, weight, nullptr, nullptr, out, a, nullptr, nullptr, s);
   TK_CHECK_ARG(workspace, "workspace required (tk_qnn_conv2d_workspace_bytes)");
   auto al = [](int64_t v) { return (v + 255) / 256 * 256; };
   char* ws = (char*)workspace;
@@ -570,7 +869,7 @@ int conv2d_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, 
   if (rc) return rc;
   rc = nchw_to_nhwc_impl(data, shadow, s);
   if (rc) return rc;
-  return conv2d_prepared_impl(data, shadow, weight, packed, sums, out, a, patch, s);
+  return conv2d_run(data, shadow, weight, packed, sums, out, a, patch, nullptr, s);
 }
 
 // ---------------------------------------------------------------- dense
@@ -583,8 +882,8 @@ int64_t dense_workspace_bytes(const tk_tensor* data, const tk_tensor* weight) {
   return al(mrows * k_pad) + al(nrows * k_pad) + al(mrows * 4) + al(nrows * 4);
 }
 
-int dense_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_dense_attrs* a,
-               void* workspace, hipStream_t s) {
+static int dense_run(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_dense_attrs* a,
+                     void* workspace, const BlockIO* blk, hipStream_t s) {
   TK_CHECK_ARG(data && weight && out && a && workspace, "null argument");
   TK_CHECK_ARG(data->ndim == 2 && weight->ndim == 2 && out->ndim == 2, "dense expects 2-D tensors");
   TK_CHECK_ARG(is_int8ish(data) && is_int8ish(weight) && is_int(out, 32), "dtypes: int8/uint8 in, int32 out");
@@ -626,10 +925,29 @@ int dense_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, c
   ga.RB = wsum;
   ga.out_nchw = 0;
   ga.ldc = Nn;
+  ga.ch_is_row = 0;
+  int rc = setup_block(ga, blk, out, Nn, 1);
+  if (rc) return rc;
+  ga.shadow_out = nullptr;
   dim3 grid((unsigned)((Nn + 127) / 128), (unsigned)((M + 127) / 128));
-  hipLaunchKernelGGL((gemm_i8_kernel<2, false>), grid, dim3(kGemmThreads), 0, s, ga);
+  if (blk)
+    hipLaunchKernelGGL((gemm_i8_kernel<2, false, true>), grid, dim3(kGemmThreads), 0, s, ga);
+  else
+    hipLaunchKernelGGL((gemm_i8_kernel<2, false, false>), grid, dim3(kGemmThreads), 0, s, ga);
   TK_LAUNCH_CHECK();
   return TK_OK;
+}
+
+int dense_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_dense_attrs* a,
+               void* workspace, hipStream_t s) {
+  return dense_run(data, weight, out, a, workspace, nullptr, s);
+}
+
+int dense_block_impl(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,
+                     int n_outs, const tk_block_attrs* attrs, void* workspace, hipStream_t s) {
+  TK_CHECK_ARG(outs && n_outs >= 3 && outs[0] && attrs, "block needs outputs and attrs");
+  BlockIO b{bias, outs, n_outs, attrs, nullptr};
+  return dense_run(data, weight, outs[0], &attrs->dense, workspace, &b, s);
 }
 
 }  // namespace tk

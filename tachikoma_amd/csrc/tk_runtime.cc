@@ -37,6 +37,11 @@ int conv2d_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, 
 int64_t dense_workspace_bytes(const tk_tensor* data, const tk_tensor* weight);
 int dense_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_dense_attrs* a,
                void* workspace, hipStream_t s);
+int conv2d_block_impl(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
+                      const int32_t* sums, const tk_tensor* bias, tk_tensor* const* outs, int n_outs,
+                      const tk_block_attrs* attrs, void* patch, void* shadow_out, hipStream_t s);
+int dense_block_impl(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,
+                     int n_outs, const tk_block_attrs* attrs, void* workspace, hipStream_t s);
 
 // A tensor descriptor owned by the module (shape copied).
 struct OwnedTensor {
@@ -59,15 +64,22 @@ struct OwnedTensor {
 struct Node {
   tk_node desc{};
   OwnedTensor in[3];
-  OwnedTensor out;
+  OwnedTensor out[TK_MAX_NODE_OUTPUTS];
+  tk_tensor* outp[TK_MAX_NODE_OUTPUTS] = {};
 };
 
 static int run_node(Node& n, hipStream_t s) {
   const tk_node& d = n.desc;
   const tk_tensor* i0 = &n.in[0].t;
   const tk_tensor* i1 = &n.in[1].t;
-  tk_tensor* o = &n.out.t;
+  const tk_tensor* i2 = &n.in[2].t;
+  tk_tensor* o = &n.out[0].t;
   switch (d.kind) {
+    case TK_NODE_CONV_BLOCK:
+      return conv2d_block_impl(i0, d.ext[0], i1, d.ext[1], (const int32_t*)d.ext[2], i2, n.outp, d.n_outputs,
+                               &d.attrs.block, d.ext[3], d.ext[4], s);
+    case TK_NODE_DENSE_BLOCK:
+      return dense_block_impl(i0, i1, i2, n.outp, d.n_outputs, &d.attrs.block, d.ext[0], s);
     case TK_NODE_CONV2D:
       return conv2d_prepared_impl(i0, d.ext[0], i1, d.ext[1], (const int32_t*)d.ext[2], o, &d.attrs.conv2d, d.ext[3], s);
     case TK_NODE_DENSE:
@@ -144,6 +156,16 @@ int tk_qnn_dense(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
                  void* workspace, void* stream) {
   return tk::dense_impl(data, weight, out, attrs, workspace, tk::as_stream(stream));
 }
+int tk_qnn_conv2d_block(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
+                        const int32_t* weight_sums, const tk_tensor* bias, tk_tensor* const* outs, int n_outs,
+                        const tk_block_attrs* attrs, void* patch_sums, void* shadow_out, void* stream) {
+  return tk::conv2d_block_impl(data, shadow, weight, packed, weight_sums, bias, outs, n_outs, attrs, patch_sums,
+                               shadow_out, tk::as_stream(stream));
+}
+int tk_qnn_dense_block(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,
+                       int n_outs, const tk_block_attrs* attrs, void* workspace, void* stream) {
+  return tk::dense_block_impl(data, weight, bias, outs, n_outs, attrs, workspace, tk::as_stream(stream));
+}
 int tk_requantize(const tk_tensor* data, tk_tensor* out, const tk_requantize_attrs* attrs, void* stream) {
   return tk::requantize_impl(data, out, attrs, tk::as_stream(stream));
 }
@@ -199,16 +221,22 @@ int tk_module_create(const tk_node* nodes, int n_nodes, tk_module** out) {
       }
       dst.in[k].assign(src.inputs[k]);
     }
-    if (src.kind != TK_NODE_SHADOW) {
-      if (!src.output) {
-        tk::set_error("tk_module_create: node " + std::to_string(i) + " has no output");
+    if (src.n_outputs < 0 || src.n_outputs > TK_MAX_NODE_OUTPUTS || (src.kind != TK_NODE_SHADOW && src.n_outputs < 1)) {
+      tk::set_error("tk_module_create: node " + std::to_string(i) + " has a bad output count");
+      return TK_ERR_INVALID_ARG;
+    }
+    for (int k = 0; k < src.n_outputs; ++k) {
+      if (!src.outputs[k]) {
+        tk::set_error("tk_module_create: node " + std::to_string(i) + " has a null output");
         return TK_ERR_INVALID_ARG;
       }
-      dst.out.assign(src.output);
+      dst.out[k].assign(src.outputs[k]);
     }
-    for (int k = 0; k < 3; ++k) dst.desc.inputs[k] = nullptr;  // resolved through dst.in
-    dst.desc.output = nullptr;
+    for (int k = 0; k < 3; ++k) dst.desc.inputs[k] = nullptr;  // resolved through dst.in / dst.out
+    for (int k = 0; k < TK_MAX_NODE_OUTPUTS; ++k) dst.desc.outputs[k] = nullptr;
   }
+  for (auto& n : mod->nodes)
+    for (int k = 0; k < TK_MAX_NODE_OUTPUTS; ++k) n.outp[k] = &n.out[k].t;
   mod->done.resize(n_nodes);
   for (int i = 0; i < n_nodes; ++i) {
     hipError_t e = hipEventCreateWithFlags(&mod->done[i], hipEventDisableTiming);
@@ -276,10 +304,17 @@ int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* cons
       return rc;
     }
     if (mod->profiling) TK_HIP(hipEventRecord(mod->prof[i + 1], s));
-    if (capture && host_dst[i] && n.desc.kind != TK_NODE_SHADOW) {
-      TK_HIP(hipEventRecord(mod->done[i], s));
-      TK_HIP(hipStreamWaitEvent(cs, mod->done[i], 0));
-      TK_HIP(hipMemcpyAsync(host_dst[i], tk::ptr(&n.out.t), tk::nbytes(&n.out.t), hipMemcpyDeviceToHost, cs));
+    if (capture && n.desc.n_outputs > 0) {
+      void* const* dst = host_dst + i * TK_MAX_NODE_OUTPUTS;
+      bool any = false;
+      for (int k = 0; k < n.desc.n_outputs; ++k) any |= dst[k] != nullptr;
+      if (any) {
+        TK_HIP(hipEventRecord(mod->done[i], s));
+        TK_HIP(hipStreamWaitEvent(cs, mod->done[i], 0));
+        for (int k = 0; k < n.desc.n_outputs; ++k)
+          if (dst[k])
+            TK_HIP(hipMemcpyAsync(dst[k], tk::ptr(&n.out[k].t), tk::nbytes(&n.out[k].t), hipMemcpyDeviceToHost, cs));
+      }
     }
   }
   mod->have_times = mod->profiling;

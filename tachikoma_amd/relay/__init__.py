@@ -25,7 +25,10 @@ class analysis:  # noqa: N801  (mirrors relay.analysis)
     post_order = staticmethod(post_order)
 
 
-def build(mod, target: str = "mi355x", params=None, mod_name: str = "default"):
-    """``relay.build``: lower a QNN module to the MI355X engine (see build_module.py)."""
+def build(mod, target: str = "mi355x", params=None, mod_name: str = "default", fuse: bool = True):
+    """``relay.build``: lower a QNN module to the MI355X engine (see build_module.py).
+
+    ``fuse=False`` keeps one device kernel per Relay op (the literal per-op record-and-run
+    shape); the default fuses conv/dense layer blocks, writing the same records."""
     from .build_module import build as _build
-    return _build(mod, target=target, params=params, mod_name=mod_name)
+    return _build(mod, target=target, params=params, mod_name=mod_name, fuse=fuse)

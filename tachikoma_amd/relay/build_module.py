@@ -292,10 +292,65 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
     return PlanOp(index, name, op, ins, a, out, consts)
 
 
+@dataclass
+class ExecGroup:
+    """One device node: a single op, or a fused layer block
+    ``qnn.conv2d|qnn.dense → nn.bias_add → qnn.requantize [→ clip|nn.relu]`` whose every op
+    output is still written (and traced) separately."""
+    kind: str            # op name, "conv_block" or "dense_block"
+    ops: List[PlanOp]
+
+    @property
+    def last(self) -> PlanOp:
+        return self.ops[-1]
+
+
+def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
+    """Group the plan's ops into device nodes (topological order preserved).
+
+    A chain fuses when each op is the first consumer of its predecessor's output; other
+    consumers of the intermediates stay correct because every intermediate is materialised
+    in its own HBM buffer anyway.  The requantize must run along the channel axis (1)."""
+    consumers: Dict[str, List[PlanOp]] = {}
+    for op in plan.ops:
+        for x in op.inputs:
+            consumers.setdefault(x, []).append(op)
+    taken = set()
+    groups: List[ExecGroup] = []
+
+    def first_consumer(op: PlanOp, kind) -> Optional[PlanOp]:
+        for c in consumers.get(op.name, []):
+            if c.op in kind and c.inputs[0] == op.name and c.name not in taken:
+                return c
+        return None
+
+    for op in plan.ops:
+        if op.name in taken:
+            continue
+        if fuse and op.op in ("qnn.conv2d", "qnn.dense"):
+            b = first_consumer(op, ("nn.bias_add",))
+            rq = first_consumer(b, ("qnn.requantize",)) if b is not None and b.attrs["axis"] == 1 else None
+            if rq is not None and rq.out.dtype in ("int8", "uint8") and rq.attrs["channel_axis"] == 1 \
+                    and b.out.dtype == "int32":
+                chain = [op, b, rq]
+                cl = first_consumer(rq, ("clip", "nn.relu"))
+                if cl is not None:
+                    chain.append(cl)
+                for c in chain:
+                    taken.add(c.name)
+                groups.append(ExecGroup("conv_block" if op.op == "qnn.conv2d" else "dense_block", chain))
+                continue
+        taken.add(op.name)
+        groups.append(ExecGroup(op.op, [op]))
+    return groups
+
+
 class ExecutorFactory:
     """What ``relay.build`` returns (backend/executor_factory.py:148-211 analogue)."""
 
-    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], target: str, mod_name: str = "default"):
+    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], target: str, mod_name: str = "default",
+                 fuse: bool = True):
+        self.fuse = fuse
         self.plan = plan
         self.params = params
         self.target = target
@@ -311,10 +366,10 @@ class ExecutorFactory:
 
     def _create(self, dev=None):
         from .device_module import DeviceModule
-        return DeviceModule(self.plan, self.params, dev)
+        return DeviceModule(self.plan, self.params, dev, fuse=self.fuse)
 
 
-def build(mod, target: str = "mi355x", params=None, mod_name: str = "default") -> ExecutorFactory:
+def build(mod, target: str = "mi355x", params=None, mod_name: str = "default", fuse: bool = True) -> ExecutorFactory:
     t = str(target).split()[0].lower()
     if t not in TARGETS:
         raise UnsupportedError(
@@ -323,4 +378,4 @@ def build(mod, target: str = "mi355x", params=None, mod_name: str = "default") -
     params = {k: np.ascontiguousarray(np.asarray(v.numpy() if hasattr(v, "numpy") else v))
               for k, v in (params or {}).items()}
     plan = lower(mod, params)
-    return ExecutorFactory(plan, params, t, mod_name)
+    return ExecutorFactory(plan, params, t, mod_name, fuse=fuse)

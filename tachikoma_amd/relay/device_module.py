@@ -7,8 +7,12 @@ Memory layout in HBM (one GPU, one batch shard):
     reuse as in graph_executor.cc:356-464), so each output stays addressable
     for the trace copy-out until the step ends — ResNet-50 at 64 samples is
     ~7 GB, nothing next to 288 GB;
-  * conv inputs have an NHWC int8 shadow (channels padded to 16) produced by a
-    shadow node right before the first conv that reads them.
+  * every tensor read by an MFMA conv has an NHWC int8 "shadow" (channels padded
+    to 16): written directly by the producing fused conv block's epilogue, or by
+    a shadow node right before the first conv that reads it.
+
+Nodes: one per ExecGroup (build_module.exec_groups) — a fused conv/dense layer
+block writes all of its ops' outputs (each a separate trace record) from one kernel.
 """
 from __future__ import annotations
 
@@ -18,15 +22,12 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from .. import _lib
-from .build_module import Plan, PlanOp
+from .build_module import ExecGroup, Plan, PlanOp, exec_groups
 
 
 def _torch():
     import torch
     return torch
-
-
-_TORCH_DT = None
 
 
 def torch_dtype(name: str):
@@ -36,7 +37,7 @@ def torch_dtype(name: str):
 
 
 class DeviceModule:
-    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], dev=None):
+    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], dev=None, fuse: bool = True):
         torch = _torch()
         if not torch.cuda.is_available():
             raise _lib.TachikomaError("no MI355X visible: the engine runs on the GPU only (no CPU fallback)")
@@ -45,7 +46,9 @@ class DeviceModule:
         self.device = torch.device("cuda", 0) if dev is None else _as_torch_device(dev)
         self.buffers: Dict[str, "torch.Tensor"] = {}
         self._keep: List[object] = []
-        self.node_names: List[Optional[str]] = []  # tk node index -> record name (None for shadows)
+        self.node_records: List[List[str]] = []  # tk node index -> record names of its outputs
+        self.node_kinds: List[str] = []
+        self.groups = exec_groups(plan, fuse=fuse)
         with torch.cuda.device(self.device):
             self._alloc(params)
             self._build_nodes()
@@ -71,122 +74,30 @@ class DeviceModule:
         self._keep.append(t)
         return t
 
-    def _scratch(self, nbytes: int):
+    def _scratch(self, nbytes: int, zero: bool = False):
         torch = _torch()
-        t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
+        alloc = torch.zeros if zero else torch.empty
+        t = alloc(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
         self._keep.append(t)
         return t
 
-    def _build_nodes(self):
-        torch = _torch()
-        nodes: List[_lib.tk_node] = []
-        shadows: Dict[str, object] = {}
-        stream = _lib.stream_handle()
-        for op in self.plan.ops:
-            kind = op.op
-            n = _lib.tk_node()
-            ins = [self._ref(x) for x in op.inputs]
-            out = self._ref(op.name)
-            a = op.attrs
-            if kind == "qnn.conv2d":
-                n.kind = _lib.NODE_KINDS["qnn.conv2d"]
-                ca = n.attrs.conv2d
-                ca.strides[:] = list(a["strides"])
-                ca.padding[:] = list(a["padding"])
-                ca.dilation[:] = list(a["dilation"])
-                ca.groups = a["groups"]
-                ca.input_zero_point = a["input_zero_point"]
-                ca.kernel_zero_point = a["kernel_zero_point"]
-                if "kernel_zero_points" in op.consts:
-                    ca.kernel_zero_points = self._dev_i32(op.consts["kernel_zero_points"]).data_ptr()
-                ws = self.lib.tk_qnn_conv2d_workspace_bytes(ins[0].ptr, ins[1].ptr, ctypes.byref(ca))
-                if ws < 0:
-                    _lib.check(-3, f"{op.name} qnn.conv2d workspace")
-                if ws > 0:  # MFMA implicit-GEMM path: shadow + packed weight
-                    src = op.inputs[0]
-                    if src not in shadows:
-                        sh = self._scratch(self.lib.tk_conv2d_shadow_bytes(ins[0].ptr))
-                        shadows[src] = sh
-                        sn = _lib.tk_node()
-                        sn.kind = _lib.NODE_KINDS["shadow"]
-                        sn.n_inputs = 1
-                        sn.inputs[0] = ins[0].ptr
-                        sn.ext[0] = sh.data_ptr()
-                        nodes.append(sn)
-                        self.node_names.append(None)
-                    packed = self._scratch(self.lib.tk_conv2d_packed_weight_bytes(ins[1].ptr, 1))
-                    o = op.out.shape[1]
-                    sums = self._scratch(((o + 127) // 128 * 128) * 4)
-                    _lib.check(self.lib.tk_conv2d_pack_weight(ins[1].ptr, 1, ctypes.c_void_p(packed.data_ptr()),
-                                                              ctypes.c_void_p(sums.data_ptr()), stream),
-                               f"{op.name} pack weight")
-                    n.ext[0] = shadows[src].data_ptr()
-                    n.ext[1] = packed.data_ptr()
-                    n.ext[2] = sums.data_ptr()
-                    if a["kernel_zero_point"] != 0 or "kernel_zero_points" in op.consts:
-                        p = int(np.prod(op.out.shape)) // op.out.shape[1]
-                        n.ext[3] = self._scratch(p * 4).data_ptr()
-            elif kind == "qnn.dense":
-                n.kind = _lib.NODE_KINDS["qnn.dense"]
-                da = n.attrs.dense
-                da.input_zero_point = a["input_zero_point"]
-                da.kernel_zero_point = a["kernel_zero_point"]
-                if "kernel_zero_points" in op.consts:
-                    da.kernel_zero_points = self._dev_i32(op.consts["kernel_zero_points"]).data_ptr()
-                ws = self.lib.tk_qnn_dense_workspace_bytes(ins[0].ptr, ins[1].ptr)
-                n.ext[0] = self._scratch(ws).data_ptr()
-            elif kind == "qnn.requantize":
-                n.kind = _lib.NODE_KINDS["qnn.requantize"]
-                self._fill_rq(n.attrs.requantize, op)
-            elif kind == "qnn.add":
-                n.kind = _lib.NODE_KINDS["qnn.add"]
-                qa = n.attrs.qnn_add
-                for side in ("lhs", "rhs"):
-                    r = getattr(qa, side)
-                    r.mode = a[f"{side}_mode"]
-                    r.axis = -1
-                    r.multiplier = a[f"{side}_multiplier"]
-                    r.shift = a[f"{side}_shift"]
-                    r.input_zero_point = a[f"{side}_zero_point"]
-                    r.output_zero_point = a["output_zero_point"]
-                qa.output_zero_point = a["output_zero_point"]
-                qa.lhs_upcast = a["lhs_upcast"]
-                qa.rhs_upcast = a["rhs_upcast"]
-            elif kind == "nn.bias_add":
-                n.kind = _lib.NODE_KINDS["nn.bias_add"]
-                n.attrs.bias_add.axis = a["axis"]
-            elif kind in ("clip", "nn.relu"):
-                n.kind = _lib.NODE_KINDS["clip"]
-                n.attrs.clip.a_min = a["lo"]
-                n.attrs.clip.a_max = a["hi"]
-            elif kind == "cast":
-                n.kind = _lib.NODE_KINDS["cast"]
-            elif kind in ("nn.max_pool2d", "nn.avg_pool2d"):
-                n.kind = _lib.NODE_KINDS[kind]
-                pa = n.attrs.pool2d
-                pa.pool_size[:] = list(a["pool_size"])
-                pa.strides[:] = list(a["strides"])
-                pa.padding[:] = list(a["padding"])
-                pa.dilation[:] = list(a["dilation"])
-                pa.count_include_pad = int(a.get("count_include_pad", False))
-            elif kind == "nn.global_avg_pool2d":
-                n.kind = _lib.NODE_KINDS[kind]
-            elif kind in ("nn.batch_flatten", "reshape"):
-                n.kind = _lib.NODE_KINDS["copy"]
-            else:
-                raise _lib.TachikomaError(f"no device lowering for {kind}")
-            n.n_inputs = len(ins)
-            for k, r in enumerate(ins):
-                n.inputs[k] = r.ptr
-            n.output = out.ptr
-            nodes.append(n)
-            self.node_names.append(op.name)
-        torch.cuda.current_stream().synchronize()
-        arr = (_lib.tk_node * max(1, len(nodes)))(*nodes)
-        handle = ctypes.c_void_p()
-        _lib.check(self.lib.tk_module_create(arr, len(nodes), ctypes.byref(handle)), "tk_module_create")
-        self.handle = handle
-        self.n_nodes = len(nodes)
+    def _conv_attrs(self, ca, op: PlanOp):
+        a = op.attrs
+        ca.strides[:] = list(a["strides"])
+        ca.padding[:] = list(a["padding"])
+        ca.dilation[:] = list(a["dilation"])
+        ca.groups = a["groups"]
+        ca.input_zero_point = a["input_zero_point"]
+        ca.kernel_zero_point = a["kernel_zero_point"]
+        if "kernel_zero_points" in op.consts:
+            ca.kernel_zero_points = self._dev_i32(op.consts["kernel_zero_points"]).data_ptr()
+
+    def _dense_attrs(self, da, op: PlanOp):
+        a = op.attrs
+        da.input_zero_point = a["input_zero_point"]
+        da.kernel_zero_point = a["kernel_zero_point"]
+        if "kernel_zero_points" in op.consts:
+            da.kernel_zero_points = self._dev_i32(op.consts["kernel_zero_points"]).data_ptr()
 
     def _fill_rq(self, r, op: PlanOp):
         a = op.attrs
@@ -201,6 +112,156 @@ class DeviceModule:
         if "input_zero_points" in op.consts:
             r.input_zero_points = self._dev_i32(op.consts["input_zero_points"]).data_ptr()
         r.output_zero_point = a["output_zero_point"]
+
+    def _is_mfma_conv(self, op: PlanOp) -> bool:
+        ca = _lib.tk_conv2d_attrs()
+        self._conv_attrs(ca, op)
+        x, w = self._ref(op.inputs[0]), self._ref(op.inputs[1])
+        ws = self.lib.tk_qnn_conv2d_workspace_bytes(x.ptr, w.ptr, ctypes.byref(ca))
+        if ws < 0:
+            _lib.check(-3, f"{op.name} qnn.conv2d workspace")
+        return ws > 0
+
+    def _build_nodes(self):
+        torch = _torch()
+        stream = _lib.stream_handle()
+        nodes: List[_lib.tk_node] = []
+        # tensors read by MFMA convs need an NHWC shadow
+        conv_ops = [g.ops[0] for g in self.groups if g.ops[0].op == "qnn.conv2d"]
+        mfma = {op.name: self._is_mfma_conv(op) for op in conv_ops}
+        shadow_bufs: Dict[str, object] = {}
+        for op in conv_ops:
+            if mfma[op.name] and op.inputs[0] not in shadow_bufs:
+                x = self._ref(op.inputs[0])
+                shadow_bufs[op.inputs[0]] = self._scratch(self.lib.tk_conv2d_shadow_bytes(x.ptr), zero=True)
+        shadow_ready = set()
+
+        def emit(n, kind, records):
+            nodes.append(n)
+            self.node_kinds.append(kind)
+            self.node_records.append(records)
+
+        def ensure_shadow(name: str):
+            if name in shadow_ready:
+                return
+            sn = _lib.tk_node()
+            sn.kind = _lib.NODE_KINDS["shadow"]
+            sn.n_inputs = 1
+            sn.inputs[0] = self._ref(name).ptr
+            sn.n_outputs = 0
+            sn.ext[0] = shadow_bufs[name].data_ptr()
+            emit(sn, "shadow", [])
+            shadow_ready.add(name)
+
+        for g in self.groups:
+            head = g.ops[0]
+            n = _lib.tk_node()
+            if g.kind in ("conv_block", "dense_block"):
+                bias_op, rq_op = g.ops[1], g.ops[2]
+                ins = [self._ref(head.inputs[0]), self._ref(head.inputs[1]), self._ref(bias_op.inputs[1])]
+                outs = [self._ref(o.name) for o in g.ops]
+                ba = n.attrs.block
+                self._fill_rq(ba.requantize, rq_op)
+                if len(g.ops) == 4:
+                    ba.has_clip = 1
+                    ba.clip_min, ba.clip_max = g.ops[3].attrs["lo"], g.ops[3].attrs["hi"]
+                if g.kind == "conv_block":
+                    n.kind = _lib.NODE_KINDS["conv_block"]
+                    self._conv_attrs(ba.conv, head)
+                    self._prep_conv(n, head, ins, mfma[head.name], shadow_bufs, ensure_shadow, stream)
+                    if g.last.name in shadow_bufs:
+                        # the epilogue writes the NHWC copy the next MFMA conv reads
+                        n.ext[4] = shadow_bufs[g.last.name].data_ptr()
+                        shadow_ready.add(g.last.name)
+                else:
+                    n.kind = _lib.NODE_KINDS["dense_block"]
+                    self._dense_attrs(ba.dense, head)
+                    n.ext[0] = self._scratch(self.lib.tk_qnn_dense_workspace_bytes(ins[0].ptr, ins[1].ptr)).data_ptr()
+            else:
+                op = head
+                kind = op.op
+                ins = [self._ref(x) for x in op.inputs]
+                outs = [self._ref(op.name)]
+                a = op.attrs
+                if kind == "qnn.conv2d":
+                    n.kind = _lib.NODE_KINDS["qnn.conv2d"]
+                    self._conv_attrs(n.attrs.conv2d, op)
+                    self._prep_conv(n, op, ins, mfma[op.name], shadow_bufs, ensure_shadow, stream)
+                elif kind == "qnn.dense":
+                    n.kind = _lib.NODE_KINDS["qnn.dense"]
+                    self._dense_attrs(n.attrs.dense, op)
+                    n.ext[0] = self._scratch(self.lib.tk_qnn_dense_workspace_bytes(ins[0].ptr, ins[1].ptr)).data_ptr()
+                elif kind == "qnn.requantize":
+                    n.kind = _lib.NODE_KINDS["qnn.requantize"]
+                    self._fill_rq(n.attrs.requantize, op)
+                elif kind == "qnn.add":
+                    n.kind = _lib.NODE_KINDS["qnn.add"]
+                    qa = n.attrs.qnn_add
+                    for side in ("lhs", "rhs"):
+                        r = getattr(qa, side)
+                        r.mode = a[f"{side}_mode"]
+                        r.axis = -1
+                        r.multiplier = a[f"{side}_multiplier"]
+                        r.shift = a[f"{side}_shift"]
+                        r.input_zero_point = a[f"{side}_zero_point"]
+                        r.output_zero_point = a["output_zero_point"]
+                    qa.output_zero_point = a["output_zero_point"]
+                    qa.lhs_upcast = a["lhs_upcast"]
+                    qa.rhs_upcast = a["rhs_upcast"]
+                elif kind == "nn.bias_add":
+                    n.kind = _lib.NODE_KINDS["nn.bias_add"]
+                    n.attrs.bias_add.axis = a["axis"]
+                elif kind in ("clip", "nn.relu"):
+                    n.kind = _lib.NODE_KINDS["clip"]
+                    n.attrs.clip.a_min = a["lo"]
+                    n.attrs.clip.a_max = a["hi"]
+                elif kind == "cast":
+                    n.kind = _lib.NODE_KINDS["cast"]
+                elif kind in ("nn.max_pool2d", "nn.avg_pool2d"):
+                    n.kind = _lib.NODE_KINDS[kind]
+                    pa = n.attrs.pool2d
+                    pa.pool_size[:] = list(a["pool_size"])
+                    pa.strides[:] = list(a["strides"])
+                    pa.padding[:] = list(a["padding"])
+                    pa.dilation[:] = list(a["dilation"])
+                    pa.count_include_pad = int(a.get("count_include_pad", False))
+                elif kind == "nn.global_avg_pool2d":
+                    n.kind = _lib.NODE_KINDS[kind]
+                elif kind in ("nn.batch_flatten", "reshape"):
+                    n.kind = _lib.NODE_KINDS["copy"]
+                else:
+                    raise _lib.TachikomaError(f"no device lowering for {kind}")
+            n.n_inputs = len(ins)
+            for k, r in enumerate(ins):
+                n.inputs[k] = r.ptr
+            n.n_outputs = len(outs)
+            for k, r in enumerate(outs):
+                n.outputs[k] = r.ptr
+            emit(n, g.kind, [o.name for o in g.ops])
+        torch.cuda.current_stream().synchronize()
+        arr = (_lib.tk_node * max(1, len(nodes)))(*nodes)
+        handle = ctypes.c_void_p()
+        _lib.check(self.lib.tk_module_create(arr, len(nodes), ctypes.byref(handle)), "tk_module_create")
+        self.handle = handle
+        self.n_nodes = len(nodes)
+
+    def _prep_conv(self, n, op: PlanOp, ins, is_mfma: bool, shadow_bufs, ensure_shadow, stream):
+        """MFMA path: shadow of the input + packed weight + weight sums (+ patch-sum scratch)."""
+        if not is_mfma:
+            return
+        ensure_shadow(op.inputs[0])
+        packed = self._scratch(self.lib.tk_conv2d_packed_weight_bytes(ins[1].ptr, 1))
+        o = op.out.shape[1]
+        sums = self._scratch(((o + 127) // 128 * 128) * 4)
+        _lib.check(self.lib.tk_conv2d_pack_weight(ins[1].ptr, 1, ctypes.c_void_p(packed.data_ptr()),
+                                                  ctypes.c_void_p(sums.data_ptr()), ctypes.c_void_p(stream)),
+                   f"{op.name} pack weight")
+        n.ext[0] = shadow_bufs[op.inputs[0]].data_ptr()
+        n.ext[1] = packed.data_ptr()
+        n.ext[2] = sums.data_ptr()
+        if op.attrs["kernel_zero_point"] != 0 or "kernel_zero_points" in op.consts:
+            p = int(np.prod(op.out.shape)) // op.out.shape[1]
+            n.ext[3] = self._scratch(p * 4).data_ptr()
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -223,12 +284,21 @@ class DeviceModule:
                 raise ValueError(f"set_input {name}: shape {v.shape} vs {tuple(buf.shape)}")
             buf.copy_(torch.from_numpy(np.ascontiguousarray(v.astype(np.dtype(str(buf.dtype).replace("torch.", ""))))))
 
+    def host_dst_array(self, record_ptrs: Dict[str, int]):
+        """Per node × output slot host pointers for tk_module_run (NULL = not captured)."""
+        slots = self.n_nodes * _lib.MAX_NODE_OUTPUTS
+        arr = (ctypes.c_void_p * slots)()
+        for i, recs in enumerate(self.node_records):
+            for k, name in enumerate(recs):
+                if name in record_ptrs:
+                    arr[i * _lib.MAX_NODE_OUTPUTS + k] = record_ptrs[name]
+        return arr
+
     def run(self, stream=None, capture_stream=None, host_dst=None) -> None:
         s = _lib.stream_handle(stream)
         if host_dst is not None:
-            arr = (ctypes.c_void_p * self.n_nodes)(*host_dst)
             _lib.check(self.lib.tk_module_run(self.handle, ctypes.c_void_p(s),
-                                              ctypes.c_void_p(_lib.stream_handle(capture_stream)), arr),
+                                              ctypes.c_void_p(_lib.stream_handle(capture_stream)), host_dst),
                        "tk_module_run")
         else:
             _lib.check(self.lib.tk_module_run(self.handle, ctypes.c_void_p(s), None, None), "tk_module_run")
@@ -238,8 +308,9 @@ class DeviceModule:
         _lib.check(self.lib.tk_module_run_profiled(self.handle, ctypes.c_void_p(_lib.stream_handle(stream)), ms),
                    "tk_module_run_profiled")
         out = {}
-        for i, name in enumerate(self.node_names):
-            out[name if name is not None else f"<shadow:{i}>"] = float(ms[i])
+        for i, recs in enumerate(self.node_records):
+            key = "+".join(recs) if recs else f"<shadow:{i}>"
+            out[key] = float(ms[i])
         return out
 
     def set_profiling(self, enable: bool) -> None:

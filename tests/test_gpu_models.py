@@ -13,8 +13,8 @@ from tachikoma_amd.trace_format import read_trace
 pytestmark = pytest.mark.gpu
 
 
-def _run_trace(model, x, tmp_path):
-    lib = relay.build(model.mod, target="mi355x", params=model.params)
+def _run_trace(model, x, tmp_path, fuse=True):
+    lib = relay.build(model.mod, target="mi355x", params=model.params, fuse=fuse)
     m = graph_executor.GraphModule(lib["default"]())
     m.set_input(model.input_name, x)
     path = str(tmp_path / f"{model.name}.tkt")
@@ -53,11 +53,12 @@ def test_lenet5_trace(device, tmp_path):
     _compare(tr.records, exp)
 
 
-@pytest.mark.parametrize("name,batch", [("resnet18", 2), ("mobilenet_v2", 1), ("resnet50", 2)])
-def test_cnn_trace_bit_exact(device, tmp_path, name, batch):
+@pytest.mark.parametrize("name,batch,fuse", [("resnet18", 2, True), ("resnet18", 2, False), ("mobilenet_v2", 1, True),
+                                             ("mobilenet_v2", 1, False), ("resnet50", 2, True)])
+def test_cnn_trace_bit_exact(device, tmp_path, name, batch, fuse):
     model = zoo.MODELS[name](batch=batch)
     x = model.random_input()
-    _, tr = _run_trace(model, x, tmp_path)
+    _, tr = _run_trace(model, x, tmp_path, fuse=fuse)
     exp = graph_ref.calibrate(model.mod, model.params, {"data": x}, backend="c")
     assert len(tr.records) == len(exp)
     _compare(tr.records, exp)

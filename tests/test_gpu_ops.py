@@ -180,3 +180,44 @@ def test_pools(tk):
                                       ref.avg_pool2d(x32, (3, 3), (2, 2), (1, 1, 1, 1), count_include_pad=cip))
     x32 = rng.integers(-10**6, 10**6, size=(3, 7, 7, 7)).astype(np.int32)
     np.testing.assert_array_equal(tk.global_avg_pool(x32), ref.global_avg_pool2d(x32))
+
+
+BLOCK_CASES = [
+    # N, C, H, W, O, K, stride, pad, groups, dx, za, out_dtype, clip
+    (2, 32, 9, 9, 64, 3, 1, 1, 1, "int8", -3, "int8", (2, 127)),
+    (1, 3, 15, 15, 64, 7, 2, 3, 1, "int8", 4, "int8", (-5, 100)),
+    (2, 64, 7, 7, 200, 1, 1, 0, 1, "uint8", 130, "uint8", None),
+    (1, 24, 10, 10, 24, 3, 2, 1, 24, "int8", 1, "int8", (0, 96)),     # depthwise (direct kernel)
+    (1, 1, 12, 12, 6, 5, 1, 2, 1, "int8", 0, "int8", (-1, 127)),      # tiny Cin (direct kernel)
+]
+
+
+@pytest.mark.parametrize("case", BLOCK_CASES, ids=[f"block{i}" for i in range(len(BLOCK_CASES))])
+def test_conv_block_matches_unfused_ops(tk, case):
+    n, c, h, w, o, k, s, p, g, dx, za, odt, clip = case
+    rng = np.random.default_rng(17 + n * c)
+    x = _rand(rng, (n, c, h, w), dx)
+    wt = _rand(rng, (o, c // g, k, k), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_in = rng.uniform(1e-5, 1e-3, size=o).astype(np.float32)
+    s_out = np.float32(0.01)
+    pad = (p, p, p, p)
+    outs = tk.conv2d_block(x, wt, bias, za, 0, s_in, s_out, 3, clip=clip, strides=(s, s), padding=pad, groups=g,
+                           out_dtype=odt, want_shadow=True)
+    conv = ref.qnn_conv2d(x, wt, za, 0, strides=(s, s), padding=pad, groups=g)
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(3), axis=1, out_dtype=odt)
+    exp = [conv, badd, rq]
+    if clip is not None:
+        exp.append(ref.clip(rq, *clip))
+    for got, e in zip(outs, exp):
+        np.testing.assert_array_equal(got, e)
+    # the NHWC shadow of the last output (what the next MFMA conv reads)
+    shadow = outs[-1]
+    last = exp[-1]
+    cpad = shadow.shape[-1]
+    nhwc = np.transpose(last, (0, 2, 3, 1))
+    view = shadow[..., :o].view(np.int8)
+    expect = (nhwc.view(np.uint8) ^ 0x80).view(np.int8) if odt == "uint8" else nhwc.view(np.int8)
+    np.testing.assert_array_equal(view, expect)
+    assert not shadow[..., o:cpad].any()

@@ -176,3 +176,70 @@ def global_avg_pool(x):
     out = empty((x.shape[0], x.shape[1], 1, 1), str(x.dtype))
     _sync_check(lib.tk_global_avg_pool2d(ref(xd).ptr, ref(out).ptr, stream()), "tk_global_avg_pool2d")
     return out.cpu().numpy()
+
+
+def _rq_attrs(r, keep, input_scale, output_scale, output_zero_point, rounding="UPWARD", axis=1):
+    mode, ms, ss = requantize_plan(input_scale, output_scale, rounding)
+    r.mode = mode
+    r.axis = axis
+    if mode >= _lib.TK_RQ_AXIS_UPWARD:
+        m_d, s_d = dev(ms), dev(ss)
+        keep += [m_d, s_d]
+        r.multipliers = m_d.data_ptr()
+        r.shifts = s_d.data_ptr()
+    else:
+        r.multiplier, r.shift = int(ms[0]), int(ss[0])
+    r.output_zero_point = int(output_zero_point)
+
+
+def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1, 1), padding=(0, 0, 0, 0),
+                 dilation=(1, 1), groups=1, out_dtype="int8", want_shadow=False):
+    """Fused conv -> bias_add -> requantize(axis 1) [-> clip] through tk_qnn_conv2d_block."""
+    lib = _lib.load()
+    n, c, h, wd = x.shape
+    o = w.shape[0]
+    kh, kw = w.shape[2], w.shape[3]
+    pt, pl, pb, pr = padding
+    oh = (h + pt + pb - dilation[0] * (kh - 1) - 1) // strides[0] + 1
+    ow = (wd + pl + pr - dilation[1] * (kw - 1) - 1) // strides[1] + 1
+    xd, wdv, bd = dev(x), dev(w), dev(bias)
+    outs = [empty((n, o, oh, ow), "int32"), empty((n, o, oh, ow), "int32"), empty((n, o, oh, ow), out_dtype)]
+    if clip is not None:
+        outs.append(empty((n, o, oh, ow), out_dtype))
+    a = _lib.tk_block_attrs()
+    a.conv.strides[:] = list(strides)
+    a.conv.padding[:] = list(padding)
+    a.conv.dilation[:] = list(dilation)
+    a.conv.groups = groups
+    a.conv.input_zero_point = int(za)
+    a.conv.kernel_zero_point = int(zw)
+    keep = []
+    _rq_attrs(a.requantize, keep, s_in, s_out, zp_out)
+    if clip is not None:
+        a.has_clip = 1
+        a.clip_min, a.clip_max = clip
+    rx, rw, rb = ref(xd), ref(wdv), ref(bd)
+    ws_bytes = lib.tk_qnn_conv2d_workspace_bytes(rx.ptr, rw.ptr, ctypes.byref(a.conv))
+    shadow = packed = sums = patch = shadow_out = None
+    st = stream()
+    if ws_bytes > 0:
+        shadow = empty((lib.tk_conv2d_shadow_bytes(rx.ptr),), "uint8")
+        packed = empty((lib.tk_conv2d_packed_weight_bytes(rw.ptr, 1),), "uint8")
+        sums = empty((((o + 127) // 128) * 128,), "int32")
+        patch = empty((max(n * oh * ow, 4),), "int32")
+        _lib.check(lib.tk_nchw_to_nhwc_i8(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), st))
+        _lib.check(lib.tk_conv2d_pack_weight(rw.ptr, 1, ctypes.c_void_p(packed.data_ptr()),
+                                             ctypes.c_void_p(sums.data_ptr()), st))
+    if want_shadow:
+        import torch
+        cpad = (o + 15) // 16 * 16
+        shadow_out = torch.zeros((n, oh, ow, cpad), dtype=torch.uint8, device="cuda")
+    refs = [ref(t) for t in outs]
+    arr = (ctypes.POINTER(_lib.tk_tensor) * len(refs))(*[r.ptr for r in refs])
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    _sync_check(lib.tk_qnn_conv2d_block(rx.ptr, ptr(shadow), rw.ptr, ptr(packed), ptr(sums), rb.ptr, arr, len(refs),
+                                        ctypes.byref(a), ptr(patch), ptr(shadow_out), st), "tk_qnn_conv2d_block")
+    res = [t.cpu().numpy() for t in outs]
+    if want_shadow:
+        res.append(shadow_out.cpu().numpy())
+    return res

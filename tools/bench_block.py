@@ -1,0 +1,84 @@
+"""Microbenchmark of the fused conv block kernel on representative ResNet-50 layer shapes
+(batch 64).  Prints time per call, algorithmic GB/s and TOPS.  GPU only."""
+import ctypes
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from tachikoma_amd import _lib  # noqa: E402
+from tachikoma_amd.relay.build_module import requantize_plan  # noqa: E402
+
+SHAPES = [  # name, C, H, O, K, stride, pad
+    ("stem 3->64 k7 s2", 3, 224, 64, 7, 2, 3),
+    ("1x1 64->256 56", 64, 56, 256, 1, 1, 0),
+    ("1x1 256->64 56", 256, 56, 64, 1, 1, 0),
+    ("3x3 64->64 56", 64, 56, 64, 3, 1, 1),
+    ("3x3 128->128 28", 128, 28, 128, 3, 1, 1),
+    ("3x3 256->256 14", 256, 14, 256, 3, 1, 1),
+    ("1x1 1024->256 14", 1024, 14, 256, 1, 1, 0),
+    ("3x3 512->512 7", 512, 7, 512, 3, 1, 1),
+    ("1x1 512->2048 7", 512, 7, 2048, 1, 1, 0),
+]
+
+
+def main(batch=64, iters=20):
+    lib = _lib.load()
+    dev = torch.device("cuda")
+    rng = np.random.default_rng(0)
+    tot_us = 0
+    for name, C, H, O, K, S, P in SHAPES:
+        OH = (H + 2 * P - K) // S + 1
+        x = torch.from_numpy(rng.integers(-128, 128, size=(batch, C, H, H)).astype(np.int8)).to(dev)
+        w = torch.from_numpy(rng.integers(-128, 128, size=(O, C, K, K)).astype(np.int8)).to(dev)
+        b = torch.from_numpy(rng.integers(-2**14, 2**14, size=O).astype(np.int32)).to(dev)
+        outs = [torch.empty((batch, O, OH, OH), dtype=t, device=dev) for t in (torch.int32, torch.int32, torch.int8,
+                                                                             torch.int8)]
+        a = _lib.tk_block_attrs()
+        a.conv.strides[:] = [S, S]
+        a.conv.padding[:] = [P] * 4
+        a.conv.dilation[:] = [1, 1]
+        a.conv.groups = 1
+        a.conv.input_zero_point = 3
+        mode, ms, ss = requantize_plan(rng.uniform(1e-5, 1e-4, size=O).astype(np.float32), np.float32(0.05), "UPWARD")
+        md, sd = torch.from_numpy(ms).to(dev), torch.from_numpy(ss).to(dev)
+        a.requantize.mode, a.requantize.axis = mode, 1
+        a.requantize.multipliers, a.requantize.shifts = md.data_ptr(), sd.data_ptr()
+        a.requantize.output_zero_point = 2
+        a.has_clip, a.clip_min, a.clip_max = 1, 2, 127
+        rx, rw, rb = [_lib.TensorRef.from_torch(t) for t in (x, w, b)]
+        refs = [_lib.TensorRef.from_torch(t) for t in outs]
+        arr = (ctypes.POINTER(_lib.tk_tensor) * 4)(*[r.ptr for r in refs])
+        st = ctypes.c_void_p(_lib.stream_handle())
+        shadow = torch.empty(lib.tk_conv2d_shadow_bytes(rx.ptr), dtype=torch.uint8, device=dev)
+        packed = torch.empty(lib.tk_conv2d_packed_weight_bytes(rw.ptr, 1), dtype=torch.uint8, device=dev)
+        sums = torch.empty(((O + 127) // 128) * 128, dtype=torch.int32, device=dev)
+        sh_out = torch.zeros(batch * OH * OH * ((O + 15) // 16 * 16), dtype=torch.uint8, device=dev)
+        _lib.check(lib.tk_nchw_to_nhwc_i8(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), st))
+        _lib.check(lib.tk_conv2d_pack_weight(rw.ptr, 1, ctypes.c_void_p(packed.data_ptr()),
+                                             ctypes.c_void_p(sums.data_ptr()), st))
+
+        def call():
+            _lib.check(lib.tk_qnn_conv2d_block(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), rw.ptr,
+                                               ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(sums.data_ptr()),
+                                               rb.ptr, arr, 4, ctypes.byref(a), None,
+                                               ctypes.c_void_p(sh_out.data_ptr()), st))
+        call()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            call()
+        e1.record()
+        e1.synchronize()
+        us = e0.elapsed_time(e1) / iters * 1e3
+        tot_us += us
+        out_el = batch * O * OH * OH
+        by = x.numel() + w.numel() + 4 * O + out_el * 10
+        macs = out_el * C * K * K
+        print(f"{name:22s} {us:8.1f} us {by / us / 1e3:8.0f} GB/s {2 * macs / us / 1e6:8.1f} TOPS", flush=True)
+    print(f"sum {tot_us:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
