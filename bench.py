@@ -49,13 +49,13 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(model_fn, batch_hint: int, budget_s: float, seed: int):
+def cpu_baseline(model_fn, batch_hint: int, budget_s: float):
     """Time the oracle's C restatement (OpenMP port of the reference's int16 conv / int64
     requantize semantics) doing the same per-op record-and-run on the host cores."""
     from oracle import graph_ref
     threads = min(16, len(os.sched_getaffinity(0)))
     model = model_fn(batch=1)
-    x_all = model.random_input(seed=seed, batch=batch_hint)
+    x_all = model.sample_inputs(0, batch_hint)
     # warm (page in weights, OpenMP pool) on one sample, then as many samples as fit the budget
     t0 = time.perf_counter()
     graph_ref.calibrate(model.mod, model.params, {"data": x_all[:1]}, backend="c", threads=threads)
@@ -68,6 +68,18 @@ def cpu_baseline(model_fn, batch_hint: int, budget_s: float, seed: int):
     return {"value": n / dt, "unit": "op-traces/s", "cores": threads, "kind": "port",
             "sample": f"{n} samples of {model.name} int8 224x224 traced one by one (batch-1 record-and-run, "
                       f"every op output kept), C/OpenMP oracle, {dt:.1f}s"}
+
+
+def pmc_traffic(model: str, batch: int, launches: int):
+    """HBM bytes per launch of the block kernel from the committed PMC summary
+    (tools/pmc.sh -> profiles/*_pmc_block.json), when it was taken on this workload."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_block.json")), reverse=True):
+        with open(path) as f:
+            doc = json.load(f)
+        if doc.get("model") == model and doc.get("batch") == batch and doc.get("launches_per_step") == launches:
+            return doc["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def main():
@@ -83,7 +95,7 @@ def main():
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
 
-    from tachikoma_amd import relay, zoo
+    from tachikoma_amd import relay, shard, zoo
     from tachikoma_amd.contrib import graph_executor
 
     B = args.batch
@@ -92,10 +104,14 @@ def main():
     _log(f"rank {rank}/{world}: building {args.model} batch {B} on {device}")
     lib = relay.build(model.mod, target="mi355x", params=model.params)
     m = graph_executor.GraphModule(lib["default"](local_rank))
-    x = model.random_input(seed=model.seed + 1000 + rank)  # this rank's shard of the global batch
+    # weak scaling: B samples per GPU; this rank traces samples [offset, offset + B) of the global batch
+    offset, count = shard.shard_range(B * world, world, rank)
+    x = model.sample_inputs(offset, count)
     m.set_input("data", x)
-    m.set_trace_meta(model=model.name, sample_offset=rank * B, rank=rank, world=world, n_samples=B)
+    m.set_trace_meta(model=model.name, sample_offset=offset, rank=rank, world=world, n_samples=count)
     cap = m.trace_capture()
+    if args.sink == "file":
+        os.makedirs(args.out_dir, exist_ok=True)
     _log(f"trace image {cap.layout.total / 1e9:.2f} GB pinned, {len(m.plan.ops)} ops")
     stream = torch.cuda.current_stream(device)
 
@@ -111,39 +127,43 @@ def main():
         m.run(trace=True)
         cap.synchronize()
         if args.sink == "file":
-            cap.write(os.path.join(args.out_dir, f"trace.rank{rank}.step{i}.tkt"))
+            cap.write(shard.shard_file(args.out_dir, rank))
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(device)
 
     # ---- timed region: K traced steps
-    m.module.set_profiling(True)
-    node_ms = np.zeros(m.module.n_nodes)
     barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
-        node_ms += np.array(m.module.node_times())
     torch.cuda.synchronize(device)
     barrier()
     elapsed = time.perf_counter() - t0
-    m.module.set_profiling(False)
-    node_ms /= max(args.steps, 1)
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
-    # ---- compute-only (no capture) for the report
+    # ---- compute-only steps (no capture): the kernels alone, each node bracketed by HIP
+    # events recorded on the stream the node's kernel runs on (tk_module_set_profiling);
+    # the roofline below is taken from these, where no D2H copy shares the device
     torch.cuda.synchronize(device)
     tc = time.perf_counter()
     for _ in range(args.steps):
         m.run(trace=False)
     torch.cuda.synchronize(device)
     compute_ms = (time.perf_counter() - tc) / max(args.steps, 1) * 1e3
+    m.module.set_profiling(True)
+    node_ms = np.zeros(m.module.n_nodes)
+    for _ in range(args.steps):
+        m.run(trace=False)
+        node_ms += np.array(m.module.node_times())
+    m.module.set_profiling(False)
+    node_ms /= max(args.steps, 1)
 
     # ---- roofline of the dominant kernel: the fused MFMA conv/dense layer block
     # (qnn.conv2d|dense -> bias_add -> requantize [-> clip] in one kernel).  It is bound by
@@ -172,15 +192,21 @@ def main():
     achieved_bw = blk_bytes / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
     achieved_ops = blk_ops / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
     total_ms = float(node_ms.sum())
+    traffic, traffic_src = pmc_traffic(args.model, B, n_launch)
 
-    # ---- optional trace-digest all-gather (RCCL over xGMI): one 8-byte digest per rank
-    digests = None
-    if world > 1:
-        dg = torch.tensor([hash(bytes(cap.image[:4096].numpy())) & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64,
-                          device=device)
-        out = [torch.zeros_like(dg) for _ in range(world)]
-        dist.all_gather(out, dg)
-        digests = [int(v.item()) for v in out]
+    # ---- trace-digest all-gather (RCCL over xGMI): one u64 record digest per rank, computed
+    # on the device over the records of the last traced step (outside the timed region)
+    m.run(trace=not args.no_trace)
+    if not args.no_trace:
+        cap.synchronize()
+    digests = shard.gather_digests(m.module.records_digest(stream))
+    if args.sink == "file" and not args.no_trace:
+        path = shard.shard_file(args.out_dir, rank)
+        cap.write(path)
+        entries = [shard.ShardEntry(r, *shard.shard_range(B * world, world, r), shard.hex64(d),
+                                    shard.shard_file(args.out_dir, r)) for r, d in enumerate(digests)]
+        if rank == 0:
+            shard.write_manifest(os.path.join(args.out_dir, "trace.manifest.json"), model.name, B * world, entries)
 
     if rank == 0:
         traces = B * world * args.steps
@@ -188,7 +214,7 @@ def main():
         cpu = None
         if not args.skip_cpu:
             _log("cpu baseline (oracle port) ...")
-            cpu = cpu_baseline(model_fn, B, args.cpu_budget_s, model.seed + 1000)
+            cpu = cpu_baseline(model_fn, B, args.cpu_budget_s)
         macs_per_sample = zoo.macs_per_sample(model_fn(batch=1))
         trace_bytes = cap.layout.total
         line = {
@@ -209,7 +235,11 @@ def main():
                        "model": args.model, "global_batch": B * world, "samples_per_gpu": B, "seq_len": None,
                        "parallelism": f"batch-shard x{world}", "sink": args.sink},
             "roofline": {"bound": "hbm", "achieved": round(achieved_bw / 1e9, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved_bw / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved_bw / 1e9 / HBM_PEAK_GBPS, 4),
+                         "traffic": None if traffic is None else int(traffic),
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": int(blk_bytes / max(n_launch, 1)),
                          "kernel": "gemm_i8_kernel<*,*,block> fused conv/dense layer block (v_mfma_i32_32x32x32_i8)",
                          "launches_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
                          "algorithmic_bytes_per_step": int(blk_bytes),
@@ -224,7 +254,7 @@ def main():
                 "trace_GBps_per_gpu": round(trace_bytes / (elapsed_max / args.steps) / 1e9, 2),
                 "macs_per_sample": macs_per_sample,
                 "ops_per_sample": 2 * macs_per_sample,
-                "digests": digests,
+                "record_digests": [shard.hex64(d) for d in digests],
             },
         }
         print(json.dumps(line), flush=True)

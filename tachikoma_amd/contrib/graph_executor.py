@@ -196,6 +196,13 @@ class GraphModule:
         cap.write(path)
         return path
 
+    def trace_digest(self) -> int:
+        """u64 digest of the last run's records, computed on the device
+        (equals trace_format.trace_file_digest of the dumped trace)."""
+        import torch
+        d = self.module.records_digest(torch.cuda.current_stream(self.module.device))
+        return int(d.item()) & 0xFFFFFFFFFFFFFFFF
+
     def profile(self) -> Dict[str, float]:
         """Per-node device time in ms (GraphExecutorDebug::RunIndividual analogue)."""
         return self.module.run_profiled()

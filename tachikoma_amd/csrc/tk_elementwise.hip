@@ -494,7 +494,7 @@ int copy_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s) {
 
 // ---------------------------------------------------------------- digest
 // Order-aware, parallel 64-bit digest: Σ_i mix(word_i ^ (i · φ)) mod 2^64 over
-// little-endian 8-byte words (tail zero-padded), finalised with the byte length.
+// little-endian 8-byte words (tail zero-padded).  Host twin: trace_format.digest_bytes.
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;

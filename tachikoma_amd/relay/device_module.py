@@ -321,6 +321,24 @@ class DeviceModule:
         _lib.check(self.lib.tk_module_node_times(self.handle, ms), "tk_module_node_times")
         return [float(v) for v in ms]
 
+    def records_digest(self, stream=None):
+        """Device digest of every trace record (trace_format.records_digest twin), enqueued on
+        ``stream``; returns a 1-element int64 device tensor (the u64 digest's bit pattern)."""
+        torch = _torch()
+        recs = self.plan.records
+        if getattr(self, "_digest_slots", None) is None:
+            self._digest_slots = torch.zeros(max(1, len(recs)), dtype=torch.int64, device=self.device)
+            self._digest_out = torch.zeros(1, dtype=torch.int64, device=self.device)
+        s = ctypes.c_void_p(_lib.stream_handle(stream))
+        base = self._digest_slots.data_ptr()
+        for i, t in enumerate(recs):
+            buf = self.buffers[t.name]
+            _lib.check(self.lib.tk_digest_bytes(ctypes.c_void_p(buf.data_ptr()), buf.numel() * buf.element_size(),
+                                                ctypes.c_void_p(base + 8 * i), s), f"digest {t.name}")
+        _lib.check(self.lib.tk_digest_bytes(ctypes.c_void_p(base), 8 * len(recs),
+                                            ctypes.c_void_p(self._digest_out.data_ptr()), s), "digest")
+        return self._digest_out
+
     def output(self, name: str):
         return self.buffers[name]
 

@@ -1,0 +1,101 @@
+"""Batch sharding of trace generation across the GPUs of one node.
+
+Every sample's trace is independent (the reference walks one sample at a time with
+no cross-sample state, python/tvm/mrt/trace.py:65-117), so the global batch is cut
+into contiguous shards, one per rank (one process per GPU), with no collective on
+the data path.  Each rank writes its own trace file whose header carries
+``sample_offset``; the only collective is an optional all-gather of one u64 record
+digest per rank (RCCL over xGMI when the tensors live on the GPU, gloo on CPU) so
+rank 0 can write a run manifest that pins every shard.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import asdict, dataclass
+from typing import List, Optional, Tuple
+
+MANIFEST_FORMAT = "tachikoma-trace-manifest"
+
+
+def shard_range(global_batch: int, world: int, rank: int) -> Tuple[int, int]:
+    """(sample_offset, n_samples) of ``rank``: contiguous, remainder to the first ranks."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    if global_batch < 0:
+        raise ValueError("negative batch")
+    base, rem = divmod(global_batch, world)
+    count = base + (1 if rank < rem else 0)
+    offset = rank * base + min(rank, rem)
+    return offset, count
+
+
+def dist_env() -> Tuple[int, int, int]:
+    """(rank, world, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def _to_i64(v: int) -> int:
+    v &= 0xFFFFFFFFFFFFFFFF
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def gather_digests(digest, device=None) -> List[int]:
+    """All-gather one u64 per rank over the default process group.
+
+    ``digest`` is an int or a 1-element int64 tensor (e.g. DeviceModule.records_digest,
+    already on the GPU so RCCL moves it over xGMI without a host round trip)."""
+    import torch
+    import torch.distributed as dist
+    if isinstance(digest, torch.Tensor):
+        t = digest.reshape(1).to(torch.int64)
+    else:
+        t = torch.tensor([_to_i64(int(digest))], dtype=torch.int64, device=device)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [int(t.item()) & 0xFFFFFFFFFFFFFFFF]
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [int(v.item()) & 0xFFFFFFFFFFFFFFFF for v in out]
+
+
+def shard_file(out_dir: str, rank: int, stem: str = "trace") -> str:
+    return os.path.join(out_dir, f"{stem}.rank{rank}.tkt")
+
+
+@dataclass
+class ShardEntry:
+    rank: int
+    sample_offset: int
+    n_samples: int
+    digest: str  # u64 as 16 hex digits
+    file: Optional[str] = None
+
+
+def write_manifest(path: str, model: str, global_batch: int, shards: List[ShardEntry]) -> None:
+    covered = sorted((s.sample_offset, s.n_samples) for s in shards)
+    pos = 0
+    for off, n in covered:
+        if off != pos:
+            raise ValueError(f"shards do not tile the batch: gap/overlap at sample {pos}")
+        pos += n
+    if pos != global_batch:
+        raise ValueError(f"shards cover {pos} of {global_batch} samples")
+    doc = {"format": MANIFEST_FORMAT, "version": 1, "model": model, "global_batch": global_batch,
+           "world": len(shards), "shards": [asdict(s) for s in sorted(shards, key=lambda s: s.rank)]}
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(doc, f, indent=1)
+    os.replace(tmp, path)
+
+
+def read_manifest(path: str) -> dict:
+    with open(path) as f:
+        doc = json.load(f)
+    if doc.get("format") != MANIFEST_FORMAT:
+        raise ValueError("not a tachikoma trace manifest")
+    return doc
+
+
+def hex64(v: int) -> str:
+    return f"{v & 0xFFFFFFFFFFFFFFFF:016x}"

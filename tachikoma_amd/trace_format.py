@@ -164,3 +164,51 @@ def read_trace(path_or_bytes, copy: bool = False) -> Trace:
     params = parse_ndarray_list(buf, po, ps, copy=copy)
     records = parse_ndarray_list(buf, ro, rs, copy=copy)
     return Trace(meta, params, records)
+
+
+# ---------------------------------------------------------------- digests
+# Host twin of the device digest (tk_digest_bytes, csrc/tk_elementwise.hip):
+#   D(bytes) = Σ_i splitmix64_final(w_i ^ i·0x9E3779B97F4A7C15)  mod 2^64
+# over little-endian 8-byte words w_i, the tail zero-padded.  The trace digest of a
+# shard is D over the u64 array [D(record_0), D(record_1), ...] in record order, so
+# it can be recomputed from a trace file without the GPU.
+
+_PHI = np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def digest_bytes(buf, chunk_words: int = 1 << 22) -> int:
+    raw = np.frombuffer(memoryview(buf).cast("B"), dtype=np.uint8)
+    nw = (raw.size + 7) // 8
+    total = np.uint64(0)
+    full = raw.size // 8
+    with np.errstate(over="ignore"):
+        for s in range(0, nw, chunk_words):
+            e = min(nw, s + chunk_words)
+            if e <= full:
+                w = raw[s * 8:e * 8].view("<u8")
+            else:
+                tail = np.zeros((e - s) * 8, np.uint8)
+                part = raw[s * 8:]
+                tail[:part.size] = part
+                w = tail.view("<u8")
+            idx = np.arange(s, e, dtype=np.uint64)
+            total = total + np.sum(_mix64(w ^ (idx * _PHI)), dtype=np.uint64)
+    return int(total)
+
+
+def records_digest(records: "Dict[str, np.ndarray] | Sequence[np.ndarray]") -> int:
+    """Digest of a shard's records in trace order (graph inputs first, then ops)."""
+    arrays = list(records.values()) if isinstance(records, dict) else list(records)
+    per = np.array([digest_bytes(np.ascontiguousarray(a).reshape(-1).view(np.uint8)) for a in arrays],
+                   dtype=np.uint64)
+    return digest_bytes(per.tobytes())
+
+
+def trace_file_digest(path_or_bytes) -> int:
+    return records_digest(read_trace(path_or_bytes).records)

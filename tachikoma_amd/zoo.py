@@ -51,6 +51,17 @@ class Model:
             shape[0] = batch
         return rng.integers(-128, 128, size=shape, dtype=np.int64).astype(self.input_dtype)
 
+    def sample_inputs(self, offset: int, count: int, seed: Optional[int] = None) -> np.ndarray:
+        """Samples [offset, offset+count) of the global synthetic batch; sample i depends only
+        on (seed, i), so a shard's content does not depend on how the batch is split."""
+        base = self.seed + 1000 if seed is None else seed
+        shape = list(self.input_shape)
+        shape[0] = 1
+        out = [np.random.default_rng([base, offset + i]).integers(-128, 128, size=shape, dtype=np.int64)
+               for i in range(count)]
+        return np.concatenate(out, axis=0).astype(self.input_dtype) if out else \
+            np.zeros([0] + shape[1:], self.input_dtype)
+
 
 class _Builder:
     def __init__(self, seed: int):

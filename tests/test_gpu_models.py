@@ -84,3 +84,23 @@ def test_resnet50_full_shard_sampled(device, tmp_path):
         if not np.array_equal(got, e):
             bad = np.argwhere(got != e)[0]
             raise AssertionError(f"{name} mismatch at {tuple(bad)}")
+    # determinism: a second traced run gives the same device record digest
+    d1 = m.trace_digest()
+    m.run(trace=True)
+    cap.synchronize()
+    assert m.trace_digest() == d1
+
+
+@pytest.mark.parametrize("name,batch", [("lenet5", 3), ("resnet18", 2)])
+def test_device_digest_matches_trace_file(device, tmp_path, name, batch):
+    """tk_digest_bytes over the HBM records == the host twin over the dumped trace file,
+    and equals the digest of the oracle's records (the multi-GPU manifest pins shards by it)."""
+    from tachikoma_amd import trace_format as tf
+    model = zoo.MODELS[name](batch=batch)
+    x = model.sample_inputs(0, batch)
+    m, tr = _run_trace(model, x, tmp_path)
+    d = m.trace_digest()
+    assert d == tf.trace_file_digest(str(tmp_path / f"{model.name}.tkt"))
+    exp = graph_ref.calibrate(model.mod, model.params, {"data": x}, backend="c")
+    ordered = {k: exp[k] for k in tr.records}
+    assert d == tf.records_digest(ordered)

@@ -1,53 +1,84 @@
-"""Summarise rocprofv3 PMC passes (tools/pmc.sh) per dispatch of the block kernel, in launch order.
-FETCH_SIZE is doubled (gfx950 reports half the bytes of wide streaming reads, MI355X_MICROARCH.md §HBM);
-FETCH_SIZE/WRITE_SIZE are in KiB."""
+"""Summarise rocprofv3 PMC passes (tools/pmc.sh) for the fused layer-block kernel.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are KiB; on
+gfx950 FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so it
+is doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  The last
+``launches`` dispatches of each pass are one step (the bench runs warmup + steps
+with the same node list).
+
+usage: python tools/pmc_summary.py <pmc outdir> [launches] [--json out.json]
+"""
+import argparse
 import csv
 import glob
+import json
 import os
-import sys
 from collections import defaultdict
+
+KIB = 1024
 
 
 def load(d):
-    per = defaultdict(dict)   # dispatch -> counter -> value
+    per = defaultdict(dict)   # (pass, dispatch) -> counter -> value
     meta = {}
-    for f in glob.glob(os.path.join(d, "pass*/run_counter_collection.csv")):
-        p = f.split("/")[-2]
-        rows = list(csv.DictReader(open(f)))
-        for r in rows:
+    for f in glob.glob(os.path.join(d, "pass*/**/*counter_collection.csv"), recursive=True):
+        p = os.path.relpath(f, d).split(os.sep)[0]
+        for r in csv.DictReader(open(f)):
             key = (p, int(r["Dispatch_Id"]))
-            per[key][r["Counter_Name"]] = float(r["Counter_Value"])
-            meta[key] = (r["Kernel_Name"], int(r["Grid_Size"]), int(r["VGPR_Count"]), int(r["Accum_VGPR_Count"]),
-                         int(r["LDS_Block_Size"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            meta[key] = {"kernel": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),
+                         "agpr": int(r.get("Accum_VGPR_Count", 0) or 0), "lds": int(r["LDS_Block_Size"])}
     return per, meta
 
 
-def main(d, last_n=54):
+def summarise(d, launches):
     per, meta = load(d)
     passes = sorted({k[0] for k in per})
-    out = defaultdict(dict)
+    steps = defaultdict(dict)
     for p in passes:
-        keys = sorted(k for k in per if k[0] == p)[-last_n:]
+        keys = sorted(k for k in per if k[0] == p)[-launches:]
         for i, k in enumerate(keys):
-            out[i].update(per[k])
-            out[i]["_meta"] = meta[k]
+            steps[i].update(per[k])
+            steps[i]["_meta"] = meta[k]
     tot = defaultdict(float)
-    for i in sorted(out):
-        for c, v in out[i].items():
+    for i in steps:
+        for c, v in steps[i].items():
             if c != "_meta":
                 tot[c] += v
-    print("per-step totals over", len(out), "dispatches:")
-    for c in sorted(tot):
-        v = tot[c]
-        if c == "FETCH_SIZE":
-            print(f"  {c:24s} {v * 2 / 1e6:10.3f} GB (x2 gfx950 correction)")
-        elif c == "WRITE_SIZE":
-            print(f"  {c:24s} {v / 1e6:10.3f} GB")
-        else:
-            print(f"  {c:24s} {v:14.0f}")
-    m0 = out[0]["_meta"]
-    print("example dispatch:", m0)
+    n = len(steps)
+    fetch = tot.get("FETCH_SIZE", 0.0) * KIB * 2
+    write = tot.get("WRITE_SIZE", 0.0) * KIB
+    out = {"launches_per_step": n,
+           "fetch_bytes_per_step": fetch, "write_bytes_per_step": write,
+           "hbm_bytes_per_step": fetch + write,
+           "hbm_bytes_per_launch": (fetch + write) / max(n, 1),
+           "correction": "FETCH_SIZE x2 (gfx950 wide reads), KiB -> bytes",
+           "counters_per_step": {c: v for c, v in sorted(tot.items())},
+           "example_dispatch": steps[0]["_meta"] if n else None}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("launches", type=int, nargs="?", default=54)
+    ap.add_argument("--json")
+    ap.add_argument("--workload", default="", help="extra bench args the passes ran with")
+    a = ap.parse_args()
+    s = summarise(a.dir, a.launches)
+    wl = a.workload.split()
+    s["bench_args"] = wl
+    s["model"] = wl[wl.index("--model") + 1] if "--model" in wl else "resnet50"
+    s["batch"] = int(wl[wl.index("--batch") + 1]) if "--batch" in wl else 64
+    print(f"per-step totals over {s['launches_per_step']} dispatches:")
+    print(f"  HBM fetch {s['fetch_bytes_per_step'] / 1e9:.3f} GB (x2 corrected), write "
+          f"{s['write_bytes_per_step'] / 1e9:.3f} GB, per launch {s['hbm_bytes_per_launch'] / 1e6:.2f} MB")
+    for c, v in s["counters_per_step"].items():
+        print(f"  {c:24s} {v:16.0f}")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(s, f, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 54)
+    main()
