@@ -156,6 +156,14 @@ typedef struct {
   int64_t clip_min, clip_max;
 } tk_block_attrs;
 
+/* A fused residual join: qnn.add [→ clip].  One kernel writes both records and,
+ * optionally, the NHWC int8 shadow of the last output for the next MFMA conv. */
+typedef struct {
+  tk_qnn_add_attrs add;
+  int32_t has_clip;
+  int64_t clip_min, clip_max;
+} tk_add_block_attrs;
+
 typedef struct {
   int32_t pool_size[2];
   int32_t strides[2];
@@ -209,6 +217,12 @@ int tk_requantize(const tk_tensor* data, tk_tensor* out, const tk_requantize_att
 int tk_qnn_add(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const tk_qnn_add_attrs* attrs,
                void* stream);
 /* nn.bias_add / add with a broadcast vector along `axis` (int32 wraps). */
+/* Fused qnn.add [→ clip] on 8-bit tensors (add.cc:40-96 + clip, python/tvm/topi/math.py:615-640).
+ * outs = {add, [clip]}.  shadow_out (optional): NHWC [N][H][W][ceil16(C)] int8 copy of the
+ * last output (uint8 stored xor 0x80, padded channels written as 0); needs 4-D NCHW operands. */
+int tk_qnn_add_block(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* const* outs, int n_outs,
+                     const tk_add_block_attrs* attrs, void* shadow_out, void* stream);
+
 int tk_bias_add(const tk_tensor* data, const tk_tensor* bias, tk_tensor* out, int axis, void* stream);
 /* clip: max(min(x, a_max), a_min) with bounds already cast to the dtype. */
 int tk_clip(const tk_tensor* data, tk_tensor* out, int64_t a_min, int64_t a_max, void* stream);
@@ -241,6 +255,7 @@ enum {
   TK_NODE_SHADOW = 12,     /* NCHW→NHWC int8 shadow for a conv input (not traced) */
   TK_NODE_CONV_BLOCK = 13, /* in: data, weight, bias; outs: 3-4; ext: shadow, packed, weight_sums, patch_sums, shadow_out */
   TK_NODE_DENSE_BLOCK = 14,/* in: data, weight, bias; outs: 3-4; ext: workspace */
+  TK_NODE_ADD_BLOCK = 15,  /* in: lhs, rhs; outs: 1-2 (add, clip); ext[4]: shadow_out */
 };
 
 #define TK_MAX_NODE_OUTPUTS 4
@@ -259,6 +274,7 @@ typedef struct {
     tk_qnn_add_attrs qnn_add;
     tk_pool2d_attrs pool2d;
     tk_block_attrs block;
+    tk_add_block_attrs add_block;
     struct { int64_t a_min, a_max; } clip;
     struct { int32_t axis; } bias_add;
   } attrs;

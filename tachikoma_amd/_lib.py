@@ -96,6 +96,15 @@ class tk_block_attrs(ctypes.Structure):
     ]
 
 
+class tk_add_block_attrs(ctypes.Structure):
+    _fields_ = [
+        ("add", tk_qnn_add_attrs),
+        ("has_clip", ctypes.c_int32),
+        ("clip_min", ctypes.c_int64),
+        ("clip_max", ctypes.c_int64),
+    ]
+
+
 class tk_pool2d_attrs(ctypes.Structure):
     _fields_ = [
         ("pool_size", ctypes.c_int32 * 2),
@@ -122,6 +131,7 @@ class tk_node_attrs(ctypes.Union):
         ("qnn_add", tk_qnn_add_attrs),
         ("pool2d", tk_pool2d_attrs),
         ("block", tk_block_attrs),
+        ("add_block", tk_add_block_attrs),
         ("clip", _clip),
         ("bias_add", _bias_add),
     ]
@@ -157,7 +167,7 @@ TK_ROUND_UPWARD, TK_ROUND_TONEAREST = 0, 1
 NODE_KINDS = {
     "qnn.conv2d": 1, "qnn.dense": 2, "qnn.requantize": 3, "nn.bias_add": 4, "clip": 5, "cast": 6,
     "qnn.add": 7, "nn.max_pool2d": 8, "nn.avg_pool2d": 9, "nn.global_avg_pool2d": 10, "copy": 11, "shadow": 12,
-    "conv_block": 13, "dense_block": 14,
+    "conv_block": 13, "dense_block": 14, "add_block": 15,
 }
 MAX_NODE_OUTPUTS = 4
 
@@ -187,6 +197,8 @@ SIGNATURES = {
                                           ctypes.POINTER(tk_block_attrs), _VP, _VP]),
     "tk_requantize": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_requantize_attrs), _VP]),
     "tk_qnn_add": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_qnn_add_attrs), _VP]),
+    "tk_qnn_add_block": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(_PT), ctypes.c_int,
+                                        ctypes.POINTER(tk_add_block_attrs), _VP, _VP]),
     "tk_bias_add": (ctypes.c_int, [_PT, _PT, _PT, ctypes.c_int, _VP]),
     "tk_clip": (ctypes.c_int, [_PT, _PT, _I64, _I64, _VP]),
     "tk_cast": (ctypes.c_int, [_PT, _PT, _VP]),

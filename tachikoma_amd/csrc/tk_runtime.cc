@@ -20,6 +20,8 @@ int bias_add_impl(const tk_tensor* x, const tk_tensor* b, tk_tensor* y, int axis
 int clip_impl(const tk_tensor* x, tk_tensor* y, int64_t lo, int64_t hi, hipStream_t s);
 int cast_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
 int qnn_add_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* y, const tk_qnn_add_attrs* at, hipStream_t s);
+int add_block_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* const* outs, int n_outs,
+                   const tk_add_block_attrs* at, void* shadow, hipStream_t s);
 int max_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s);
 int avg_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s);
 int global_avg_pool_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
@@ -94,6 +96,8 @@ static int run_node(Node& n, hipStream_t s) {
       return cast_impl(i0, o, s);
     case TK_NODE_QNN_ADD:
       return qnn_add_impl(i0, i1, o, &d.attrs.qnn_add, s);
+    case TK_NODE_ADD_BLOCK:
+      return add_block_impl(i0, i1, n.outp, d.n_outputs, &d.attrs.add_block, d.ext[4], s);
     case TK_NODE_MAX_POOL2D:
       return max_pool_impl(i0, o, &d.attrs.pool2d, s);
     case TK_NODE_AVG_POOL2D:
@@ -168,6 +172,10 @@ int tk_qnn_dense_block(const tk_tensor* data, const tk_tensor* weight, const tk_
 }
 int tk_requantize(const tk_tensor* data, tk_tensor* out, const tk_requantize_attrs* attrs, void* stream) {
   return tk::requantize_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_add_block(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* const* outs, int n_outs,
+                     const tk_add_block_attrs* attrs, void* shadow_out, void* stream) {
+  return tk::add_block_impl(lhs, rhs, outs, n_outs, attrs, shadow_out, tk::as_stream(stream));
 }
 int tk_qnn_add(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const tk_qnn_add_attrs* attrs,
                void* stream) {

@@ -295,9 +295,9 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
 @dataclass
 class ExecGroup:
     """One device node: a single op, or a fused layer block
-    ``qnn.conv2d|qnn.dense → nn.bias_add → qnn.requantize [→ clip|nn.relu]`` whose every op
-    output is still written (and traced) separately."""
-    kind: str            # op name, "conv_block" or "dense_block"
+    ``qnn.conv2d|qnn.dense → nn.bias_add → qnn.requantize [→ clip|nn.relu]`` or residual join
+    ``qnn.add [→ clip|nn.relu]`` whose every op output is still written (and traced) separately."""
+    kind: str            # op name, "conv_block", "dense_block" or "add_block"
     ops: List[PlanOp]
 
     @property
@@ -340,6 +340,16 @@ def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
                     taken.add(c.name)
                 groups.append(ExecGroup("conv_block" if op.op == "qnn.conv2d" else "dense_block", chain))
                 continue
+        if fuse and op.op == "qnn.add" and op.out.dtype in ("int8", "uint8") and \
+                all(plan.tensor(x).shape == op.out.shape for x in op.inputs[:2]):
+            chain = [op]
+            cl = first_consumer(op, ("clip", "nn.relu"))
+            if cl is not None:
+                chain.append(cl)
+            for c in chain:
+                taken.add(c.name)
+            groups.append(ExecGroup("add_block", chain))
+            continue
         taken.add(op.name)
         groups.append(ExecGroup(op.op, [op]))
     return groups

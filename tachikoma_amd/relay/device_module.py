@@ -12,7 +12,8 @@ Memory layout in HBM (one GPU, one batch shard):
     a shadow node right before the first conv that reads it.
 
 Nodes: one per ExecGroup (build_module.exec_groups) — a fused conv/dense layer
-block writes all of its ops' outputs (each a separate trace record) from one kernel.
+block or residual (qnn.add → clip) block writes all of its ops' outputs (each a
+separate trace record) from one kernel.
 """
 from __future__ import annotations
 
@@ -177,6 +178,18 @@ class DeviceModule:
                     n.kind = _lib.NODE_KINDS["dense_block"]
                     self._dense_attrs(ba.dense, head)
                     n.ext[0] = self._scratch(self.lib.tk_qnn_dense_workspace_bytes(ins[0].ptr, ins[1].ptr)).data_ptr()
+            elif g.kind == "add_block":
+                n.kind = _lib.NODE_KINDS["add_block"]
+                ins = [self._ref(x) for x in head.inputs[:2]]
+                outs = [self._ref(o.name) for o in g.ops]
+                ab = n.attrs.add_block
+                _fill_qnn_add(ab.add, head.attrs)
+                if len(g.ops) == 2:
+                    ab.has_clip = 1
+                    ab.clip_min, ab.clip_max = g.ops[1].attrs["lo"], g.ops[1].attrs["hi"]
+                if g.last.name in shadow_bufs and len(head.out.shape) == 4:
+                    n.ext[4] = shadow_bufs[g.last.name].data_ptr()
+                    shadow_ready.add(g.last.name)
             else:
                 op = head
                 kind = op.op
@@ -196,18 +209,7 @@ class DeviceModule:
                     self._fill_rq(n.attrs.requantize, op)
                 elif kind == "qnn.add":
                     n.kind = _lib.NODE_KINDS["qnn.add"]
-                    qa = n.attrs.qnn_add
-                    for side in ("lhs", "rhs"):
-                        r = getattr(qa, side)
-                        r.mode = a[f"{side}_mode"]
-                        r.axis = -1
-                        r.multiplier = a[f"{side}_multiplier"]
-                        r.shift = a[f"{side}_shift"]
-                        r.input_zero_point = a[f"{side}_zero_point"]
-                        r.output_zero_point = a["output_zero_point"]
-                    qa.output_zero_point = a["output_zero_point"]
-                    qa.lhs_upcast = a["lhs_upcast"]
-                    qa.rhs_upcast = a["rhs_upcast"]
+                    _fill_qnn_add(n.attrs.qnn_add, a)
                 elif kind == "nn.bias_add":
                     n.kind = _lib.NODE_KINDS["nn.bias_add"]
                     n.attrs.bias_add.axis = a["axis"]
@@ -341,6 +343,21 @@ class DeviceModule:
 
     def output(self, name: str):
         return self.buffers[name]
+
+
+def _fill_qnn_add(qa, a) -> None:
+    """tk_qnn_add_attrs from a lowered qnn.add (per-tensor RequantizeOrUpcast per side)."""
+    for side in ("lhs", "rhs"):
+        r = getattr(qa, side)
+        r.mode = a[f"{side}_mode"]
+        r.axis = -1
+        r.multiplier = a[f"{side}_multiplier"]
+        r.shift = a[f"{side}_shift"]
+        r.input_zero_point = a[f"{side}_zero_point"]
+        r.output_zero_point = a["output_zero_point"]
+    qa.output_zero_point = a["output_zero_point"]
+    qa.lhs_upcast = a["lhs_upcast"]
+    qa.rhs_upcast = a["rhs_upcast"]
 
 
 def _as_torch_device(dev):

@@ -155,6 +155,40 @@ def test_qnn_add_random(tk):
         np.testing.assert_array_equal(tk.qnn_add(a, b, *params), ref.qnn_add(a, b, *params))
 
 
+ADD_BLOCK_CASES = [
+    # shape, dtype, (ls, lz, rs, rz, os, oz), clip, shadow
+    ((2, 64, 56, 56), "int8", (0.05, 3, 0.07, -2, 0.09, 1), (1, 127), True),     # HW % 16 == 0, 16-byte path
+    ((3, 80, 14, 14), "int8", (0.05, 3, 0.05, 3, 0.05, 3), (3, 127), True),      # HW % 4 == 0, C % 64 != 0
+    ((2, 40, 7, 7), "uint8", (0.125, 130, 0.5, 120, 0.25, 128), (128, 255), True),  # HW odd, uint8 xor shadow
+    ((2, 24, 9, 9), "int8", (0.02, 0, 0.3, 5, 0.1, -4), None, True),             # no clip: shadow of the add
+    ((5, 1000), "int8", (0.05, 3, 0.07, -2, 0.09, 1), (-20, 100), False),        # 2-D, flat view
+    ((1, 7, 3, 5), "uint8", (1.0, 0, 1.0, 0, 1.0, 0), None, False),             # both upcast, odd size
+]
+
+
+@pytest.mark.parametrize("case", ADD_BLOCK_CASES, ids=[f"addblock{i}" for i in range(len(ADD_BLOCK_CASES))])
+def test_qnn_add_block(tk, case):
+    shape, dt, params, clip, want_shadow = case
+    rng = np.random.default_rng(len(shape) * 31 + shape[1])
+    a = _rand(rng, shape, dt)
+    b = _rand(rng, shape, dt)
+    outs = tk.qnn_add_block(a, b, *params, clip=clip, want_shadow=want_shadow)
+    add = ref.qnn_add(a, b, *params)
+    np.testing.assert_array_equal(outs[0], add)
+    last = add
+    if clip is not None:
+        last = ref.clip(add, *clip)
+        np.testing.assert_array_equal(outs[1], last)
+    if want_shadow:
+        shadow = outs[-1]
+        c = shape[1]
+        nhwc = np.transpose(last, (0, 2, 3, 1))
+        view = shadow[..., :c].view(np.int8)
+        expect = (nhwc.view(np.uint8) ^ 0x80).view(np.int8) if dt == "uint8" else nhwc.view(np.int8)
+        np.testing.assert_array_equal(view, expect)
+        assert not shadow[..., c:].any()
+
+
 def test_elementwise_random(tk):
     rng = np.random.default_rng(9)
     x32 = rng.integers(-2**31, 2**31, size=(3, 5, 7, 3), dtype=np.int64).astype(np.int32)

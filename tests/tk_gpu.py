@@ -119,6 +119,14 @@ def requantize(x, input_scale, input_zero_point, output_scale, output_zero_point
 def qnn_add(lhs, rhs, ls, lz, rs, rz, os_, oz):
     lib = _lib.load()
     a = _lib.tk_qnn_add_attrs()
+    _add_attrs(a, ls, lz, rs, rz, os_, oz)
+    ld, rd = dev(lhs), dev(rhs)
+    out = empty(lhs.shape, str(lhs.dtype))
+    _sync_check(lib.tk_qnn_add(ref(ld).ptr, ref(rd).ptr, ref(out).ptr, ctypes.byref(a), stream()), "tk_qnn_add")
+    return out.cpu().numpy()
+
+
+def _add_attrs(a, ls, lz, rs, rz, os_, oz):
     for side, s, z in (("lhs", ls, lz), ("rhs", rs, rz)):
         r = getattr(a, side)
         up = np.float32(s).tobytes() == np.float32(os_).tobytes() and int(z) == int(oz)
@@ -129,10 +137,35 @@ def qnn_add(lhs, rhs, ls, lz, rs, rz, os_, oz):
         r.input_zero_point = int(z)
         r.output_zero_point = int(oz)
     a.output_zero_point = int(oz)
+
+
+def qnn_add_block(lhs, rhs, ls, lz, rs, rz, os_, oz, clip=None, want_shadow=False):
+    """Fused qnn.add [-> clip] through tk_qnn_add_block; returns [add, (clip), (shadow)]."""
+    lib = _lib.load()
+    a = _lib.tk_add_block_attrs()
+    _add_attrs(a.add, ls, lz, rs, rz, os_, oz)
+    if clip is not None:
+        a.has_clip = 1
+        a.clip_min, a.clip_max = clip
     ld, rd = dev(lhs), dev(rhs)
-    out = empty(lhs.shape, str(lhs.dtype))
-    _sync_check(lib.tk_qnn_add(ref(ld).ptr, ref(rd).ptr, ref(out).ptr, ctypes.byref(a), stream()), "tk_qnn_add")
-    return out.cpu().numpy()
+    outs = [empty(lhs.shape, str(lhs.dtype))]
+    if clip is not None:
+        outs.append(empty(lhs.shape, str(lhs.dtype)))
+    shadow = None
+    if want_shadow:
+        torch = _torch()
+        n, c, h, w = lhs.shape
+        # poisoned: the kernel must write every byte incl. the padded channels
+        shadow = torch.full((n, h, w, (c + 15) // 16 * 16), 0x5A, dtype=torch.uint8, device="cuda")
+    refs = [ref(t) for t in outs]
+    arr = (ctypes.POINTER(_lib.tk_tensor) * len(refs))(*[r.ptr for r in refs])
+    _sync_check(lib.tk_qnn_add_block(ref(ld).ptr, ref(rd).ptr, arr, len(refs), ctypes.byref(a),
+                                     ctypes.c_void_p(shadow.data_ptr()) if shadow is not None else None, stream()),
+                "tk_qnn_add_block")
+    res = [t.cpu().numpy() for t in outs]
+    if shadow is not None:
+        res.append(shadow.cpu().numpy())
+    return res
 
 
 def unary(name, x, out_dtype=None, *extra):
