@@ -28,8 +28,7 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 
 constexpr int kBK = 64;          // bytes of K per stage
 constexpr int kGemmThreads = 256;
-constexpr int kEpiRows = 32;     // epilogue chunk: 32 rows x 128 columns of int32 in LDS
-constexpr int kEpiStride = 132;  // dwords per LDS row (128 + 4: breaks the 64-bank period)
+constexpr int kEpiStride = 132;  // dwords per LDS row of the epilogue tile (128 + 4: breaks the 64-bank period)
 
 struct GemmArgs {
   const int8_t* A;     // [rowsA_pad][lda]
@@ -62,7 +61,9 @@ struct GemmArgs {
   int32_t has_clip, clip_lo, clip_hi, shadow_cpad;
   uint32_t shadow_xor;  // 0x80 when the block output is uint8 (shadow stores int8 = u8 ^ 0x80)
   int32_t ch_is_row;    // channel index = row (conv: Cout) or column (dense: units)
-  int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue
+  int32_t vecw;         // epilogue store vector (4 or 1 elements): divides the plane / row length
+  int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
+                       // 8/16/32/64 skip the conv / bias_add / requantize / clip record
 };
 
 // Writes one element of every output of a fused block.  Mirrors, per element:
@@ -85,6 +86,77 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, int64_t off, i
   if (g.shadow_out) g.shadow_out[pix * g.shadow_cpad + ch] = (uint8_t)((uint32_t)last ^ g.shadow_xor);
 }
 
+__device__ __forceinline__ uint32_t pack4(const int32_t* x) {
+  return (uint32_t)(x[0] & 0xFF) | ((uint32_t)(x[1] & 0xFF) << 8) | ((uint32_t)(x[2] & 0xFF) << 16) |
+         ((uint32_t)x[3] << 24);
+}
+
+// Per-row constants of the fused epilogue (one output channel per row for conv
+// blocks), staged once per tile in LDS: 32 bytes, read back with two ds_read_b128.
+struct EpiRow {
+  uint32_t fold;  // K·zA·zB − zB·RA[row]: the whole zero-point correction when zB and RB are uniform/absent
+  uint32_t ra, za;
+  int32_t bias, m, s, zp, pad;
+};
+
+template <int V>
+__device__ __forceinline__ void st_i32(int32_t* dst, const int32_t* v) {
+  if constexpr (V == 4) *reinterpret_cast<v4i*>(dst) = v4i{v[0], v[1], v[2], v[3]};
+  else *dst = v[0];
+}
+
+template <int V>
+__device__ __forceinline__ void st_i8(uint8_t* dst, const int32_t* v) {
+  if constexpr (V == 4) *reinterpret_cast<uint32_t*>(dst) = pack4(v);
+  else *dst = (uint8_t)v[0];
+}
+
+// V consecutive columns of one row after zero-point folding: stores each record as
+// soon as it is complete, transforming v in place (conv → bias_add → requantize →
+// clip); mirrors nn.bias_add (int32 wrap), RequantizeLowerInt + clip/cast
+// (src/relay/qnn/op/requantize.cc:195-273) and clip (python/tvm/topi/math.py:615-640).
+template <int V, bool kBlock>
+__device__ __forceinline__ void epi_apply(const GemmArgs& g, const EpiRow& r, int32_t* v, int64_t off, bool st,
+                                          int col) {
+  if (st && !(g.ablate & 8)) st_i32<V>(g.C + off, v);
+  if (!kBlock) return;
+  const int qmin = (int)g.rq.qmin, qmax = (int)g.rq.qmax;
+  if (g.ch_is_row) {
+#pragma unroll
+    for (int q = 0; q < V; ++q) v[q] = (int32_t)((uint32_t)v[q] + (uint32_t)r.bias);
+    if (st && !(g.ablate & 16)) st_i32<V>(g.bias_out + off, v);
+    const int mode = g.rq.mode;
+    if (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD) {
+#pragma unroll
+      for (int q = 0; q < V; ++q) v[q] = qms_upward((int32_t)((uint32_t)v[q] - (uint32_t)r.zp), r.m, r.s);
+    } else if (mode == TK_RQ_TENSOR_POW2) {
+#pragma unroll
+      for (int q = 0; q < V; ++q) v[q] = qms_pow2((int32_t)((uint32_t)v[q] - (uint32_t)r.zp), r.s);
+    } else if (mode == TK_RQ_IDENTITY) {
+#pragma unroll
+      for (int q = 0; q < V; ++q) v[q] = (int32_t)((uint32_t)v[q] - (uint32_t)r.zp);
+    } else {
+#pragma unroll
+      for (int q = 0; q < V; ++q) v[q] = qms_tonearest((int32_t)((uint32_t)v[q] - (uint32_t)r.zp), r.m, r.s);
+    }
+#pragma unroll
+    for (int q = 0; q < V; ++q) v[q] = min(max((int32_t)((uint32_t)g.rq.zp_out + (uint32_t)v[q]), qmin), qmax);
+  } else {
+    // channel = column (dense blocks)
+#pragma unroll
+    for (int q = 0; q < V; ++q) v[q] = (int32_t)((uint32_t)v[q] + (uint32_t)g.bias[col + q]);
+    if (st && !(g.ablate & 16)) st_i32<V>(g.bias_out + off, v);
+#pragma unroll
+    for (int q = 0; q < V; ++q) v[q] = min(max(rq_apply(v[q], col + q, g.rq), qmin), qmax);
+  }
+  if (st && !(g.ablate & 32)) st_i8<V>(g.rq_out + off, v);
+  if (g.has_clip) {
+#pragma unroll
+    for (int q = 0; q < V; ++q) v[q] = min(max(v[q], g.clip_lo), g.clip_hi);
+    if (st && !(g.ablate & 64)) st_i8<V>(g.clip_out + off, v);
+  }
+}
+
 // Workgroup barrier that only drains this wave's LDS traffic.  __syncthreads() also waits
 // vmcnt(0), i.e. for every outstanding global store of the epilogue to complete, which
 // serialises the store latency once per barrier; the epilogue's barriers only order LDS.
@@ -95,13 +167,13 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * kBK + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
 template <int MT, bool kIm2col, bool kBlock>
-__global__ __launch_bounds__(kGemmThreads) void gemm_i8_kernel(GemmArgs g) {
+__global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(GemmArgs g) {
   constexpr int BM = 64 * MT;   // rows of A per block (2 waves along M, MT 32-row tiles each)
   constexpr int BN = 128;       // rows of B per block (2 waves along N, 2 32-col tiles each)
   constexpr int A_CHUNKS = BM * kBK / 16 / kGemmThreads;  // 16-byte loads per thread per stage
   constexpr int B_CHUNKS = BN * kBK / 16 / kGemmThreads;
   constexpr int kStage = 2 * (BM + BN) * kBK;
-  constexpr int kEpi = kEpiRows * kEpiStride * 4;
+  constexpr int kEpi = BM * kEpiStride * 4 + BM * (int)sizeof(EpiRow);
   __shared__ __attribute__((aligned(16))) int8_t smem[kStage > kEpi ? kStage : kEpi];
   int8_t* As = smem;
   int8_t* Bs = smem + 2 * BM * kBK;
@@ -229,184 +301,125 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_i8_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  // ---- epilogue, staged through LDS 32 rows at a time:
-  //  (1) the two waves owning the chunk dump their raw accumulators to LDS [row][col]
-  //      (no loads, no branches: everything per-row/per-column happens in (2));
-  //  (2) every thread takes 4 consecutive columns of one row: zero-point folding, then
-  //      16-byte int32 stores for the conv / bias_add records and 4-byte stores for
-  //      requantize / clip (NCHW: consecutive pixels of one channel are contiguous); it
-  //      overwrites its LDS slot with the block's final int8 values;
-  //  (3) the NHWC shadow for the next conv: each thread gathers 16 channels of one pixel
-  //      (a wave reads 64 consecutive columns per row: conflict-free) into one 16-byte store.
-  // Per-row constants are loaded at the top of each chunk (latency hidden by (1)); all
-  // optional operands are guarded by uniform flags so the waitcnt pass sees straight code.
+  // ---- epilogue: the whole BM x BN accumulator tile is staged through LDS.
+  //  (1) every wave dumps its raw accumulators to LDS [row][col]; threads < BM stage their
+  //      row's constants (bias, multiplier, shift, zero points, fold term) next to it;
+  //  (2) every thread owns fixed columns (4 consecutive ones when the plane length is a
+  //      multiple of 4, else 1) and walks rows: per row, zero-point folding, then each record
+  //      is stored as soon as it is complete.  The lanes of a wave run along the columns, so
+  //      every store instruction writes whole 128-byte lines of one or two rows (int32: 16 B
+  //      per lane, int8: 4 B per lane); the final int8 values go back to the LDS slot;
+  //  (3) the NHWC shadow for the next conv: each item gathers 16 channels of one pixel
+  //      (a wave reads 64 consecutive columns per row: conflict-free) into a 16 B store.
   if (g.ablate & 4) return;
-  lds_barrier();  // staging buffers are free
   int32_t* tileI = reinterpret_cast<int32_t*>(smem);
+  EpiRow* rowc = reinterpret_cast<EpiRow*>(smem + BM * kEpiStride * 4);
   const int hw = g.OH * g.OW;
-  const bool has_ra = g.RA != nullptr, has_rb = g.RB != nullptr;
-  const bool za_vec = g.zA_vec != nullptr, zb_vec = g.zB_vec != nullptr;
-  const uint32_t keff = (uint32_t)g.k_eff;
+  const bool zb_vec = g.zB_vec != nullptr, has_rb = g.RB != nullptr;
+  const bool simple_fold = !zb_vec && !has_rb;
+  lds_barrier();  // staging buffers are free
+  if (tid < BM) {
+    const int row = min(m0 + tid, g.M - 1);
+    EpiRow r{};
+    r.ra = g.RA ? (uint32_t)g.RA[row] : 0u;
+    r.za = g.zA_vec ? (uint32_t)g.zA_vec[row] : (uint32_t)g.zA;
+    r.fold = (uint32_t)g.k_eff * r.za * (uint32_t)g.zB - (uint32_t)g.zB * r.ra;
+    if (kBlock && g.ch_is_row) {
+      r.bias = g.bias[row];
+      const bool axis = g.rq.mode >= TK_RQ_AXIS_UPWARD;
+      r.m = axis ? g.rq.ms[row] : g.rq.multiplier;
+      r.s = axis ? g.rq.ss[row] : g.rq.shift;
+      r.zp = g.rq.zps ? g.rq.zps[row] : g.rq.zp_in;
+    }
+    rowc[tid] = r;
+  }
 #pragma unroll
-  for (int c = 0; c < MT * 2; ++c) {
-    // per-row constants of the 4 rows this thread processes in this chunk
-    uint32_t kra[4], kza[4];
-    int32_t kb[4], km[4], ks[4], kz[4];
+  for (int i = 0; i < MT; ++i) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int row = m0 + c * 32 + ((tid + kGemmThreads * k) >> 5);
-      const int rowc = row < g.M ? row : 0;
-      kra[k] = has_ra ? (uint32_t)g.RA[rowc] : 0u;
-      kza[k] = za_vec ? (uint32_t)g.zA_vec[rowc] : (uint32_t)g.zA;
-      kb[k] = km[k] = ks[k] = kz[k] = 0;
-      if (kBlock && g.ch_is_row) {
-        kb[k] = g.bias[rowc];
-        const bool axis = g.rq.mode >= TK_RQ_AXIS_UPWARD;
-        km[k] = axis ? g.rq.ms[rowc] : g.rq.multiplier;
-        ks[k] = axis ? g.rq.ss[rowc] : g.rq.shift;
-        kz[k] = g.rq.zps ? g.rq.zps[rowc] : g.rq.zp_in;
+    for (int j = 0; j < 2; ++j) {
+      const int lc = wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int lr = wm * 32 * MT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        tileI[lr * kEpiStride + lc] = acc[i][j][r];
       }
     }
-    if (wm == c / MT) {
-      const int i = c % MT;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int lc = wn * 64 + j * 32 + (lane & 31);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int lr = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          tileI[lr * kEpiStride + lc] = acc[i][j][r];
-        }
+  }
+  lds_barrier();
+
+  // zero-point folding of V columns: acc - zB[col]*RA[row] - zA[row]*RB[col] + K*zA[row]*zB[col]
+  auto fold = [&](int32_t* v, const EpiRow& r, int col, int V) {
+    if (simple_fold) {
+      for (int q = 0; q < V; ++q) v[q] = (int32_t)((uint32_t)v[q] + r.fold);
+    } else {
+      for (int q = 0; q < V; ++q) {
+        const int cq = min(col + q, g.N - 1);
+        const uint32_t zb = zb_vec ? (uint32_t)g.zB_vec[cq] : (uint32_t)g.zB;
+        const uint32_t rb = has_rb ? (uint32_t)g.RB[cq] : 0u;
+        v[q] = (int32_t)((uint32_t)v[q] - zb * r.ra - r.za * rb + (uint32_t)g.k_eff * r.za * zb);
       }
     }
+  };
+  const bool store_on = !(g.ablate & 2);
+  if (g.vecw >= 4) {
+    // 4 consecutive columns x rows (tid>>5) + 8k; the 4 never straddle an image plane
+    const int c4 = (tid & 31) * 4;
+    const int col = n0 + c4;
+    const bool colok = col < g.N;
+    int64_t cbase, rstride;
+    if (g.out_nchw) {
+      const int img = col / hw;
+      cbase = (int64_t)img * g.M * hw + (col - img * hw);
+      rstride = hw;
+    } else {
+      cbase = col;
+      rstride = g.ldc;
+    }
+#pragma unroll 2
+    for (int k = 0; k < BM / 8; ++k) {
+      const int lr = (tid >> 5) + 8 * k;
+      const int row = m0 + lr;
+      const EpiRow r = rowc[lr];
+      int32_t* slot = tileI + lr * kEpiStride + c4;
+      const v4i t = *reinterpret_cast<const v4i*>(slot);
+      int32_t v[4] = {t.x, t.y, t.z, t.w};
+      fold(v, r, col, 4);
+      epi_apply<4, kBlock>(g, r, v, cbase + (int64_t)row * rstride, store_on && colok && row < g.M, col);
+      if (kBlock && g.shadow_out) *reinterpret_cast<v4i*>(slot) = v4i{v[0], v[1], v[2], v[3]};
+    }
+  } else {
+    // one column x rows (tid>>7) + 2k (planes whose length is not a multiple of 4)
+    const int lc = tid & (BN - 1);
+    const int col = n0 + lc;
+    const bool colok = col < g.N;
+    int64_t cbase = col, rstride = g.ldc;
+    if (g.out_nchw) {
+      const int img = col / hw;
+      cbase = (int64_t)img * g.M * hw + (col - img * hw);
+      rstride = hw;
+    }
+#pragma unroll 4
+    for (int k = 0; k < BM / 2; ++k) {
+      const int lr = (tid >> 7) + 2 * k;
+      const int row = m0 + lr;
+      const EpiRow r = rowc[lr];
+      int32_t* slot = tileI + lr * kEpiStride + lc;
+      int32_t v[1] = {*slot};
+      fold(v, r, col, 1);
+      epi_apply<1, kBlock>(g, r, v, cbase + (int64_t)row * rstride, store_on && colok && row < g.M, col);
+      if (kBlock && g.shadow_out) *slot = v[0];
+    }
+  }
+  if (kBlock && g.shadow_out && !(g.ablate & 1)) {
     lds_barrier();
+    constexpr int kItems = (BM / 16) * BN;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int item = tid + kGemmThreads * k;
-      const int lr = item >> 5;
-      const int lc4 = (item & 31) * 4;
-      const int row = m0 + c * 32 + lr;
-      const int col0 = n0 + lc4;
-      if (row >= g.M || col0 >= g.N) continue;
-      const bool full = col0 + 3 < g.N;
-      v4i vv = *reinterpret_cast<const v4i*>(tileI + lr * kEpiStride + lc4);
-      // zero-point folding: acc - zB[col]*RA[row] - zA[row]*RB[col] + K*zA[row]*zB[col]
-      uint32_t zb[4], rb[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int colq = full ? col0 + q : min(col0 + q, g.N - 1);
-        zb[q] = zb_vec ? (uint32_t)g.zB_vec[colq] : (uint32_t)g.zB;
-        rb[q] = has_rb ? (uint32_t)g.RB[colq] : 0u;
-      }
-      int32_t conv[4];
-      {
-        const int32_t a4[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          conv[q] = (int32_t)((uint32_t)a4[q] - zb[q] * kra[k] - kza[k] * rb[q] + keff * kza[k] * zb[q]);
-      }
-      vv = v4i{conv[0], conv[1], conv[2], conv[3]};
-      // output offsets of the 4 elements
-      int64_t off0;
-      bool vec = full;
-      if (g.out_nchw) {
-        const int img = col0 / hw;
-        const int pix = col0 - img * hw;
-        off0 = ((int64_t)img * g.M + row) * hw + pix;
-        vec = vec && (pix + 3 < hw) && ((off0 & 3) == 0);
-      } else {
-        off0 = (int64_t)row * g.ldc + col0;
-        vec = vec && ((off0 & 3) == 0);
-      }
-      if (!kBlock) {
-        if (vec) {
-          *reinterpret_cast<v4i*>(g.C + off0) = vv;
-        } else {
-          for (int q = 0; q < 4 && col0 + q < g.N; ++q) {
-            const int col = col0 + q;
-            int64_t off = off0 + q;
-            if (g.out_nchw) {
-              const int img = col / hw;
-              off = ((int64_t)img * g.M + row) * hw + (col - img * hw);
-            }
-            g.C[off] = conv[q];
-          }
-        }
-        continue;
-      }
-      int32_t badd[4], rqv[4], last[4];
-      if (g.ch_is_row) {
-        // one channel for the 4 elements: constants from registers, mode branch hoisted
-        const int32_t bch = kb[k], mch = km[k], sch = ks[k], zch = kz[k];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) badd[q] = (int32_t)((uint32_t)conv[q] + (uint32_t)bch);
-        const int mode = g.rq.mode;
-        if (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) rqv[q] = qms_upward((int32_t)((uint32_t)badd[q] - (uint32_t)zch), mch, sch);
-        } else if (mode == TK_RQ_TENSOR_POW2) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) rqv[q] = qms_pow2((int32_t)((uint32_t)badd[q] - (uint32_t)zch), sch);
-        } else if (mode == TK_RQ_IDENTITY) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) rqv[q] = (int32_t)((uint32_t)badd[q] - (uint32_t)zch);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) rqv[q] = qms_tonearest((int32_t)((uint32_t)badd[q] - (uint32_t)zch), mch, sch);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          int32_t t = (int32_t)((uint32_t)g.rq.zp_out + (uint32_t)rqv[q]);
-          t = (int32_t)min(max((int64_t)t, g.rq.qmin), g.rq.qmax);
-          rqv[q] = t;
-          last[q] = g.has_clip ? min(max(t, g.clip_lo), g.clip_hi) : t;
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int ch = full ? col0 + q : min(col0 + q, g.N - 1);
-          badd[q] = (int32_t)((uint32_t)conv[q] + (uint32_t)g.bias[ch]);
-          int32_t t = rq_apply(badd[q], ch, g.rq);
-          t = (int32_t)min(max((int64_t)t, g.rq.qmin), g.rq.qmax);
-          rqv[q] = t;
-          last[q] = g.has_clip ? min(max(t, g.clip_lo), g.clip_hi) : t;
-        }
-      }
-      if (g.shadow_out)
-        *reinterpret_cast<v4i*>(tileI + lr * kEpiStride + lc4) = v4i{last[0], last[1], last[2], last[3]};
-      if (g.ablate & 2) {
-        if (badd[0] == 0x7fffffff && rqv[0] == 3 && last[0] == 5) g.C[0] = 1;  // keep values live
-      } else if (vec) {
-        *reinterpret_cast<v4i*>(g.C + off0) = vv;
-        *reinterpret_cast<v4i*>(g.bias_out + off0) = v4i{badd[0], badd[1], badd[2], badd[3]};
-        uint32_t pr = (rqv[0] & 0xFF) | ((rqv[1] & 0xFF) << 8) | ((rqv[2] & 0xFF) << 16) | ((uint32_t)rqv[3] << 24);
-        *reinterpret_cast<uint32_t*>(g.rq_out + off0) = pr;
-        if (g.has_clip) {
-          uint32_t pc = (last[0] & 0xFF) | ((last[1] & 0xFF) << 8) | ((last[2] & 0xFF) << 16) |
-                        ((uint32_t)last[3] << 24);
-          *reinterpret_cast<uint32_t*>(g.clip_out + off0) = pc;
-        }
-      } else {
-        for (int q = 0; q < 4 && col0 + q < g.N; ++q) {
-          const int col = col0 + q;
-          int64_t off = off0 + q;
-          if (g.out_nchw) {
-            const int img = col / hw;
-            off = ((int64_t)img * g.M + row) * hw + (col - img * hw);
-          }
-          g.C[off] = conv[q];
-          g.bias_out[off] = badd[q];
-          g.rq_out[off] = (uint8_t)rqv[q];
-          if (g.has_clip) g.clip_out[off] = (uint8_t)last[q];
-        }
-      }
-    }
-    if (kBlock && g.shadow_out && !(g.ablate & 1)) {
-      lds_barrier();
-      const int lc = tid & 127;
-      const int half = tid >> 7;
+    for (int it0 = 0; it0 < kItems; it0 += kGemmThreads) {
+      const int it = it0 + tid;
+      const int lc = it & (BN - 1);
+      const int grp = it / BN;
       const int col = n0 + lc;
-      const int ch0 = m0 + c * 32 + half * 16;
+      const int ch0 = m0 + grp * 16;
       if (col < g.N && ch0 < g.shadow_cpad) {
         uint32_t w[4];
 #pragma unroll
@@ -415,7 +428,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_i8_kernel(GemmArgs g) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int ch = ch0 + d * 4 + q;
-            uint32_t b = (uint32_t)tileI[(half * 16 + d * 4 + q) * kEpiStride + lc] ^ g.shadow_xor;
+            uint32_t b = (uint32_t)tileI[(grp * 16 + d * 4 + q) * kEpiStride + lc] ^ g.shadow_xor;
             if (ch >= g.M) b = 0;  // padded channels of a partial group stay zero
             word |= (b & 0xFFu) << (8 * q);
           }
@@ -425,7 +438,6 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_i8_kernel(GemmArgs g) {
             v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
       }
     }
-    lds_barrier();
   }
 }
 
@@ -796,6 +808,10 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   ga.taps = g.KH * g.KW;
   ga.fill = rep4(za);
   ga.out_nchw = 1;
+  {
+    const int hwv = g.OH * g.OW;  // store vectors must not straddle an image plane
+    ga.vecw = hwv % 4 == 0 ? 4 : 1;
+  }
   if (zw != 0 || a->kernel_zero_points) {
     TK_CHECK_ARG(workspace_patch, "non-zero kernel zero point needs a patch-sum workspace");
     int32_t* ps = (int32_t*)workspace_patch;
@@ -925,6 +941,7 @@ static int dense_run(const tk_tensor* data, const tk_tensor* weight, tk_tensor* 
   ga.RB = wsum;
   ga.out_nchw = 0;
   ga.ldc = Nn;
+  ga.vecw = Nn % 4 == 0 ? 4 : 1;
   ga.ch_is_row = 0;
   int rc = setup_block(ga, blk, out, Nn, 1);
   if (rc) return rc;
