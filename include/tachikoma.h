@@ -157,7 +157,7 @@ typedef struct {
 } tk_block_attrs;
 
 /* A fused residual join: qnn.add [→ clip].  One kernel writes both records and,
- * optionally, the NHWC int8 shadow of the last output for the next MFMA conv. */
+ * optionally, the int8 shadow (tk_conv2d_make_shadow layout) of the last output for the next MFMA conv. */
 typedef struct {
   tk_qnn_add_attrs add;
   int32_t has_clip;
@@ -181,15 +181,21 @@ typedef struct {
 int64_t tk_conv2d_packed_weight_bytes(const tk_tensor* weight, int groups);
 int tk_conv2d_pack_weight(const tk_tensor* weight, int groups, void* packed, int32_t* weight_sums,
                           void* stream);
-/* NHWC int8 activation copy with channels padded to 16 (uint8 data stored xor 0x80). */
+/* The int8 "shadow" an MFMA conv reads its activations from: channel-blocked
+ * [ceil(C/16)][N·H·W][16] (16 channels of one pixel per 16-byte chunk; a channel group's
+ * pixels are contiguous), padded channels 0, uint8 data stored xor 0x80. */
 int64_t tk_conv2d_shadow_bytes(const tk_tensor* data);
-int tk_nchw_to_nhwc_i8(const tk_tensor* data, void* shadow, void* stream);
-/* qnn.conv2d on a prepared shadow + packed weight (what the executor runs). */
-/* `patch_sums` (int32 per output pixel, N*OH*OW) is scratch used only when the kernel
- * zero point is non-zero; may be NULL otherwise. */
+int tk_conv2d_make_shadow(const tk_tensor* data, void* shadow, void* stream);
+/* Device scratch of a prepared conv (tk_qnn_conv2d_prepared: block = 0; tk_qnn_conv2d_block:
+ * block = 1): per-pixel patch sums when the kernel zero point is non-zero, plus split-K
+ * partial tiles for layers whose tile grid cannot fill the GPU.  0 = no scratch needed. */
+int64_t tk_conv2d_scratch_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* attrs,
+                                int block);
+/* qnn.conv2d on a prepared shadow + packed weight (what the executor runs).
+ * `scratch`: tk_conv2d_scratch_bytes(..., 0) bytes (may be NULL when that is 0). */
 int tk_qnn_conv2d_prepared(const tk_tensor* data, const void* shadow, const tk_tensor* weight,
                            const void* packed, const int32_t* weight_sums, tk_tensor* out,
-                           const tk_conv2d_attrs* attrs, void* patch_sums, void* stream);
+                           const tk_conv2d_attrs* attrs, void* scratch, void* stream);
 /* One-shot qnn.conv2d (src/relay/qnn/op/convolution.cc:708-811; x86 legalization
  * python/tvm/relay/qnn/op/legalizations.py:177-232): prepares into `workspace`
  * (tk_qnn_conv2d_workspace_bytes) then runs. */
@@ -199,11 +205,11 @@ int tk_qnn_conv2d(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out
                   const tk_conv2d_attrs* attrs, void* workspace, void* stream);
 
 /* Fused conv block: outs = {conv int32, bias_add int32, requantize int8/uint8, clip (if has_clip)}.
- * `shadow_out` (optional): NHWC int8 copy of the block's last output, channels padded to
- * 16, for a following MFMA conv (same layout as tk_nchw_to_nhwc_i8). */
+ * `scratch`: tk_conv2d_scratch_bytes(..., 1) bytes.  `shadow_out` (optional): the int8 shadow
+ * (tk_conv2d_make_shadow layout) of the block's last output, for a following MFMA conv. */
 int tk_qnn_conv2d_block(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
                         const int32_t* weight_sums, const tk_tensor* bias, tk_tensor* const* outs, int n_outs,
-                        const tk_block_attrs* attrs, void* patch_sums, void* shadow_out, void* stream);
+                        const tk_block_attrs* attrs, void* scratch, void* shadow_out, void* stream);
 
 /* qnn.dense (src/relay/qnn/op/dense.cc:87-206). */
 int64_t tk_qnn_dense_workspace_bytes(const tk_tensor* data, const tk_tensor* weight);
@@ -218,7 +224,7 @@ int tk_qnn_add(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const
                void* stream);
 /* nn.bias_add / add with a broadcast vector along `axis` (int32 wraps). */
 /* Fused qnn.add [→ clip] on 8-bit tensors (add.cc:40-96 + clip, python/tvm/topi/math.py:615-640).
- * outs = {add, [clip]}.  shadow_out (optional): NHWC [N][H][W][ceil16(C)] int8 copy of the
+ * outs = {add, [clip]}.  shadow_out (optional): int8 shadow (tk_conv2d_make_shadow layout) of the
  * last output (uint8 stored xor 0x80, padded channels written as 0); needs 4-D NCHW operands. */
 int tk_qnn_add_block(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* const* outs, int n_outs,
                      const tk_add_block_attrs* attrs, void* shadow_out, void* stream);
@@ -241,7 +247,7 @@ int tk_copy(const tk_tensor* data, tk_tensor* out, void* stream);
  * caller for the module's lifetime (the caller keeps them alive).          */
 
 enum {
-  TK_NODE_CONV2D = 1,      /* in: data, weight; ext: shadow, packed, weight_sums, patch_sums */
+  TK_NODE_CONV2D = 1,      /* in: data, weight; ext: shadow, packed, weight_sums, scratch */
   TK_NODE_DENSE = 2,       /* in: data, weight; ext: workspace */
   TK_NODE_REQUANTIZE = 3,
   TK_NODE_BIAS_ADD = 4,
@@ -253,7 +259,7 @@ enum {
   TK_NODE_GLOBAL_AVG_POOL2D = 10,
   TK_NODE_COPY = 11,       /* batch_flatten / reshape */
   TK_NODE_SHADOW = 12,     /* NCHW→NHWC int8 shadow for a conv input (not traced) */
-  TK_NODE_CONV_BLOCK = 13, /* in: data, weight, bias; outs: 3-4; ext: shadow, packed, weight_sums, patch_sums, shadow_out */
+  TK_NODE_CONV_BLOCK = 13, /* in: data, weight, bias; outs: 3-4; ext: shadow, packed, weight_sums, scratch, shadow_out */
   TK_NODE_DENSE_BLOCK = 14,/* in: data, weight, bias; outs: 3-4; ext: workspace */
   TK_NODE_ADD_BLOCK = 15,  /* in: lhs, rhs; outs: 1-2 (add, clip); ext[4]: shadow_out */
 };

@@ -184,7 +184,8 @@ SIGNATURES = {
     "tk_conv2d_packed_weight_bytes": (_I64, [_PT, ctypes.c_int]),
     "tk_conv2d_pack_weight": (ctypes.c_int, [_PT, ctypes.c_int, _VP, _VP, _VP]),
     "tk_conv2d_shadow_bytes": (_I64, [_PT]),
-    "tk_nchw_to_nhwc_i8": (ctypes.c_int, [_PT, _VP, _VP]),
+    "tk_conv2d_scratch_bytes": (_I64, [_PT, _PT, ctypes.POINTER(tk_conv2d_attrs), ctypes.c_int]),
+    "tk_conv2d_make_shadow": (ctypes.c_int, [_PT, _VP, _VP]),
     "tk_qnn_conv2d_prepared": (ctypes.c_int, [_PT, _VP, _PT, _VP, _VP, _PT, ctypes.POINTER(tk_conv2d_attrs), _VP,
                                               _VP]),
     "tk_qnn_conv2d_workspace_bytes": (_I64, [_PT, _PT, ctypes.POINTER(tk_conv2d_attrs)]),

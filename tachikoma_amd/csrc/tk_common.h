@@ -76,6 +76,28 @@ inline int dt_of(const tk_tensor* t) {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---------------------------------------------------------------- streaming stores
+// Trace records are written once and only read back by later kernels / the D2H copy
+// long after L2 has cycled: nontemporal stores keep them from thrashing L2/MALL and
+// measurably raise the write rate of multi-record epilogues (tools/probe_store2.hip).
+typedef int tk_v4i __attribute__((ext_vector_type(4)));
+
+template <int kBytes>
+__device__ __forceinline__ void store_nt(void* dst, const void* src) {
+  if constexpr (kBytes == 16) {
+    tk_v4i v;
+    __builtin_memcpy(&v, src, 16);
+    __builtin_nontemporal_store(v, reinterpret_cast<tk_v4i*>(dst));
+  } else if constexpr (kBytes == 4) {
+    uint32_t v;
+    __builtin_memcpy(&v, src, 4);
+    __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(dst));
+  } else {
+    static_assert(kBytes == 1, "16, 4 or 1 bytes");
+    __builtin_nontemporal_store(*reinterpret_cast<const uint8_t*>(src), reinterpret_cast<uint8_t*>(dst));
+  }
+}
+
 // ---------------------------------------------------------------- fixed point (device)
 // q_multiply_shift general form, q = 31 (src/target/intrin_rule.cc:166-195):
 //   y = (int64(x) << ls) * m;  y += 1 << (30 + rs);  y >>= 31 + rs;  int32(y)

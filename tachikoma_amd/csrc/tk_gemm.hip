@@ -6,7 +6,7 @@
 // reduction axis is contiguous:
 //   * weights are packed once to [Cout][KH][KW][Cin_pad] (Cin_pad = Cin rounded
 //     to 16, K rounded to 64; padding bytes are 0, uint8 stored xor 0x80),
-//   * conv activations are read from an NHWC int8 "shadow" of the NCHW tensor,
+//   * conv activations are read from a channel-blocked int8 "shadow" of the NCHW tensor,
 //     gathered per 16-byte chunk (one tap, 16 channels) straight into LDS.
 // The zero points are folded exactly (modulo 2^32, like the reference's int32
 // accumulation) with row sums:
@@ -32,7 +32,7 @@ constexpr int kEpiStride = 132;  // dwords per LDS row of the epilogue tile (128
 
 struct GemmArgs {
   const int8_t* A;     // [rowsA_pad][lda]
-  const int8_t* B;     // plain: [rowsB_pad][ldb]; im2col: NHWC shadow [N][H][W][cin_pad]
+  const int8_t* B;     // plain: [rowsB_pad][ldb]; im2col: shadow [cin_pad/16][N*H*W][16]
   int32_t* C;
   int32_t M, N;        // real rows of A / rows of B (pixels for conv)
   int32_t lda, ldb;    // row pitch in bytes (plain), K_pad
@@ -46,6 +46,7 @@ struct GemmArgs {
   const int32_t* RB;      // row sums of B (needed when zA != 0)
   // im2col geometry (conv)
   int32_t H, W, cin_pad, KH, KW, sh, sw, pt, pl, dh, dw, OH, OW;
+  int64_t in_pix;                 // N*H*W of the input: pixels per channel group of the shadow
   uint32_t fill;                  // za replicated 4x: out-of-bounds taps (padded channels multiply w = 0)
   int32_t taps;                   // KH*KW
   // output addressing
@@ -55,13 +56,18 @@ struct GemmArgs {
   int32_t* bias_out;
   uint8_t* rq_out;
   uint8_t* clip_out;
-  uint8_t* shadow_out;  // NHWC copy of the last output (conv blocks), channels padded to shadow_cpad
+  uint8_t* shadow_out;  // shadow [shadow_cpad/16][N][16] of the last output (conv blocks)
   const int32_t* bias;
   RqParams rq;
   int32_t has_clip, clip_lo, clip_hi, shadow_cpad;
   uint32_t shadow_xor;  // 0x80 when the block output is uint8 (shadow stores int8 = u8 ^ 0x80)
   int32_t ch_is_row;    // channel index = row (conv: Cout) or column (dense: units)
   int32_t vecw;         // epilogue store vector (4 or 1 elements): divides the plane / row length
+  // split-K (small grids): kMode 1 writes raw partial tiles for k-steps [z*kper, (z+1)*kper) to ws,
+  // kMode 2 sums `splits` of them and runs the epilogue
+  int32_t* ws;
+  int32_t splits, kper;
+  int32_t nt;           // nontemporal record stores
   int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
                        // 8/16/32/64 skip the conv / bias_add / requantize / clip record
 };
@@ -83,7 +89,11 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, int64_t off, i
     last = min(max(q, g.clip_lo), g.clip_hi);
     g.clip_out[off] = (uint8_t)last;
   }
-  if (g.shadow_out) g.shadow_out[pix * g.shadow_cpad + ch] = (uint8_t)((uint32_t)last ^ g.shadow_xor);
+  if (g.shadow_out) {
+    g.shadow_out[((int64_t)(ch >> 4) * g.N + pix) * 16 + (ch & 15)] = (uint8_t)((uint32_t)last ^ g.shadow_xor);
+    if (ch == g.M - 1)  // the padded channels of the last group are written as 0
+      for (int c2 = ch + 1; c2 < g.shadow_cpad; ++c2) g.shadow_out[((int64_t)(c2 >> 4) * g.N + pix) * 16 + (c2 & 15)] = 0;
+  }
 }
 
 __device__ __forceinline__ uint32_t pack4(const int32_t* x) {
@@ -99,16 +109,25 @@ struct EpiRow {
   int32_t bias, m, s, zp, pad;
 };
 
+// record stores (nontemporal: see store_nt in tk_common.h)
 template <int V>
-__device__ __forceinline__ void st_i32(int32_t* dst, const int32_t* v) {
-  if constexpr (V == 4) *reinterpret_cast<v4i*>(dst) = v4i{v[0], v[1], v[2], v[3]};
-  else *dst = v[0];
+__device__ __forceinline__ void st_i32(int32_t* dst, const int32_t* v, bool nt) {
+  if constexpr (V == 4) {
+    if (nt) __builtin_nontemporal_store(v4i{v[0], v[1], v[2], v[3]}, reinterpret_cast<v4i*>(dst));
+    else *reinterpret_cast<v4i*>(dst) = v4i{v[0], v[1], v[2], v[3]};
+  } else {
+    *dst = v[0];  // partial lines: let L2 merge them
+  }
 }
 
 template <int V>
-__device__ __forceinline__ void st_i8(uint8_t* dst, const int32_t* v) {
-  if constexpr (V == 4) *reinterpret_cast<uint32_t*>(dst) = pack4(v);
-  else *dst = (uint8_t)v[0];
+__device__ __forceinline__ void st_i8(uint8_t* dst, const int32_t* v, bool nt) {
+  if constexpr (V == 4) {
+    if (nt) __builtin_nontemporal_store(pack4(v), reinterpret_cast<uint32_t*>(dst));
+    else *reinterpret_cast<uint32_t*>(dst) = pack4(v);
+  } else {
+    *dst = (uint8_t)v[0];
+  }
 }
 
 // V consecutive columns of one row after zero-point folding: stores each record as
@@ -118,17 +137,27 @@ __device__ __forceinline__ void st_i8(uint8_t* dst, const int32_t* v) {
 template <int V, bool kBlock>
 __device__ __forceinline__ void epi_apply(const GemmArgs& g, const EpiRow& r, int32_t* v, int64_t off, bool st,
                                           int col) {
-  if (st && !(g.ablate & 8)) st_i32<V>(g.C + off, v);
+  if (st && !(g.ablate & 8)) st_i32<V>(g.C + off, v, g.nt);
   if (!kBlock) return;
   const int qmin = (int)g.rq.qmin, qmax = (int)g.rq.qmax;
   if (g.ch_is_row) {
 #pragma unroll
     for (int q = 0; q < V; ++q) v[q] = (int32_t)((uint32_t)v[q] + (uint32_t)r.bias);
-    if (st && !(g.ablate & 16)) st_i32<V>(g.bias_out + off, v);
+    if (st && !(g.ablate & 16)) st_i32<V>(g.bias_out + off, v, g.nt);
     const int mode = g.rq.mode;
     if (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD) {
+      if (r.s <= -2) {
+        // right shift >= 2: the rounding constant 2^(30+rs) has a zero low word, so
+        // (x·m + 2^(30+rs)) >> (31+rs) only needs the high word of x·m (v_mul_hi_i32)
+        const int sh2 = -r.s - 1;
+        const uint32_t rnd = 1u << (sh2 - 1);
 #pragma unroll
-      for (int q = 0; q < V; ++q) v[q] = qms_upward((int32_t)((uint32_t)v[q] - (uint32_t)r.zp), r.m, r.s);
+        for (int q = 0; q < V; ++q)
+          v[q] = (int32_t)((uint32_t)__mulhi((int32_t)((uint32_t)v[q] - (uint32_t)r.zp), r.m) + rnd) >> sh2;
+      } else {
+#pragma unroll
+        for (int q = 0; q < V; ++q) v[q] = qms_upward((int32_t)((uint32_t)v[q] - (uint32_t)r.zp), r.m, r.s);
+      }
     } else if (mode == TK_RQ_TENSOR_POW2) {
 #pragma unroll
       for (int q = 0; q < V; ++q) v[q] = qms_pow2((int32_t)((uint32_t)v[q] - (uint32_t)r.zp), r.s);
@@ -145,15 +174,15 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, const EpiRow& r, in
     // channel = column (dense blocks)
 #pragma unroll
     for (int q = 0; q < V; ++q) v[q] = (int32_t)((uint32_t)v[q] + (uint32_t)g.bias[col + q]);
-    if (st && !(g.ablate & 16)) st_i32<V>(g.bias_out + off, v);
+    if (st && !(g.ablate & 16)) st_i32<V>(g.bias_out + off, v, g.nt);
 #pragma unroll
     for (int q = 0; q < V; ++q) v[q] = min(max(rq_apply(v[q], col + q, g.rq), qmin), qmax);
   }
-  if (st && !(g.ablate & 32)) st_i8<V>(g.rq_out + off, v);
+  if (st && !(g.ablate & 32)) st_i8<V>(g.rq_out + off, v, g.nt);
   if (g.has_clip) {
 #pragma unroll
     for (int q = 0; q < V; ++q) v[q] = min(max(v[q], g.clip_lo), g.clip_hi);
-    if (st && !(g.ablate & 64)) st_i8<V>(g.clip_out + off, v);
+    if (st && !(g.ablate & 64)) st_i8<V>(g.clip_out + off, v, g.nt);
   }
 }
 
@@ -166,7 +195,9 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // the 16-lane groups of ds_read_b128 then hit 16 distinct bank slots.
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * kBK + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int MT, bool kIm2col, bool kBlock>
+// kMode: 0 = whole K + epilogue; 1 = split-K partial (raw accumulators to g.ws);
+//        2 = sum the split-K partials of this tile + epilogue (no main loop).
+template <int MT, bool kIm2col, bool kBlock, int kMode = 0>
 __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(GemmArgs g) {
   constexpr int BM = 64 * MT;   // rows of A per block (2 waves along M, MT 32-row tiles each)
   constexpr int BN = 128;       // rows of B per block (2 waves along N, 2 32-col tiles each)
@@ -235,7 +266,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
         int iw = b_iw0[t] + kw * g.dw;
         if (b_valid[t] && tap_ok) {
           if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
-            const int8_t* src = g.B + (((int64_t)b_img[t] * g.H + ih) * g.W + iw) * g.cin_pad + c0;
+            const int8_t* src = g.B + ((int64_t)(c0 >> 4) * g.in_pix + ((int64_t)b_img[t] * g.H + ih) * g.W + iw) * 16;
             rb[t] = *reinterpret_cast<const v4i*>(src);
           } else {
             rb[t] = v4i{(int)fill, (int)fill, (int)fill, (int)fill};
@@ -268,13 +299,38 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = v16i{0};
 
-  const int nk = g.k_pad / kBK;
-  load_stage(0);
+  // partial tiles live in g.ws in register order: v4i r4 of fragment (i, j) of thread tid
+  constexpr int kTileInts = MT * 2 * 16 * kGemmThreads;
+  const int64_t tile = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  if constexpr (kMode == 2) {
+    for (int sp = 0; sp < g.splits; ++sp) {
+      const v4i* src = reinterpret_cast<const v4i*>(g.ws + (tile * g.splits + sp) * kTileInts);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const v4i t = src[((i * 2 + j) * 4 + r4) * kGemmThreads + tid];
+            acc[i][j][4 * r4] += t.x;
+            acc[i][j][4 * r4 + 1] += t.y;
+            acc[i][j][4 * r4 + 2] += t.z;
+            acc[i][j][4 * r4 + 3] += t.w;
+          }
+    }
+  }
+  int kt0 = 0, nk = g.k_pad / kBK;
+  if constexpr (kMode == 1) {
+    kt0 = blockIdx.z * g.kper;
+    nk = min(nk, kt0 + g.kper);
+  }
+  if constexpr (kMode != 2) {
+  load_stage(kt0 * kBK);
   store_stage(0);
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
+  for (int kt = kt0; kt < nk; ++kt) {
+    const int buf = (kt - kt0) & 1;
     if (kt + 1 < nk) load_stage((kt + 1) * kBK);  // issue early, land under the MFMAs
     const int8_t* a = As + buf * BM * kBK;
     const int8_t* b = Bs + buf * BN * kBK;
@@ -300,6 +356,19 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
     if (kt + 1 < nk) store_stage(buf ^ 1);
     __syncthreads();
   }
+  }  // kMode != 2
+  if constexpr (kMode == 1) {
+    v4i* dst = reinterpret_cast<v4i*>(g.ws + (tile * gridDim.z + blockIdx.z) * kTileInts);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          dst[((i * 2 + j) * 4 + r4) * kGemmThreads + tid] =
+              v4i{acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]};
+    return;
+  }
 
   // ---- epilogue: the whole BM x BN accumulator tile is staged through LDS.
   //  (1) every wave dumps its raw accumulators to LDS [row][col]; threads < BM stage their
@@ -309,8 +378,9 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   //      is stored as soon as it is complete.  The lanes of a wave run along the columns, so
   //      every store instruction writes whole 128-byte lines of one or two rows (int32: 16 B
   //      per lane, int8: 4 B per lane); the final int8 values go back to the LDS slot;
-  //  (3) the NHWC shadow for the next conv: each item gathers 16 channels of one pixel
-  //      (a wave reads 64 consecutive columns per row: conflict-free) into a 16 B store.
+  //  (3) the shadow for the next conv: each item gathers 16 channels of one pixel (a wave
+  //      reads 64 consecutive columns per row: conflict-free) into a 16 B store; the lanes'
+  //      stores are contiguous (channel-blocked layout).
   if (g.ablate & 4) return;
   int32_t* tileI = reinterpret_cast<int32_t*>(smem);
   EpiRow* rowc = reinterpret_cast<EpiRow*>(smem + BM * kEpiStride * 4);
@@ -434,7 +504,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
           }
           w[d] = word;
         }
-        *reinterpret_cast<v4i*>(g.shadow_out + (int64_t)col * g.shadow_cpad + ch0) =
+        *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)(ch0 >> 4) * g.N + col) * 16) =
             v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
       }
     }
@@ -473,9 +543,9 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(const int8_t* __restri
   if (threadIdx.x == 0 && o < Cout) sums[o] = red[0];
 }
 
-// NCHW int8/uint8 -> NHWC [N][H][W][cin_pad]; padded channels 0; uint8 xor 0x80.
-// One thread per (pixel, 16-channel chunk); lanes run along pixels so each channel
-// plane read is a contiguous 64-byte span.
+// NCHW int8/uint8 -> shadow [cin_pad/16][N*HW][16]; padded channels 0; uint8 xor 0x80.
+// One thread per (16-channel chunk, pixel); lanes run along pixels, so each channel
+// plane read is a contiguous 64-byte span and the 16-byte stores are contiguous.
 __global__ __launch_bounds__(256) void shadow_kernel(const uint8_t* __restrict__ x, uint8_t* __restrict__ y, int N,
                                                      int C, int HW, int cin_pad, int xor_u8) {
   int chunks = cin_pad / 16;
@@ -495,7 +565,7 @@ __global__ __launch_bounds__(256) void shadow_kernel(const uint8_t* __restrict__
       if (c < C) b = xor_u8 ? (uint8_t)(src[(int64_t)c * HW] ^ 0x80) : src[(int64_t)c * HW];
       v[j] = b;
     }
-    __builtin_memcpy(y + ((int64_t)n * HW + pix) * cin_pad + chunk * 16, v, 16);
+    __builtin_memcpy(y + ((int64_t)chunk * N * HW + (int64_t)n * HW + pix) * 16, v, 16);
   }
 }
 
@@ -543,8 +613,8 @@ __global__ __launch_bounds__(256) void patch_sum_kernel(const int8_t* __restrict
         if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) {
           s += (int32_t)zpa * Cin;
         } else {
-          const int8_t* src = shadow + (((int64_t)img * g.H + ih) * g.W + iw) * g.cin_pad;
-          for (int c = 0; c < Cin; ++c) s += src[c];
+          const int64_t pix = ((int64_t)img * g.H + ih) * g.W + iw;
+          for (int c = 0; c < Cin; ++c) s += shadow[((int64_t)(c >> 4) * g.in_pix + pix) * 16 + (c & 15)];
         }
       }
     }
@@ -654,7 +724,7 @@ int64_t conv_shadow_bytes(const tk_tensor* data) {
   return data->shape[0] * data->shape[2] * data->shape[3] * cin_pad;
 }
 
-int nchw_to_nhwc_impl(const tk_tensor* data, void* shadow, hipStream_t s) {
+int make_shadow_impl(const tk_tensor* data, void* shadow, hipStream_t s) {
   TK_CHECK_ARG(data && shadow && data->ndim == 4 && is_int8ish(data), "data must be 4-D int8/uint8");
   int N = (int)data->shape[0], C = (int)data->shape[1], HW = (int)(data->shape[2] * data->shape[3]);
   int cin_pad = (C + 15) / 16 * 16;
@@ -732,6 +802,11 @@ static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out
   return TK_OK;
 }
 
+static int nt_stores() {
+  const char* e = getenv("TK_NT");
+  return e ? atoi(e) : 1;
+}
+
 static int ablate_flags() {
   static int v = [] {
     const char* e = getenv("TK_ABLATE");
@@ -740,8 +815,48 @@ static int ablate_flags() {
   return v;
 }
 
+// Split-K plan of an MFMA conv: layers whose tile grid cannot give every CU a workgroup
+// (the 7x7 stage at 64 samples) split the reduction so that ~3 workgroups per CU stay
+// resident (each split keeps >= 6 k-steps); kper = k-steps per split.
+struct SplitPlan {
+  int splits, kper;
+  int64_t tiles;
+};
+static SplitPlan conv_split_plan(const ConvGeom& g, bool mt1) {
+  const int64_t P = (int64_t)g.N * g.OH * g.OW;
+  const int64_t tiles = ((P + 127) / 128) * ((g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128));
+  const int nk = (int)(g.k_pad / kBK);
+  SplitPlan sp{1, nk, tiles};
+  // measured: splitting grids of >= 256 tiles (one per CU) loses more to the partial-tile
+  // round trip than it gains in latency hiding
+  if (!mt1 || tiles >= 256) return sp;
+  int want = (int)std::min<int64_t>((768 + tiles - 1) / tiles, nk / 6);
+  if (want <= 1) return sp;
+  sp.kper = (nk + want - 1) / want;
+  sp.splits = (nk + sp.kper - 1) / sp.kper;
+  return sp;
+}
+
+static bool conv_needs_patch(const tk_tensor* weight, const tk_conv2d_attrs* a) {
+  return (a->kernel_zero_point - (is_uint(weight, 8) ? 128 : 0)) != 0 || a->kernel_zero_points;
+}
+
+static inline int64_t al256(int64_t v) { return (v + 255) / 256 * 256; }
+
+int64_t conv_scratch_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* a, int block) {
+  if (!a) return -1;
+  ConvGeom g;
+  if (conv_geom(data, weight, a, &g) != TK_OK) return -1;
+  if (!use_mfma_conv(g, a->groups)) return 0;
+  int64_t bytes = 0;
+  if (conv_needs_patch(weight, a)) bytes += al256((int64_t)g.N * g.OH * g.OW * 4);
+  const SplitPlan sp = conv_split_plan(g, g.O <= 64 || block);
+  if (sp.splits > 1) bytes += al256(sp.tiles * sp.splits * (int64_t)(2 * 16 * kGemmThreads) * 4);
+  return bytes;
+}
+
 static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
-                      const int32_t* sums, tk_tensor* out, const tk_conv2d_attrs* a, void* workspace_patch,
+                      const int32_t* sums, tk_tensor* out, const tk_conv2d_attrs* a, void* scratch,
                       const BlockIO* blk, hipStream_t s) {
   TK_CHECK_ARG(data && weight && out && a, "null argument");
   TK_CHECK_ARG(is_int8ish(data) && is_int8ish(weight) && is_int(out, 32), "dtypes: int8/uint8 in, int32 out");
@@ -764,6 +879,7 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   ga.OW = g.OW;
   ga.ch_is_row = 1;
   ga.ablate = ablate_flags();
+  ga.nt = nt_stores();
   int rc = setup_block(ga, blk, out, g.O, 1);
   if (rc) return rc;
   if (!use_mfma_conv(g, a->groups)) {
@@ -803,6 +919,7 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   ga.zB = za;
   ga.RA = sums;
   ga.H = g.H; ga.W = g.W; ga.cin_pad = g.cin_pad; ga.KH = g.KH; ga.KW = g.KW;
+  ga.in_pix = (int64_t)g.N * g.H * g.W;
   ga.sh = a->strides[0]; ga.sw = a->strides[1]; ga.pt = a->padding[0]; ga.pl = a->padding[1];
   ga.dh = a->dilation[0]; ga.dw = a->dilation[1];
   ga.taps = g.KH * g.KW;
@@ -812,24 +929,37 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     const int hwv = g.OH * g.OW;  // store vectors must not straddle an image plane
     ga.vecw = hwv % 4 == 0 ? 4 : 1;
   }
-  if (zw != 0 || a->kernel_zero_points) {
-    TK_CHECK_ARG(workspace_patch, "non-zero kernel zero point needs a patch-sum workspace");
-    int32_t* ps = (int32_t*)workspace_patch;
+  char* sc = (char*)scratch;
+  if (conv_needs_patch(weight, a)) {
+    TK_CHECK_ARG(sc, "non-zero kernel zero point needs scratch (tk_conv2d_scratch_bytes)");
+    int32_t* ps = (int32_t*)sc;
+    sc += al256(P * 4);
     int grid = (int)std::max<int64_t>(1, std::min<int64_t>((P + 255) / 256, 4096));
     hipLaunchKernelGGL(patch_sum_kernel, dim3(grid), dim3(256), 0, s, (const int8_t*)shadow, ps, ga, g.C);
     TK_LAUNCH_CHECK();
     ga.RB = ps;
     ga.zA_vec = a->kernel_zero_points;
   }
-  dim3 grid((unsigned)((P + 127) / 128), (unsigned)((g.O + 127) / 128));
-#define TK_GEMM(MT, BLK) hipLaunchKernelGGL((gemm_i8_kernel<MT, true, BLK>), grid, dim3(kGemmThreads), 0, s, ga)
-  if (g.O <= 64 || (blk && !getenv("TK_MT2"))) {
-    grid.y = (unsigned)((g.O + 63) / 64);
-    if (blk) TK_GEMM(1, true); else TK_GEMM(1, false);
+  const bool mt1 = g.O <= 64 || (blk && !getenv("TK_MT2"));
+  dim3 grid((unsigned)((P + 127) / 128), (unsigned)((g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128)));
+  const SplitPlan sp = conv_split_plan(g, mt1);
+  if (sp.splits > 1) {
+    TK_CHECK_ARG(sc, "split-K conv needs scratch (tk_conv2d_scratch_bytes)");
+    ga.ws = (int32_t*)sc;
+    ga.splits = sp.splits;
+    ga.kper = sp.kper;
+    dim3 pgrid(grid.x, grid.y, (unsigned)sp.splits);
+    hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1>), pgrid, dim3(kGemmThreads), 0, s, ga);
+    TK_LAUNCH_CHECK();
+    if (blk) hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 2>), grid, dim3(kGemmThreads), 0, s, ga);
+    else hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 2>), grid, dim3(kGemmThreads), 0, s, ga);
+  } else if (mt1) {
+    if (blk) hipLaunchKernelGGL((gemm_i8_kernel<1, true, true>), grid, dim3(kGemmThreads), 0, s, ga);
+    else hipLaunchKernelGGL((gemm_i8_kernel<1, true, false>), grid, dim3(kGemmThreads), 0, s, ga);
   } else {
-    if (blk) TK_GEMM(2, true); else TK_GEMM(2, false);
+    if (blk) hipLaunchKernelGGL((gemm_i8_kernel<2, true, true>), grid, dim3(kGemmThreads), 0, s, ga);
+    else hipLaunchKernelGGL((gemm_i8_kernel<2, true, false>), grid, dim3(kGemmThreads), 0, s, ga);
   }
-#undef TK_GEMM
   TK_LAUNCH_CHECK();
   return TK_OK;
 }
@@ -856,9 +986,8 @@ int64_t conv2d_workspace_bytes(const tk_tensor* data, const tk_tensor* weight, c
   int64_t packed = conv_packed_weight_bytes(weight, 1);
   int64_t sums = (int64_t)g.rows_pad * 4;
   int64_t shadow = conv_shadow_bytes(data);
-  int64_t patch = (int64_t)g.N * g.OH * g.OW * 4;
   auto al = [](int64_t v) { return (v + 255) / 256 * 256; };
-  return al(packed) + al(sums) + al(shadow) + al(patch);
+  return al(packed) + al(sums) + al(shadow) + conv_scratch_bytes(data, weight, a, 0);
 }
 
 int conv2d_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_conv2d_attrs* a,
@@ -880,12 +1009,12 @@ int conv2d_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, 
   ws += al((int64_t)g.rows_pad * 4);
   void* shadow = ws;
   ws += al(conv_shadow_bytes(data));
-  void* patch = ws;
+  void* scratch = ws;
   int rc = conv_pack_weight(weight, 1, packed, sums, s);
   if (rc) return rc;
-  rc = nchw_to_nhwc_impl(data, shadow, s);
+  rc = make_shadow_impl(data, shadow, s);
   if (rc) return rc;
-  return conv2d_run(data, shadow, weight, packed, sums, out, a, patch, nullptr, s);
+  return conv2d_run(data, shadow, weight, packed, sums, out, a, scratch, nullptr, s);
 }
 
 // ---------------------------------------------------------------- dense

@@ -6,12 +6,12 @@
 // inputs, so each workgroup tabulates RQ for both operands in LDS once (computed with
 // the same rq_apply the requantize kernel uses, hence bit-exact by construction) and
 // the element loop is two table lookups, an add and two clamps: the kernel is a pure
-// HBM stream of 2 bytes in, 2 bytes out (+ the NHWC shadow) per element.
+// HBM stream of 2 bytes in, 2 bytes out (+ the shadow) per element.
 //
 // Tile = 64 channels x PT pixels of one image.  Records are stored NCHW with
 // kV-byte vectors (16 when HW % 16 == 0, else 4 or 1); when the next MFMA conv
-// reads this output, the final bytes are also staged in LDS and re-emitted as the
-// NHWC shadow [N][H][W][C_pad16], 16 channels (16 B) per store.
+// reads this output, the final bytes are also staged in LDS and re-emitted as its
+// int8 shadow [C_pad16/16][N·HW][16] (tk_conv2d_make_shadow layout), 16 B per store.
 #include <algorithm>
 
 #include "tk_common.h"
@@ -30,7 +30,7 @@ struct AddBlockArgs {
   const uint8_t* b;
   uint8_t* add_out;
   uint8_t* clip_out;  // null: no clip record
-  uint8_t* shadow;    // null: no NHWC copy
+  uint8_t* shadow;    // null: no shadow copy
   int32_t N, C, HW, PT, tiles_per_image;
   int32_t is_u8, zp_c, has_clip, clip_lo, clip_hi, cpad;
   RqParams pa, pb;
@@ -76,8 +76,8 @@ __global__ __launch_bounds__(kThreads) void add_block_kernel(AddBlockArgs g) {
       vo[j] = (uint8_t)o;
       vc[j] = (uint8_t)min(max(o, g.clip_lo), g.clip_hi);
     }
-    __builtin_memcpy(g.add_out + off, vo, kV);
-    if (g.has_clip) __builtin_memcpy(g.clip_out + off, vc, kV);
+    store_nt<kV>(g.add_out + off, vo);
+    if (g.has_clip) store_nt<kV>(g.clip_out + off, vc);
     if (want_shadow) {
       const uint8_t* last = g.has_clip ? vc : vo;
 #pragma unroll
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kThreads) void add_block_kernel(AddBlockArgs g) {
   if (!want_shadow) return;
   __syncthreads();
 
-  // NHWC shadow: one 16-channel chunk of one pixel per item
+  // shadow: one 16-channel chunk of one pixel per item (lanes along pixels: contiguous)
   const int chunks = kCT / 16;
   const int items = chunks * g.PT;
   const uint8_t xr = g.is_u8 ? 0x80 : 0;
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kThreads) void add_block_kernel(AddBlockArgs g) {
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       out[j] = (cbase + j < g.C) ? (uint8_t)(tile[(ch * 16 + j) * kLdsStride + pl] ^ xr) : 0;
-    __builtin_memcpy(g.shadow + ((int64_t)n * g.HW + p) * g.cpad + cbase, out, 16);
+    __builtin_memcpy(g.shadow + ((int64_t)(cbase >> 4) * g.N * g.HW + (int64_t)n * g.HW + p) * 16, out, 16);
   }
 }
 

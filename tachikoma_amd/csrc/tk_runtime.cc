@@ -30,9 +30,10 @@ int digest_impl(const void* data, int64_t nbytes, uint64_t* out, hipStream_t s);
 int64_t conv_packed_weight_bytes(const tk_tensor* weight, int groups);
 int conv_pack_weight(const tk_tensor* weight, int groups, void* packed, int32_t* sums, hipStream_t s);
 int64_t conv_shadow_bytes(const tk_tensor* data);
-int nchw_to_nhwc_impl(const tk_tensor* data, void* shadow, hipStream_t s);
+int64_t conv_scratch_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* a, int block);
+int make_shadow_impl(const tk_tensor* data, void* shadow, hipStream_t s);
 int conv2d_prepared_impl(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
-                         const int32_t* sums, tk_tensor* out, const tk_conv2d_attrs* a, void* patch, hipStream_t s);
+                         const int32_t* sums, tk_tensor* out, const tk_conv2d_attrs* a, void* scratch, hipStream_t s);
 int64_t conv2d_workspace_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* a);
 int conv2d_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_conv2d_attrs* a,
                 void* workspace, hipStream_t s);
@@ -41,7 +42,7 @@ int dense_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, c
                void* workspace, hipStream_t s);
 int conv2d_block_impl(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
                       const int32_t* sums, const tk_tensor* bias, tk_tensor* const* outs, int n_outs,
-                      const tk_block_attrs* attrs, void* patch, void* shadow_out, hipStream_t s);
+                      const tk_block_attrs* attrs, void* scratch, void* shadow_out, hipStream_t s);
 int dense_block_impl(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,
                      int n_outs, const tk_block_attrs* attrs, void* workspace, hipStream_t s);
 
@@ -107,7 +108,7 @@ static int run_node(Node& n, hipStream_t s) {
     case TK_NODE_COPY:
       return copy_impl(i0, o, s);
     case TK_NODE_SHADOW:
-      return nchw_to_nhwc_impl(i0, d.ext[0], s);
+      return make_shadow_impl(i0, d.ext[0], s);
   }
   set_error("tk_module: unknown node kind " + std::to_string(d.kind));
   return TK_ERR_INVALID_ARG;
@@ -137,13 +138,17 @@ int tk_conv2d_pack_weight(const tk_tensor* weight, int groups, void* packed, int
   return tk::conv_pack_weight(weight, groups, packed, weight_sums, tk::as_stream(stream));
 }
 int64_t tk_conv2d_shadow_bytes(const tk_tensor* data) { return tk::conv_shadow_bytes(data); }
-int tk_nchw_to_nhwc_i8(const tk_tensor* data, void* shadow, void* stream) {
-  return tk::nchw_to_nhwc_impl(data, shadow, tk::as_stream(stream));
+int64_t tk_conv2d_scratch_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* attrs,
+                                int block) {
+  return tk::conv_scratch_bytes(data, weight, attrs, block);
+}
+int tk_conv2d_make_shadow(const tk_tensor* data, void* shadow, void* stream) {
+  return tk::make_shadow_impl(data, shadow, tk::as_stream(stream));
 }
 int tk_qnn_conv2d_prepared(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
-                           const int32_t* weight_sums, tk_tensor* out, const tk_conv2d_attrs* attrs, void* patch_sums,
+                           const int32_t* weight_sums, tk_tensor* out, const tk_conv2d_attrs* attrs, void* scratch,
                            void* stream) {
-  return tk::conv2d_prepared_impl(data, shadow, weight, packed, weight_sums, out, attrs, patch_sums,
+  return tk::conv2d_prepared_impl(data, shadow, weight, packed, weight_sums, out, attrs, scratch,
                                   tk::as_stream(stream));
 }
 int64_t tk_qnn_conv2d_workspace_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* attrs) {
@@ -162,8 +167,8 @@ int tk_qnn_dense(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
 }
 int tk_qnn_conv2d_block(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
                         const int32_t* weight_sums, const tk_tensor* bias, tk_tensor* const* outs, int n_outs,
-                        const tk_block_attrs* attrs, void* patch_sums, void* shadow_out, void* stream) {
-  return tk::conv2d_block_impl(data, shadow, weight, packed, weight_sums, bias, outs, n_outs, attrs, patch_sums,
+                        const tk_block_attrs* attrs, void* scratch, void* shadow_out, void* stream) {
+  return tk::conv2d_block_impl(data, shadow, weight, packed, weight_sums, bias, outs, n_outs, attrs, scratch,
                                shadow_out, tk::as_stream(stream));
 }
 int tk_qnn_dense_block(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,

@@ -7,8 +7,8 @@ Memory layout in HBM (one GPU, one batch shard):
     reuse as in graph_executor.cc:356-464), so each output stays addressable
     for the trace copy-out until the step ends — ResNet-50 at 64 samples is
     ~7 GB, nothing next to 288 GB;
-  * every tensor read by an MFMA conv has an NHWC int8 "shadow" (channels padded
-    to 16): written directly by the producing fused conv block's epilogue, or by
+  * every tensor read by an MFMA conv has an int8 "shadow", channel-blocked
+    [C_pad16/16][N·H·W][16]: written directly by the producing fused conv block's epilogue, or by
     a shadow node right before the first conv that reads it.
 
 Nodes: one per ExecGroup (build_module.exec_groups) — a fused conv/dense layer
@@ -127,7 +127,7 @@ class DeviceModule:
         torch = _torch()
         stream = _lib.stream_handle()
         nodes: List[_lib.tk_node] = []
-        # tensors read by MFMA convs need an NHWC shadow
+        # tensors read by MFMA convs need a shadow
         conv_ops = [g.ops[0] for g in self.groups if g.ops[0].op == "qnn.conv2d"]
         mfma = {op.name: self._is_mfma_conv(op) for op in conv_ops}
         shadow_bufs: Dict[str, object] = {}
@@ -171,7 +171,7 @@ class DeviceModule:
                     self._conv_attrs(ba.conv, head)
                     self._prep_conv(n, head, ins, mfma[head.name], shadow_bufs, ensure_shadow, stream)
                     if g.last.name in shadow_bufs:
-                        # the epilogue writes the NHWC copy the next MFMA conv reads
+                        # the epilogue writes the shadow the next MFMA conv reads
                         n.ext[4] = shadow_bufs[g.last.name].data_ptr()
                         shadow_ready.add(g.last.name)
                 else:
@@ -248,7 +248,8 @@ class DeviceModule:
         self.n_nodes = len(nodes)
 
     def _prep_conv(self, n, op: PlanOp, ins, is_mfma: bool, shadow_bufs, ensure_shadow, stream):
-        """MFMA path: shadow of the input + packed weight + weight sums (+ patch-sum scratch)."""
+        """MFMA path: shadow of the input + packed weight + weight sums (+ scratch: patch sums,
+        split-K partial tiles)."""
         if not is_mfma:
             return
         ensure_shadow(op.inputs[0])
@@ -261,9 +262,13 @@ class DeviceModule:
         n.ext[0] = shadow_bufs[op.inputs[0]].data_ptr()
         n.ext[1] = packed.data_ptr()
         n.ext[2] = sums.data_ptr()
-        if op.attrs["kernel_zero_point"] != 0 or "kernel_zero_points" in op.consts:
-            p = int(np.prod(op.out.shape)) // op.out.shape[1]
-            n.ext[3] = self._scratch(p * 4).data_ptr()
+        block = n.kind == _lib.NODE_KINDS["conv_block"]
+        ca = n.attrs.block.conv if block else n.attrs.conv2d
+        nbytes = self.lib.tk_conv2d_scratch_bytes(ins[0].ptr, ins[1].ptr, ctypes.byref(ca), int(block))
+        if nbytes < 0:
+            _lib.check(-3, f"{op.name} conv scratch")
+        if nbytes > 0:
+            n.ext[3] = self._scratch(nbytes).data_ptr()
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -61,6 +61,17 @@ def test_add_kat(tk, case):
     np.testing.assert_array_equal(out, load_array(case["expected"]))
 
 
+def blocked_shadow(x: np.ndarray) -> np.ndarray:
+    """Expected tk_conv2d_make_shadow layout of an NCHW 8-bit tensor: [C_pad16/16][N*H*W][16] uint8,
+    padded channels 0, uint8 stored xor 0x80."""
+    n, c, h, w = x.shape
+    cpad = (c + 15) // 16 * 16
+    b = x.view(np.uint8) ^ (0x80 if x.dtype == np.uint8 else 0)
+    full = np.zeros((n, cpad, h, w), np.uint8)
+    full[:, :c] = b
+    return full.reshape(n, cpad // 16, 16, h * w).transpose(1, 0, 3, 2).reshape(cpad // 16, n * h * w, 16)
+
+
 def _rand(rng, shape, dtype):
     info = np.iinfo(dtype)
     return rng.integers(info.min, int(info.max) + 1, size=shape, dtype=np.int64).astype(dtype)
@@ -80,6 +91,8 @@ CONV_CASES = [
     (1, 32, 9, 9, 64, 3, 2, 1, 1, 4, "uint8", "int8", 100, 1),      # grouped, mixed dtypes
     (1, 1, 28, 28, 6, 5, 1, 2, 1, 1, "int8", "int8", -4, 0),        # LeNet conv1 (direct path)
     (3, 256, 7, 7, 512, 3, 1, 1, 1, 1, "int8", "int8", -1, 0),      # K = 2304, image-straddling tiles
+    (2, 256, 7, 7, 64, 3, 1, 1, 1, 1, "int8", "int8", 4, 3),        # split-K (small grid) + patch sums
+    (1, 160, 6, 6, 48, 3, 1, 1, 1, 1, "uint8", "int8", 130, 0),     # split-K, ragged last split, HW % 4 == 0
 ]
 
 
@@ -180,13 +193,7 @@ def test_qnn_add_block(tk, case):
         last = ref.clip(add, *clip)
         np.testing.assert_array_equal(outs[1], last)
     if want_shadow:
-        shadow = outs[-1]
-        c = shape[1]
-        nhwc = np.transpose(last, (0, 2, 3, 1))
-        view = shadow[..., :c].view(np.int8)
-        expect = (nhwc.view(np.uint8) ^ 0x80).view(np.int8) if dt == "uint8" else nhwc.view(np.int8)
-        np.testing.assert_array_equal(view, expect)
-        assert not shadow[..., c:].any()
+        np.testing.assert_array_equal(outs[-1], blocked_shadow(last))
 
 
 def test_elementwise_random(tk):
@@ -223,7 +230,29 @@ BLOCK_CASES = [
     (2, 64, 7, 7, 200, 1, 1, 0, 1, "uint8", 130, "uint8", None),
     (1, 24, 10, 10, 24, 3, 2, 1, 24, "int8", 1, "int8", (0, 96)),     # depthwise (direct kernel)
     (1, 1, 12, 12, 6, 5, 1, 2, 1, "int8", 0, "int8", (-1, 127)),      # tiny Cin (direct kernel)
+    (2, 128, 7, 7, 256, 3, 1, 1, 1, "int8", -2, "int8", (0, 127)),    # split-K block, scalar-store epilogue
+    (4, 256, 14, 14, 96, 1, 2, 0, 1, "int8", 5, "uint8", None),       # split-K strided 1x1, 7x7 out
 ]
+
+
+def test_conv_block_requantize_shift_regimes(tk):
+    """Per-channel multipliers spanning right shifts 0..8 and left shifts 1..2, so the block
+    epilogue's mul_hi fast path (right shift >= 2) and the general int64 path both run,
+    against the oracle on the same inputs."""
+    rng = np.random.default_rng(77)
+    n, c, h, w, o = 2, 64, 8, 8, 64
+    x = _rand(rng, (n, c, h, w), "int8")
+    wt = _rand(rng, (o, c, 1, 1), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_out = np.float32(0.5)
+    mult = np.geomspace(2.0 ** -8, 3.5, o)  # M = s_in / s_out
+    s_in = (mult * s_out).astype(np.float32)
+    outs = tk.conv2d_block(x, wt, bias, 3, 0, s_in, s_out, -4, clip=(-128, 127), want_shadow=True)
+    conv = ref.qnn_conv2d(x, wt, 3, 0)
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(-4), axis=1, out_dtype="int8")
+    for got, e in zip(outs, [conv, badd, rq, rq]):
+        np.testing.assert_array_equal(got, e)
 
 
 @pytest.mark.parametrize("case", BLOCK_CASES, ids=[f"block{i}" for i in range(len(BLOCK_CASES))])
@@ -246,12 +275,5 @@ def test_conv_block_matches_unfused_ops(tk, case):
         exp.append(ref.clip(rq, *clip))
     for got, e in zip(outs, exp):
         np.testing.assert_array_equal(got, e)
-    # the NHWC shadow of the last output (what the next MFMA conv reads)
-    shadow = outs[-1]
-    last = exp[-1]
-    cpad = shadow.shape[-1]
-    nhwc = np.transpose(last, (0, 2, 3, 1))
-    view = shadow[..., :o].view(np.int8)
-    expect = (nhwc.view(np.uint8) ^ 0x80).view(np.int8) if odt == "uint8" else nhwc.view(np.int8)
-    np.testing.assert_array_equal(view, expect)
-    assert not shadow[..., o:cpad].any()
+    # the shadow of the last output (what the next MFMA conv reads)
+    np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))

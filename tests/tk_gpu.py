@@ -156,7 +156,7 @@ def qnn_add_block(lhs, rhs, ls, lz, rs, rz, os_, oz, clip=None, want_shadow=Fals
         torch = _torch()
         n, c, h, w = lhs.shape
         # poisoned: the kernel must write every byte incl. the padded channels
-        shadow = torch.full((n, h, w, (c + 15) // 16 * 16), 0x5A, dtype=torch.uint8, device="cuda")
+        shadow = torch.full(((c + 15) // 16, n * h * w, 16), 0x5A, dtype=torch.uint8, device="cuda")
     refs = [ref(t) for t in outs]
     arr = (ctypes.POINTER(_lib.tk_tensor) * len(refs))(*[r.ptr for r in refs])
     _sync_check(lib.tk_qnn_add_block(ref(ld).ptr, ref(rd).ptr, arr, len(refs), ctypes.byref(a),
@@ -259,14 +259,17 @@ def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1,
         shadow = empty((lib.tk_conv2d_shadow_bytes(rx.ptr),), "uint8")
         packed = empty((lib.tk_conv2d_packed_weight_bytes(rw.ptr, 1),), "uint8")
         sums = empty((((o + 127) // 128) * 128,), "int32")
-        patch = empty((max(n * oh * ow, 4),), "int32")
-        _lib.check(lib.tk_nchw_to_nhwc_i8(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), st))
+        sb = lib.tk_conv2d_scratch_bytes(rx.ptr, rw.ptr, ctypes.byref(a.conv), 1)
+        assert sb >= 0
+        patch = empty((max(sb, 16),), "uint8")
+        _lib.check(lib.tk_conv2d_make_shadow(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), st))
         _lib.check(lib.tk_conv2d_pack_weight(rw.ptr, 1, ctypes.c_void_p(packed.data_ptr()),
                                              ctypes.c_void_p(sums.data_ptr()), st))
     if want_shadow:
         import torch
         cpad = (o + 15) // 16 * 16
-        shadow_out = torch.zeros((n, oh, ow, cpad), dtype=torch.uint8, device="cuda")
+        # poisoned: the kernel must write every byte incl. the padded channels
+        shadow_out = torch.full((cpad // 16, n * oh * ow, 16), 0x5A, dtype=torch.uint8, device="cuda")
     refs = [ref(t) for t in outs]
     arr = (ctypes.POINTER(_lib.tk_tensor) * len(refs))(*[r.ptr for r in refs])
     ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731

@@ -23,11 +23,15 @@ SHAPES = [  # name, C, H, O, K, stride, pad
 ]
 
 
-def main(batch=64, iters=20):
+def main(batch=64, iters=20, configs=None, reps=3):
+    """configs: list of env-var dicts (TK_ABLATE / TK_NT are read per launch); each layer is
+    timed for every config, interleaved `reps` times, and the minimum is reported."""
+    import os
+    configs = configs or [{}]
     lib = _lib.load()
     dev = torch.device("cuda")
     rng = np.random.default_rng(0)
-    tot_us = 0
+    tot = [0.0] * len(configs)
     for name, C, H, O, K, S, P in SHAPES:
         OH = (H + 2 * P - K) // S + 1
         x = torch.from_numpy(rng.integers(-128, 128, size=(batch, C, H, H)).astype(np.int8)).to(dev)
@@ -54,31 +58,47 @@ def main(batch=64, iters=20):
         shadow = torch.empty(lib.tk_conv2d_shadow_bytes(rx.ptr), dtype=torch.uint8, device=dev)
         packed = torch.empty(lib.tk_conv2d_packed_weight_bytes(rw.ptr, 1), dtype=torch.uint8, device=dev)
         sums = torch.empty(((O + 127) // 128) * 128, dtype=torch.int32, device=dev)
+        sb = lib.tk_conv2d_scratch_bytes(rx.ptr, rw.ptr, ctypes.byref(a.conv), 1)
+        scratch = torch.empty(max(sb, 16), dtype=torch.uint8, device=dev)
         sh_out = torch.zeros(batch * OH * OH * ((O + 15) // 16 * 16), dtype=torch.uint8, device=dev)
-        _lib.check(lib.tk_nchw_to_nhwc_i8(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), st))
+        _lib.check(lib.tk_conv2d_make_shadow(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), st))
         _lib.check(lib.tk_conv2d_pack_weight(rw.ptr, 1, ctypes.c_void_p(packed.data_ptr()),
                                              ctypes.c_void_p(sums.data_ptr()), st))
 
         def call():
             _lib.check(lib.tk_qnn_conv2d_block(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), rw.ptr,
                                                ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(sums.data_ptr()),
-                                               rb.ptr, arr, 4, ctypes.byref(a), None,
+                                               rb.ptr, arr, 4, ctypes.byref(a), ctypes.c_void_p(scratch.data_ptr()),
                                                ctypes.c_void_p(sh_out.data_ptr()), st))
-        call()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(iters):
-            call()
-        e1.record()
-        e1.synchronize()
-        us = e0.elapsed_time(e1) / iters * 1e3
-        tot_us += us
+        best = [float("inf")] * len(configs)
+        for _ in range(reps):
+            for ci, cfg in enumerate(configs):
+                saved = {k: os.environ.get(k) for k in cfg}
+                os.environ.update(cfg)
+                call()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(iters):
+                    call()
+                e1.record()
+                e1.synchronize()
+                best[ci] = min(best[ci], e0.elapsed_time(e1) / iters * 1e3)
+                for k, v in saved.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
         out_el = batch * O * OH * OH
         by = x.numel() + w.numel() + 4 * O + out_el * 10
         macs = out_el * C * K * K
-        print(f"{name:22s} {us:8.1f} us {by / us / 1e3:8.0f} GB/s {2 * macs / us / 1e6:8.1f} TOPS", flush=True)
-    print(f"sum {tot_us:.1f} us")
+        cols = "  ".join(f"{us:8.1f} us {by / us / 1e3:6.0f} GB/s" for us in best)
+        print(f"{name:22s} {cols}   ({2 * macs / best[0] / 1e6:.0f} TOPS)", flush=True)
+        tot = [t + u for t, u in zip(tot, best)]
+    print("configs:", configs)
+    print("sum", "  ".join(f"{t:8.1f} us" for t in tot))
 
 
 if __name__ == "__main__":
-    main()
+    import json
+    cfgs = json.loads(sys.argv[1]) if len(sys.argv) > 1 else None
+    main(configs=cfgs)
