@@ -8,10 +8,12 @@
 // the element loop is two table lookups, an add and two clamps: the kernel is a pure
 // HBM stream of 2 bytes in, 2 bytes out (+ the shadow) per element.
 //
-// Tile = 64 channels x PT pixels of one image.  Records are stored NCHW with
-// kV-byte vectors (16 when HW % 16 == 0, else 4 or 1); when the next MFMA conv
-// reads this output, the final bytes are also staged in LDS and re-emitted as its
-// int8 shadow [C_pad16/16][N·HW][16] (tk_conv2d_make_shadow layout), 16 B per store.
+// Work unit = 16 channels (one shadow group) x kV consecutive pixels of one image
+// (kV = 16 when HW % 16 == 0, else 4 or 1), lanes along the pixels: every load and
+// record store of a wave covers 64·kV contiguous bytes of one channel plane.  When
+// the next MFMA conv reads this output, the unit's final 16 x kV bytes are transposed
+// in registers (v_perm_b32) into kV 16-byte shadow chunks [C_pad16/16][N·HW][16]
+// (tk_conv2d_make_shadow layout); channels >= C are written as 0.
 #include <algorithm>
 
 #include "tk_common.h"
@@ -21,9 +23,6 @@ namespace tk {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kCT = 64;     // channels per tile
-constexpr int kPTMax = 256; // pixels per tile
-constexpr int kLdsStride = kPTMax + 4;
 
 struct AddBlockArgs {
   const uint8_t* a;
@@ -31,18 +30,25 @@ struct AddBlockArgs {
   uint8_t* add_out;
   uint8_t* clip_out;  // null: no clip record
   uint8_t* shadow;    // null: no shadow copy
-  int32_t N, C, HW, PT, tiles_per_image;
-  int32_t is_u8, zp_c, has_clip, clip_lo, clip_hi, cpad;
+  int32_t N, C, HW, G;  // G = channel groups of 16
+  int32_t is_u8, zp_c, has_clip, clip_lo, clip_hi;
   RqParams pa, pb;
   int32_t up_a, up_b;
 };
 
+// byte k of each of w0..w3, packed little-endian into one dword
+__device__ __forceinline__ uint32_t gather_byte(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int k) {
+  const uint32_t sel = (uint32_t)k | ((uint32_t)(k + 4) << 8) | 0x0c0c0000u;
+  const uint32_t lo = __builtin_amdgcn_perm(w1, w0, sel);  // {w0.k, w1.k, 0, 0}
+  const uint32_t hi = __builtin_amdgcn_perm(w3, w2, sel);  // {w2.k, w3.k, 0, 0}
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);       // {w0.k, w1.k, w2.k, w3.k}
+}
+
 template <int kV>
 __global__ __launch_bounds__(kThreads) void add_block_kernel(AddBlockArgs g) {
+  constexpr int kW = kV >= 4 ? kV / 4 : 1;  // dwords per channel row of the unit
   __shared__ int32_t lut_a[256];
   __shared__ int32_t lut_b[256];
-  __shared__ uint8_t tile[kCT * kLdsStride];
-
   const int tid = threadIdx.x;
   {
     // RequantizeOrUpcast of every representable 8-bit value (op_common.h:186-200)
@@ -52,56 +58,139 @@ __global__ __launch_bounds__(kThreads) void add_block_kernel(AddBlockArgs g) {
   }
   __syncthreads();
 
-  const int n = blockIdx.z;
-  const int c0 = blockIdx.y * kCT;
-  const int p0 = blockIdx.x * g.PT;
   const int tmin = g.is_u8 ? 0 : -128, tmax = g.is_u8 ? 255 : 127;
-  const int vec_per_row = g.PT / kV;
-  const int nvec = kCT * vec_per_row;
-  const bool want_shadow = g.shadow != nullptr;
-
-  for (int v = tid; v < nvec; v += kThreads) {
-    int cl = v / vec_per_row;
-    int pl = (v - cl * vec_per_row) * kV;
-    int c = c0 + cl, p = p0 + pl;
-    if (c >= g.C || p >= g.HW) continue;  // HW % kV == 0: vectors never straddle the plane
-    int64_t off = ((int64_t)n * g.C + c) * g.HW + p;
-    uint8_t va[kV], vb[kV], vo[kV], vc[kV];
-    __builtin_memcpy(va, g.a + off, kV);
-    __builtin_memcpy(vb, g.b + off, kV);
+  const int units_per_plane = g.HW / kV;
+  const int64_t units = (int64_t)g.N * g.G * units_per_plane;
+  const uint32_t xr = g.is_u8 ? 0x80808080u : 0u;
+  for (int64_t u = (int64_t)blockIdx.x * kThreads + tid; u < units; u += (int64_t)gridDim.x * kThreads) {
+    const int pu = (int)(u % units_per_plane);
+    const int64_t rest = u / units_per_plane;
+    const int grp = (int)(rest % g.G);
+    const int n = (int)(rest / g.G);
+    const int p = pu * kV;
+    uint32_t last[16][kW];
+    const uint8_t* __restrict__ pa = g.a;
+    const uint8_t* __restrict__ pb = g.b;
+    // 4 channel rows per batch: all 8 loads are issued before the first use (the record
+    // stores cannot alias the operands), so each wave pays the load latency 4x, not 16x
 #pragma unroll
-    for (int j = 0; j < kV; ++j) {
-      int32_t o = (int32_t)((uint32_t)lut_a[va[j]] + (uint32_t)lut_b[vb[j]] - (uint32_t)g.zp_c);
-      o = min(max(o, tmin), tmax);
-      vo[j] = (uint8_t)o;
-      vc[j] = (uint8_t)min(max(o, g.clip_lo), g.clip_hi);
+    for (int j0 = 0; j0 < 16; j0 += 4) {
+      uint8_t va[4][kV], vb[4][kV];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int c = min(grp * 16 + j0 + jj, g.C - 1);  // clamped: rows >= C are loaded but not used
+        const int64_t off = ((int64_t)n * g.C + c) * g.HW + p;
+        __builtin_memcpy(va[jj], pa + off, kV);
+        __builtin_memcpy(vb[jj], pb + off, kV);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int j = j0 + jj;
+        const int c = grp * 16 + j;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) last[j][w] = 0;
+        if (c >= g.C) continue;
+        const int64_t off = ((int64_t)n * g.C + c) * g.HW + p;
+        uint8_t vo[kV], vc[kV];
+#pragma unroll
+        for (int q = 0; q < kV; ++q) {
+          int32_t o = (int32_t)((uint32_t)lut_a[va[jj][q]] + (uint32_t)lut_b[vb[jj][q]] - (uint32_t)g.zp_c);
+          o = min(max(o, tmin), tmax);
+          vo[q] = (uint8_t)o;
+          vc[q] = (uint8_t)min(max(o, g.clip_lo), g.clip_hi);
+        }
+        store_nt<kV>(g.add_out + off, vo);
+        if (g.has_clip) store_nt<kV>(g.clip_out + off, vc);
+        __builtin_memcpy(&last[j][0], g.has_clip ? vc : vo, kV);
+      }
     }
-    store_nt<kV>(g.add_out + off, vo);
-    if (g.has_clip) store_nt<kV>(g.clip_out + off, vc);
-    if (want_shadow) {
-      const uint8_t* last = g.has_clip ? vc : vo;
+    if (!g.shadow) continue;
+    // 16 channels x kV pixels -> kV chunks of 16 channel bytes
+    uint8_t* dst = g.shadow + ((int64_t)grp * g.N * g.HW + (int64_t)n * g.HW + p) * 16;
 #pragma unroll
-      for (int j = 0; j < kV; ++j) tile[cl * kLdsStride + pl + j] = last[j];
+    for (int q = 0; q < kV; ++q) {
+      uint32_t o4[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if constexpr (kV == 1)
+          o4[d] = (last[4 * d][0] & 0xFF) | ((last[4 * d + 1][0] & 0xFF) << 8) | ((last[4 * d + 2][0] & 0xFF) << 16) |
+                  ((last[4 * d + 3][0] & 0xFF) << 24);
+        else
+          o4[d] = gather_byte(last[4 * d][q >> 2], last[4 * d + 1][q >> 2], last[4 * d + 2][q >> 2],
+                              last[4 * d + 3][q >> 2], q & 3);
+      }
+      // uint8 data is stored xor 0x80; padded channels (>= C) stay 0
+      const int cvalid = g.C - grp * 16;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) m |= (4 * d + bb < cvalid ? 0xFFu : 0u) << (8 * bb);
+        o4[d] = (o4[d] ^ xr) & m;
+      }
+      *reinterpret_cast<tk_v4i*>(dst + q * 16) = tk_v4i{(int)o4[0], (int)o4[1], (int)o4[2], (int)o4[3]};
     }
   }
-  if (!want_shadow) return;
-  __syncthreads();
+}
 
-  // shadow: one 16-channel chunk of one pixel per item (lanes along pixels: contiguous)
-  const int chunks = kCT / 16;
-  const int items = chunks * g.PT;
-  const uint8_t xr = g.is_u8 ? 0x80 : 0;
-  for (int it = tid; it < items; it += kThreads) {
-    int pl = it % g.PT;
-    int ch = it / g.PT;
-    int p = p0 + pl;
-    int cbase = c0 + ch * 16;
-    if (p >= g.HW || cbase >= g.cpad) continue;
-    uint8_t out[16];
+// Small planes (16·HW <= 16 KB, C % 16 == 0): the 16 channel rows of one image's
+// channel group are one contiguous 16·HW-byte block in NCHW, and consecutive blocks
+// are adjacent, so a workgroup streams K whole blocks (~16 KB) with flat 16-byte
+// vectors (no plane-length constraint), parks the final bytes in LDS and re-reads
+// them per pixel for the shadow.
+constexpr int kPlaneLds = 16384;
+
+__global__ __launch_bounds__(kThreads) void add_block_plane_kernel(AddBlockArgs g, int K) {
+  __shared__ int32_t lut_a[256];
+  __shared__ int32_t lut_b[256];
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kPlaneLds];
+  const int tid = threadIdx.x;
+  {
+    int32_t x = g.is_u8 ? tid : (int32_t)(int8_t)(uint8_t)tid;
+    lut_a[tid] = g.up_a ? x : rq_apply(x, 0, g.pa);
+    lut_b[tid] = g.up_b ? x : rq_apply(x, 0, g.pb);
+  }
+  __syncthreads();
+  const int tmin = g.is_u8 ? 0 : -128, tmax = g.is_u8 ? 255 : 127;
+  const int blk = 16 * g.HW;
+  const int64_t nblocks = (int64_t)g.N * g.G;
+  const int64_t nsuper = (nblocks + K - 1) / K;
+  const uint8_t* __restrict__ pa = g.a;
+  const uint8_t* __restrict__ pb = g.b;
+  for (int64_t sb = blockIdx.x; sb < nsuper; sb += gridDim.x) {
+    const int64_t b0 = sb * K;
+    const int nb = (int)min<int64_t>(K, nblocks - b0);
+    const int64_t base = b0 * blk;
+    const int nvec = nb * blk / 16;
+    for (int v = tid; v < nvec; v += kThreads) {
+      uint8_t va[16], vb[16], vo[16], vc[16];
+      __builtin_memcpy(va, pa + base + 16 * v, 16);
+      __builtin_memcpy(vb, pb + base + 16 * v, 16);
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      out[j] = (cbase + j < g.C) ? (uint8_t)(tile[(ch * 16 + j) * kLdsStride + pl] ^ xr) : 0;
-    __builtin_memcpy(g.shadow + ((int64_t)(cbase >> 4) * g.N * g.HW + (int64_t)n * g.HW + p) * 16, out, 16);
+      for (int q = 0; q < 16; ++q) {
+        int32_t o = (int32_t)((uint32_t)lut_a[va[q]] + (uint32_t)lut_b[vb[q]] - (uint32_t)g.zp_c);
+        o = min(max(o, tmin), tmax);
+        vo[q] = (uint8_t)o;
+        vc[q] = (uint8_t)min(max(o, g.clip_lo), g.clip_hi);
+      }
+      store_nt<16>(g.add_out + base + 16 * v, vo);
+      if (g.has_clip) store_nt<16>(g.clip_out + base + 16 * v, vc);
+      if (g.shadow) __builtin_memcpy(tile + 16 * v, g.has_clip ? vc : vo, 16);
+    }
+    if (!g.shadow) continue;
+    __syncthreads();
+    const uint8_t xr = g.is_u8 ? 0x80 : 0;
+    for (int it = tid; it < nb * g.HW; it += kThreads) {
+      const int bl = it / g.HW;
+      const int pix = it - bl * g.HW;
+      const int64_t gb = b0 + bl;
+      const int n = (int)(gb / g.G), grp = (int)(gb - (int64_t)n * g.G);
+      uint8_t out[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) out[j] = tile[bl * blk + j * g.HW + pix] ^ xr;
+      __builtin_memcpy(g.shadow + ((int64_t)grp * g.N * g.HW + (int64_t)n * g.HW + pix) * 16, out, 16);
+    }
+    __syncthreads();
   }
 }
 
@@ -158,33 +247,43 @@ int add_block_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* const* out
     N = a->shape[0];
     C = a->shape[1];
     HW = a->shape[2] * a->shape[3];
+  } else if (total % 1024 == 0) {
+    // no layout needed: flat view as 1-KB blocks
+    N = 1;
+    HW = 64;
+    C = total / 64;
   } else {
-    // no layout needed: view the tensor as rows of the longest power-of-4 length dividing it
+    // odd sizes: rows of the longest power-of-4 length <= 4096 dividing the tensor
     int64_t L = 4096;
     while (total % L) L /= 4;
     N = 1;
     C = total / L;
     HW = L;
-    if (C > (int64_t)kCT * 65535) {  // keep gridDim.y in range with a 2-level split
-      N = C / kCT;
-      while (C % N) --N;
-      C /= N;
-    }
   }
-  TK_CHECK_ARG(N <= 65535 && (C + kCT - 1) / kCT <= 65535 && HW <= INT32_MAX, "tensor too large");
+  TK_CHECK_ARG(HW <= INT32_MAX && C <= INT32_MAX && N <= INT32_MAX, "tensor too large");
   g.N = (int32_t)N;
   g.C = (int32_t)C;
   g.HW = (int32_t)HW;
-  g.cpad = (int32_t)((C + 15) / 16 * 16);
-  g.PT = (int32_t)std::min<int64_t>(kPTMax, (HW + 15) / 16 * 16);
-  g.tiles_per_image = (int32_t)((HW + g.PT - 1) / g.PT);
-  dim3 grid(g.tiles_per_image, (unsigned)((C + kCT - 1) / kCT), (unsigned)N);
-  if (HW % 16 == 0)
-    hipLaunchKernelGGL(add_block_kernel<16>, grid, dim3(kThreads), 0, s, g);
-  else if (HW % 4 == 0)
-    hipLaunchKernelGGL(add_block_kernel<4>, grid, dim3(kThreads), 0, s, g);
+  g.G = (int32_t)((C + 15) / 16);
+  if (C % 16 == 0 && 16 * HW <= kPlaneLds) {
+    // ~16 KB per workgroup iteration, fewer when that would leave < 2048 workgroups
+    const int64_t nblocks = N * g.G;
+    const int K = (int)std::max<int64_t>(1, std::min<int64_t>(kPlaneLds / (16 * HW), nblocks / 2048));
+    const int64_t nsuper = (nblocks + K - 1) / K;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nsuper, 256 * 16));
+    hipLaunchKernelGGL(add_block_plane_kernel, dim3(grid), dim3(kThreads), 0, s, g, K);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  }
+  const int kv = HW % 16 == 0 ? 16 : HW % 4 == 0 ? 4 : 1;
+  const int64_t units = N * g.G * (HW / kv);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((units + kThreads - 1) / kThreads, 256 * 16));
+  if (kv == 16)
+    hipLaunchKernelGGL(add_block_kernel<16>, dim3(grid), dim3(kThreads), 0, s, g);
+  else if (kv == 4)
+    hipLaunchKernelGGL(add_block_kernel<4>, dim3(grid), dim3(kThreads), 0, s, g);
   else
-    hipLaunchKernelGGL(add_block_kernel<1>, grid, dim3(kThreads), 0, s, g);
+    hipLaunchKernelGGL(add_block_kernel<1>, dim3(grid), dim3(kThreads), 0, s, g);
   TK_LAUNCH_CHECK();
   return TK_OK;
 }
