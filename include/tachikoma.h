@@ -143,17 +143,23 @@ typedef struct {
   int32_t rhs_upcast;
 } tk_qnn_add_attrs;
 
-/* A fused layer "block": qnn.conv2d|qnn.dense → nn.bias_add → qnn.requantize [→ clip].
- * One kernel computes the contraction and writes EVERY op output of the chain from
- * registers (each stays a separate trace record), so the int32 intermediates are never
- * re-read from HBM.  Requantize/bias must run along the channel axis (NCHW axis 1 /
- * dense units). */
+/* A fused layer "block": qnn.conv2d|qnn.dense → nn.bias_add → qnn.requantize
+ * [→ qnn.add(·, residual)] [→ clip].  One kernel computes the contraction and writes EVERY
+ * op output of the chain from registers (each stays a separate trace record), so the int32
+ * intermediates are never re-read from HBM.  Requantize/bias must run along the channel
+ * axis (NCHW axis 1 / dense units).
+ * outs = {conv int32, bias_add int32, requantize 8-bit, [add 8-bit], [clip 8-bit]}: with
+ * has_add the clip (if any) applies to the add (the ResNet bottleneck tail). */
 typedef struct {
   tk_conv2d_attrs conv;         /* conv blocks */
   tk_dense_attrs dense;         /* dense blocks */
   tk_requantize_attrs requantize;
   int32_t has_clip;
   int64_t clip_min, clip_max;
+  int32_t has_add;              /* MFMA conv blocks only */
+  int32_t block_is_rhs;         /* 1: the requantize output is qnn.add's rhs operand */
+  const tk_tensor* residual;    /* the other qnn.add operand (same shape and dtype, NCHW) */
+  tk_qnn_add_attrs add;
 } tk_block_attrs;
 
 /* A fused residual join: qnn.add [→ clip].  One kernel writes both records and,
@@ -259,17 +265,18 @@ enum {
   TK_NODE_GLOBAL_AVG_POOL2D = 10,
   TK_NODE_COPY = 11,       /* batch_flatten / reshape */
   TK_NODE_SHADOW = 12,     /* NCHW→NHWC int8 shadow for a conv input (not traced) */
-  TK_NODE_CONV_BLOCK = 13, /* in: data, weight, bias; outs: 3-4; ext: shadow, packed, weight_sums, scratch, shadow_out */
+  TK_NODE_CONV_BLOCK = 13, /* in: data, weight, bias, [residual]; outs: 3-5; ext: shadow, packed, weight_sums, scratch, shadow_out */
   TK_NODE_DENSE_BLOCK = 14,/* in: data, weight, bias; outs: 3-4; ext: workspace */
   TK_NODE_ADD_BLOCK = 15,  /* in: lhs, rhs; outs: 1-2 (add, clip); ext[4]: shadow_out */
 };
 
-#define TK_MAX_NODE_OUTPUTS 4
+#define TK_MAX_NODE_INPUTS 4
+#define TK_MAX_NODE_OUTPUTS 6
 
 typedef struct {
   int32_t kind;                 /* TK_NODE_* */
   int32_t n_inputs;
-  const tk_tensor* inputs[3];
+  const tk_tensor* inputs[TK_MAX_NODE_INPUTS];
   int32_t n_outputs;            /* traced outputs (0 for SHADOW) */
   tk_tensor* outputs[TK_MAX_NODE_OUTPUTS];
   void* ext[5];                 /* kind-specific device pointers (see enum) */

@@ -93,6 +93,10 @@ class tk_block_attrs(ctypes.Structure):
         ("has_clip", ctypes.c_int32),
         ("clip_min", ctypes.c_int64),
         ("clip_max", ctypes.c_int64),
+        ("has_add", ctypes.c_int32),
+        ("block_is_rhs", ctypes.c_int32),
+        ("residual", ctypes.POINTER(tk_tensor)),
+        ("add", tk_qnn_add_attrs),
     ]
 
 
@@ -141,9 +145,9 @@ class tk_node(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_int32),
         ("n_inputs", ctypes.c_int32),
-        ("inputs", ctypes.POINTER(tk_tensor) * 3),
+        ("inputs", ctypes.POINTER(tk_tensor) * 4),
         ("n_outputs", ctypes.c_int32),
-        ("outputs", ctypes.POINTER(tk_tensor) * 4),
+        ("outputs", ctypes.POINTER(tk_tensor) * 6),
         ("ext", ctypes.c_void_p * 5),
         ("attrs", tk_node_attrs),
     ]
@@ -169,7 +173,8 @@ NODE_KINDS = {
     "qnn.add": 7, "nn.max_pool2d": 8, "nn.avg_pool2d": 9, "nn.global_avg_pool2d": 10, "copy": 11, "shadow": 12,
     "conv_block": 13, "dense_block": 14, "add_block": 15,
 }
-MAX_NODE_OUTPUTS = 4
+MAX_NODE_INPUTS = 4
+MAX_NODE_OUTPUTS = 6
 
 # Every symbol declared in include/tachikoma.h, with its ctypes signature.
 _VP, _I32, _I64, _F32, _F64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double

@@ -67,6 +67,11 @@ struct GemmArgs {
   // kMode 2 sums `splits` of them and runs the epilogue
   int32_t* ws;
   int32_t splits, kper;
+  // residual join (conv blocks): add = RQ(requantize) + RQ(residual) - zp, via 256-entry LUTs
+  int32_t has_add, add_zp, add_up_b, add_up_r;
+  const uint8_t* add_res;
+  uint8_t* add_out;
+  RqParams add_pb, add_pr;
   int32_t nt;           // nontemporal record stores
   int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
                        // 8/16/32/64 skip the conv / bias_add / requantize / clip record
@@ -136,7 +141,7 @@ __device__ __forceinline__ void st_i8(uint8_t* dst, const int32_t* v, bool nt) {
 // (src/relay/qnn/op/requantize.cc:195-273) and clip (python/tvm/topi/math.py:615-640).
 template <int V, bool kBlock>
 __device__ __forceinline__ void epi_apply(const GemmArgs& g, const EpiRow& r, int32_t* v, int64_t off, bool st,
-                                          int col) {
+                                          int col, uint32_t resid, const int32_t* lut) {
   if (st && !(g.ablate & 8)) st_i32<V>(g.C + off, v, g.nt);
   if (!kBlock) return;
   const int qmin = (int)g.rq.qmin, qmax = (int)g.rq.qmax;
@@ -179,6 +184,17 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, const EpiRow& r, in
     for (int q = 0; q < V; ++q) v[q] = min(max(rq_apply(v[q], col + q, g.rq), qmin), qmax);
   }
   if (st && !(g.ablate & 32)) st_i8<V>(g.rq_out + off, v, g.nt);
+  if (g.has_add) {
+    // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out, clip to the dtype
+    const int tlo = (int)g.rq.qmin, thi = (int)g.rq.qmax;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const uint32_t rb = (resid >> (8 * q)) & 0xFFu;
+      const int32_t o = (int32_t)((uint32_t)lut[v[q] & 0xFF] + (uint32_t)lut[256 + rb] - (uint32_t)g.add_zp);
+      v[q] = min(max(o, tlo), thi);
+    }
+    if (st) st_i8<V>(g.add_out + off, v, g.nt);
+  }
   if (g.has_clip) {
 #pragma unroll
     for (int q = 0; q < V; ++q) v[q] = min(max(v[q], g.clip_lo), g.clip_hi);
@@ -204,7 +220,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   constexpr int A_CHUNKS = BM * kBK / 16 / kGemmThreads;  // 16-byte loads per thread per stage
   constexpr int B_CHUNKS = BN * kBK / 16 / kGemmThreads;
   constexpr int kStage = 2 * (BM + BN) * kBK;
-  constexpr int kEpi = BM * kEpiStride * 4 + BM * (int)sizeof(EpiRow);
+  constexpr int kEpi = BM * kEpiStride * 4 + BM * (int)sizeof(EpiRow) + (kBlock ? 512 * 4 : 0);
   __shared__ __attribute__((aligned(16))) int8_t smem[kStage > kEpi ? kStage : kEpi];
   int8_t* As = smem;
   int8_t* Bs = smem + 2 * BM * kBK;
@@ -384,6 +400,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   if (g.ablate & 4) return;
   int32_t* tileI = reinterpret_cast<int32_t*>(smem);
   EpiRow* rowc = reinterpret_cast<EpiRow*>(smem + BM * kEpiStride * 4);
+  int32_t* lut = reinterpret_cast<int32_t*>(smem + BM * kEpiStride * 4 + BM * sizeof(EpiRow));  // [2][256]
   const int hw = g.OH * g.OW;
   const bool zb_vec = g.zB_vec != nullptr, has_rb = g.RB != nullptr;
   const bool simple_fold = !zb_vec && !has_rb;
@@ -402,6 +419,12 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
       r.zp = g.rq.zps ? g.rq.zps[row] : g.rq.zp_in;
     }
     rowc[tid] = r;
+  }
+  if (kBlock && g.has_add) {
+    // RequantizeOrUpcast of every 8-bit value of both qnn.add operands (op_common.h:186-200)
+    const int32_t x = g.rq.qmin == 0 ? tid : (int32_t)(int8_t)(uint8_t)tid;
+    lut[tid] = g.add_up_b ? x : rq_apply(x, 0, g.add_pb);
+    lut[256 + tid] = g.add_up_r ? x : rq_apply(x, 0, g.add_pr);
   }
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -445,16 +468,29 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
       cbase = col;
       rstride = g.ldc;
     }
-#pragma unroll 2
+    // residual bytes of every row this thread will write, issued up front so their
+    // latency is paid once (the loads are in flight during the tile dump)
+    uint32_t resid_all[BM / 8];
+#pragma unroll
+    for (int k = 0; k < BM / 8; ++k) {
+      const int row = m0 + (tid >> 5) + 8 * k;
+      resid_all[k] = 0;
+      if (kBlock && g.has_add && colok && row < g.M)
+        resid_all[k] = *reinterpret_cast<const uint32_t*>(g.add_res + cbase + (int64_t)row * rstride);
+    }
+#pragma unroll
     for (int k = 0; k < BM / 8; ++k) {
       const int lr = (tid >> 5) + 8 * k;
       const int row = m0 + lr;
       const EpiRow r = rowc[lr];
+      const bool ok = colok && row < g.M;
+      const int64_t off = cbase + (int64_t)row * rstride;
+      const uint32_t resid = resid_all[k];
       int32_t* slot = tileI + lr * kEpiStride + c4;
       const v4i t = *reinterpret_cast<const v4i*>(slot);
       int32_t v[4] = {t.x, t.y, t.z, t.w};
       fold(v, r, col, 4);
-      epi_apply<4, kBlock>(g, r, v, cbase + (int64_t)row * rstride, store_on && colok && row < g.M, col);
+      epi_apply<4, kBlock>(g, r, v, off, store_on && ok, col, resid, lut);
       if (kBlock && g.shadow_out) *reinterpret_cast<v4i*>(slot) = v4i{v[0], v[1], v[2], v[3]};
     }
   } else {
@@ -473,10 +509,14 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
       const int lr = (tid >> 7) + 2 * k;
       const int row = m0 + lr;
       const EpiRow r = rowc[lr];
+      const bool ok = colok && row < g.M;
+      const int64_t off = cbase + (int64_t)row * rstride;
+      uint32_t resid = 0;
+      if (kBlock && g.has_add && ok) resid = g.add_res[off];
       int32_t* slot = tileI + lr * kEpiStride + lc;
       int32_t v[1] = {*slot};
       fold(v, r, col, 1);
-      epi_apply<1, kBlock>(g, r, v, cbase + (int64_t)row * rstride, store_on && colok && row < g.M, col);
+      epi_apply<1, kBlock>(g, r, v, off, store_on && ok, col, resid, lut);
       if (kBlock && g.shadow_out) *slot = v[0];
     }
   }
@@ -754,8 +794,9 @@ struct BlockIO {
 static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out, int channels, int ch_axis) {
   if (!b) return TK_OK;
   const tk_block_attrs* at = b->attrs;
-  TK_CHECK_ARG(at && b->outs && b->bias && (b->n_outs == 3 || b->n_outs == 4), "block needs bias, attrs, 3-4 outs");
-  TK_CHECK_ARG((b->n_outs == 4) == (at->has_clip != 0), "clip output count mismatch");
+  TK_CHECK_ARG(at && b->outs && b->bias, "block needs bias, attrs and outputs");
+  const int has_add = at->has_add ? 1 : 0;
+  TK_CHECK_ARG(b->n_outs == 3 + has_add + (at->has_clip ? 1 : 0), "outs = {conv, bias_add, requantize, [add], [clip]}");
   TK_CHECK_ARG(is_int(b->bias, 32) && numel(b->bias) == channels, "bias must be int32 [channels]");
   const tk_tensor* bo = b->outs[1];
   const tk_tensor* rq = b->outs[2];
@@ -764,15 +805,42 @@ static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out
   int rq_axis = at->requantize.axis;
   TK_CHECK_ARG(rq_axis == ch_axis || at->requantize.mode <= TK_RQ_TENSOR_TONEAREST,
                "requantize must run along the channel axis to fuse");
-  if (b->n_outs == 4) {
-    TK_CHECK_ARG(b->outs[3]->dtype.code == rq->dtype.code && b->outs[3]->dtype.bits == 8 &&
-                     numel(b->outs[3]) == numel(conv_out),
-                 "clip output must match the requantize output");
+  for (int k = 3; k < b->n_outs; ++k)
+    TK_CHECK_ARG(b->outs[k]->dtype.code == rq->dtype.code && b->outs[k]->dtype.bits == 8 &&
+                     numel(b->outs[k]) == numel(conv_out) && compact(b->outs[k]),
+                 "add / clip outputs must match the requantize output");
+  if (has_add) {
+    const tk_tensor* res = at->residual;
+    TK_CHECK_ARG(res && dt_of(res) == dt_of(rq) && numel(res) == numel(conv_out) && compact(res),
+                 "residual must match the requantize output (same shape and dtype)");
+    TK_CHECK_ARG(at->add.lhs.mode <= TK_RQ_TENSOR_TONEAREST && at->add.rhs.mode <= TK_RQ_TENSOR_TONEAREST,
+                 "qnn.add: per-tensor parameters only");
+    const tk_requantize_attrs& blk_side = at->block_is_rhs ? at->add.rhs : at->add.lhs;
+    const tk_requantize_attrs& res_side = at->block_is_rhs ? at->add.lhs : at->add.rhs;
+    auto rqp = [](const tk_requantize_attrs& r) {
+      RqParams q{};
+      q.mode = r.mode;
+      q.multiplier = r.multiplier;
+      q.shift = r.shift;
+      q.zp_in = r.input_zero_point;
+      q.zp_out = r.output_zero_point;
+      q.inner = 1;
+      q.C = 1;
+      return q;
+    };
+    ga.has_add = 1;
+    ga.add_res = (const uint8_t*)ptr(res);
+    ga.add_out = (uint8_t*)ptr(b->outs[3]);
+    ga.add_pb = rqp(blk_side);
+    ga.add_pr = rqp(res_side);
+    ga.add_up_b = at->block_is_rhs ? at->add.rhs_upcast : at->add.lhs_upcast;
+    ga.add_up_r = at->block_is_rhs ? at->add.lhs_upcast : at->add.rhs_upcast;
+    ga.add_zp = at->add.output_zero_point;
   }
   ga.bias = (const int32_t*)ptr(b->bias);
   ga.bias_out = (int32_t*)ptr(bo);
   ga.rq_out = (uint8_t*)ptr(rq);
-  ga.clip_out = b->n_outs == 4 ? (uint8_t*)ptr(b->outs[3]) : nullptr;
+  ga.clip_out = at->has_clip ? (uint8_t*)ptr(b->outs[3 + has_add]) : nullptr;
   ga.has_clip = at->has_clip;
   bool u8 = is_uint(rq, 8);
   int64_t lo = u8 ? 0 : -128, hi = u8 ? 255 : 127;
@@ -883,6 +951,7 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   int rc = setup_block(ga, blk, out, g.O, 1);
   if (rc) return rc;
   if (!use_mfma_conv(g, a->groups)) {
+    TK_CHECK_ARG(!(blk && blk->attrs->has_add), "residual join needs an MFMA conv block");
     // grouped / depthwise / tiny channel counts: direct VALU kernel on NCHW
     int64_t total = (int64_t)g.N * g.O * g.OH * g.OW;
     int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
@@ -1072,6 +1141,7 @@ static int dense_run(const tk_tensor* data, const tk_tensor* weight, tk_tensor* 
   ga.ldc = Nn;
   ga.vecw = Nn % 4 == 0 ? 4 : 1;
   ga.ch_is_row = 0;
+  TK_CHECK_ARG(!(blk && blk->attrs->has_add), "residual join is supported on conv blocks only");
   int rc = setup_block(ga, blk, out, Nn, 1);
   if (rc) return rc;
   ga.shadow_out = nullptr;

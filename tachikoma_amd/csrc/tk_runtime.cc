@@ -66,7 +66,7 @@ struct OwnedTensor {
 
 struct Node {
   tk_node desc{};
-  OwnedTensor in[3];
+  OwnedTensor in[TK_MAX_NODE_INPUTS];
   OwnedTensor out[TK_MAX_NODE_OUTPUTS];
   tk_tensor* outp[TK_MAX_NODE_OUTPUTS] = {};
 };
@@ -78,9 +78,12 @@ static int run_node(Node& n, hipStream_t s) {
   const tk_tensor* i2 = &n.in[2].t;
   tk_tensor* o = &n.out[0].t;
   switch (d.kind) {
-    case TK_NODE_CONV_BLOCK:
-      return conv2d_block_impl(i0, d.ext[0], i1, d.ext[1], (const int32_t*)d.ext[2], i2, n.outp, d.n_outputs,
-                               &d.attrs.block, d.ext[3], d.ext[4], s);
+    case TK_NODE_CONV_BLOCK: {
+      tk_block_attrs at = d.attrs.block;
+      if (at.has_add) at.residual = &n.in[3].t;  // the module's own copy of the descriptor
+      return conv2d_block_impl(i0, d.ext[0], i1, d.ext[1], (const int32_t*)d.ext[2], i2, n.outp, d.n_outputs, &at,
+                               d.ext[3], d.ext[4], s);
+    }
     case TK_NODE_DENSE_BLOCK:
       return dense_block_impl(i0, i1, i2, n.outp, d.n_outputs, &d.attrs.block, d.ext[0], s);
     case TK_NODE_CONV2D:
@@ -223,8 +226,12 @@ int tk_module_create(const tk_node* nodes, int n_nodes, tk_module** out) {
     const tk_node& src = nodes[i];
     tk::Node& dst = mod->nodes[i];
     dst.desc = src;
-    if (src.n_inputs < 0 || src.n_inputs > 3) {
+    if (src.n_inputs < 0 || src.n_inputs > TK_MAX_NODE_INPUTS) {
       tk::set_error("tk_module_create: node " + std::to_string(i) + " has a bad input count");
+      return TK_ERR_INVALID_ARG;
+    }
+    if (src.kind == TK_NODE_CONV_BLOCK && src.attrs.block.has_add && src.n_inputs != 4) {
+      tk::set_error("tk_module_create: node " + std::to_string(i) + ": a residual block takes the residual as input 3");
       return TK_ERR_INVALID_ARG;
     }
     for (int k = 0; k < src.n_inputs; ++k) {
@@ -245,7 +252,7 @@ int tk_module_create(const tk_node* nodes, int n_nodes, tk_module** out) {
       }
       dst.out[k].assign(src.outputs[k]);
     }
-    for (int k = 0; k < 3; ++k) dst.desc.inputs[k] = nullptr;  // resolved through dst.in / dst.out
+    for (int k = 0; k < TK_MAX_NODE_INPUTS; ++k) dst.desc.inputs[k] = nullptr;  // resolved through dst.in / dst.out
     for (int k = 0; k < TK_MAX_NODE_OUTPUTS; ++k) dst.desc.outputs[k] = nullptr;
   }
   for (auto& n : mod->nodes)

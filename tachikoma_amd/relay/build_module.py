@@ -298,6 +298,11 @@ class ExecGroup:
     ``qnn.conv2d|qnn.dense → nn.bias_add → qnn.requantize [→ clip|nn.relu]`` or residual join
     ``qnn.add [→ clip|nn.relu]`` whose every op output is still written (and traced) separately."""
     kind: str            # op name, "conv_block", "dense_block" or "add_block"
+
+    @property
+    def add(self) -> Optional["PlanOp"]:
+        """The residual qnn.add absorbed by a conv block, if any."""
+        return self.ops[3] if len(self.ops) > 3 and self.ops[3].op == "qnn.add" else None
     ops: List[PlanOp]
 
     @property
@@ -306,23 +311,50 @@ class ExecGroup:
 
 
 def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
-    """Group the plan's ops into device nodes (topological order preserved).
+    """Group the plan's ops into device nodes.
 
     A chain fuses when each op is the first consumer of its predecessor's output; other
     consumers of the intermediates stay correct because every intermediate is materialised
-    in its own HBM buffer anyway.  The requantize must run along the channel axis (1)."""
+    in its own HBM buffer anyway.  The requantize must run along the channel axis (1).
+
+    A conv block whose requantize output feeds a same-shape 8-bit ``qnn.add`` (the ResNet
+    bottleneck tail) also absorbs the add [→ clip] when nothing else reads the block's
+    intermediates; that group runs at the add's position in topological order, where the
+    add's other operand (the residual) is available.  Every other group runs at its
+    first op's position."""
     consumers: Dict[str, List[PlanOp]] = {}
     for op in plan.ops:
         for x in op.inputs:
             consumers.setdefault(x, []).append(op)
+    pos = {op.name: i for i, op in enumerate(plan.ops)}
     taken = set()
-    groups: List[ExecGroup] = []
+    placed: List[Tuple[int, int, ExecGroup]] = []
 
     def first_consumer(op: PlanOp, kind) -> Optional[PlanOp]:
         for c in consumers.get(op.name, []):
             if c.op in kind and c.inputs[0] == op.name and c.name not in taken:
                 return c
         return None
+
+    def residual_add(rq: PlanOp, chain: List[PlanOp]) -> Optional[PlanOp]:
+        cs = consumers.get(rq.name, [])
+        if len(cs) != 1 or cs[0].op != "qnn.add" or cs[0].name in taken:
+            return None
+        add = cs[0]
+        if add.out.dtype != rq.out.dtype or add.inputs[0] == add.inputs[1]:
+            return None
+        other = add.inputs[1] if add.inputs[0] == rq.name else add.inputs[0]
+        if plan.tensor(other).shape != rq.out.shape or plan.tensor(other).dtype != rq.out.dtype:
+            return None
+        # the block's intermediates must have no reader outside the chain
+        members = {c.name for c in chain} | {add.name}
+        for c in chain[:-1]:
+            if any(x.name not in members for x in consumers.get(c.name, [])):
+                return None
+        return add
+
+    def place(at: int, group: ExecGroup):
+        placed.append((at, len(placed), group))
 
     for op in plan.ops:
         if op.name in taken:
@@ -333,12 +365,18 @@ def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
             if rq is not None and rq.out.dtype in ("int8", "uint8") and rq.attrs["channel_axis"] == 1 \
                     and b.out.dtype == "int32":
                 chain = [op, b, rq]
-                cl = first_consumer(rq, ("clip", "nn.relu"))
+                add = residual_add(rq, chain) if op.op == "qnn.conv2d" else None
+                if add is not None:
+                    chain.append(add)
+                    cl = first_consumer(add, ("clip", "nn.relu"))
+                else:
+                    cl = first_consumer(rq, ("clip", "nn.relu"))
                 if cl is not None:
                     chain.append(cl)
                 for c in chain:
                     taken.add(c.name)
-                groups.append(ExecGroup("conv_block" if op.op == "qnn.conv2d" else "dense_block", chain))
+                kind = "conv_block" if op.op == "qnn.conv2d" else "dense_block"
+                place(pos[add.name] if add is not None else pos[op.name], ExecGroup(kind, chain))
                 continue
         if fuse and op.op == "qnn.add" and op.out.dtype in ("int8", "uint8") and \
                 all(plan.tensor(x).shape == op.out.shape for x in op.inputs[:2]):
@@ -348,11 +386,12 @@ def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
                 chain.append(cl)
             for c in chain:
                 taken.add(c.name)
-            groups.append(ExecGroup("add_block", chain))
+            place(pos[op.name], ExecGroup("add_block", chain))
             continue
         taken.add(op.name)
-        groups.append(ExecGroup(op.op, [op]))
-    return groups
+        place(pos[op.name], ExecGroup(op.op, [op]))
+    placed.sort(key=lambda t: (t[0], t[1]))
+    return [g for _, _, g in placed]
 
 
 class ExecutorFactory:

@@ -163,9 +163,17 @@ class DeviceModule:
                 outs = [self._ref(o.name) for o in g.ops]
                 ba = n.attrs.block
                 self._fill_rq(ba.requantize, rq_op)
-                if len(g.ops) == 4:
+                add = g.add
+                if add is not None:
+                    # residual join: the block's requantize output is one qnn.add operand
+                    ba.has_add = 1
+                    ba.block_is_rhs = int(add.inputs[1] == rq_op.name)
+                    residual = add.inputs[0] if ba.block_is_rhs else add.inputs[1]
+                    ins.append(self._ref(residual))
+                    _fill_qnn_add(ba.add, add.attrs)
+                if g.last.op in ("clip", "nn.relu"):
                     ba.has_clip = 1
-                    ba.clip_min, ba.clip_max = g.ops[3].attrs["lo"], g.ops[3].attrs["hi"]
+                    ba.clip_min, ba.clip_max = g.last.attrs["lo"], g.last.attrs["hi"]
                 if g.kind == "conv_block":
                     n.kind = _lib.NODE_KINDS["conv_block"]
                     self._conv_attrs(ba.conv, head)

@@ -255,6 +255,44 @@ def test_conv_block_requantize_shift_regimes(tk):
         np.testing.assert_array_equal(got, e)
 
 
+RESIDUAL_CASES = [
+    # N, C, H, W, O, K, stride, pad, dtype, add params (lhs s/zp, rhs s/zp, out s/zp), clip, block_is_rhs
+    (2, 32, 8, 8, 128, 1, 1, 0, "int8", (0.05, 3, 0.07, -2, 0.09, 1), (1, 127), False),
+    (2, 32, 8, 8, 128, 1, 1, 0, "int8", (0.05, 3, 0.07, -2, 0.09, 1), (1, 127), True),
+    (2, 64, 7, 7, 96, 3, 1, 1, "int8", (0.04, 0, 0.04, 0, 0.04, 0), None, False),     # both upcast, scalar stores
+    (1, 48, 12, 12, 64, 3, 1, 1, "uint8", (0.1, 130, 0.2, 120, 0.15, 128), (128, 255), True),
+    (2, 256, 7, 7, 128, 3, 1, 1, "int8", (0.05, -3, 0.06, 4, 0.08, -1), (-1, 127), False),  # split-K
+]
+
+
+@pytest.mark.parametrize("case", RESIDUAL_CASES, ids=[f"resid{i}" for i in range(len(RESIDUAL_CASES))])
+def test_conv_block_residual_join(tk, case):
+    """conv -> bias_add -> requantize -> qnn.add(., residual) [-> clip] in one block kernel, every
+    record plus the shadow of the last one against the unfused oracle ops."""
+    n, c, h, w, o, k, s, p, dt, ap, clip, rhs = case
+    rng = np.random.default_rng(1000 + o + k)
+    x = _rand(rng, (n, c, h, w), dt)
+    wt = _rand(rng, (o, c, k, k), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_in = rng.uniform(1e-5, 1e-3, size=o).astype(np.float32)
+    s_out = np.float32(0.01)
+    za = 130 if dt == "uint8" else 2
+    oh = (h + 2 * p - k) // s + 1
+    residual = _rand(rng, (n, o, oh, oh), dt)
+    outs = tk.conv2d_block(x, wt, bias, za, 0, s_in, s_out, 3, clip=clip, strides=(s, s), padding=(p, p, p, p),
+                           out_dtype=dt, want_shadow=True, residual=residual, add_params=ap, block_is_rhs=rhs)
+    conv = ref.qnn_conv2d(x, wt, za, 0, strides=(s, s), padding=(p, p, p, p))
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(3), axis=1, out_dtype=dt)
+    add = ref.qnn_add(residual, rq, *ap) if rhs else ref.qnn_add(rq, residual, *ap)
+    exp = [conv, badd, rq, add]
+    if clip is not None:
+        exp.append(ref.clip(add, *clip))
+    for got, e in zip(outs, exp):
+        np.testing.assert_array_equal(got, e)
+    np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
+
+
 @pytest.mark.parametrize("case", BLOCK_CASES, ids=[f"block{i}" for i in range(len(BLOCK_CASES))])
 def test_conv_block_matches_unfused_ops(tk, case):
     n, c, h, w, o, k, s, p, g, dx, za, odt, clip = case

@@ -226,8 +226,11 @@ def _rq_attrs(r, keep, input_scale, output_scale, output_zero_point, rounding="U
 
 
 def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1, 1), padding=(0, 0, 0, 0),
-                 dilation=(1, 1), groups=1, out_dtype="int8", want_shadow=False):
-    """Fused conv -> bias_add -> requantize(axis 1) [-> clip] through tk_qnn_conv2d_block."""
+                 dilation=(1, 1), groups=1, out_dtype="int8", want_shadow=False, residual=None, add_params=None,
+                 block_is_rhs=False):
+    """Fused conv -> bias_add -> requantize(axis 1) [-> qnn.add(., residual)] [-> clip] through
+    tk_qnn_conv2d_block.  add_params = (ls, lz, rs, rz, os, oz) of the qnn.add (lhs = the block's
+    requantize output unless block_is_rhs)."""
     lib = _lib.load()
     n, c, h, wd = x.shape
     o = w.shape[0]
@@ -237,6 +240,8 @@ def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1,
     ow = (wd + pl + pr - dilation[1] * (kw - 1) - 1) // strides[1] + 1
     xd, wdv, bd = dev(x), dev(w), dev(bias)
     outs = [empty((n, o, oh, ow), "int32"), empty((n, o, oh, ow), "int32"), empty((n, o, oh, ow), out_dtype)]
+    if residual is not None:
+        outs.append(empty((n, o, oh, ow), out_dtype))
     if clip is not None:
         outs.append(empty((n, o, oh, ow), out_dtype))
     a = _lib.tk_block_attrs()
@@ -251,6 +256,14 @@ def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1,
     if clip is not None:
         a.has_clip = 1
         a.clip_min, a.clip_max = clip
+    res_keep = None
+    if residual is not None:
+        res_keep = dev(residual)
+        res_ref = ref(res_keep)
+        a.has_add = 1
+        a.block_is_rhs = int(block_is_rhs)
+        a.residual = res_ref.ptr
+        _add_attrs(a.add, *add_params)
     rx, rw, rb = ref(xd), ref(wdv), ref(bd)
     ws_bytes = lib.tk_qnn_conv2d_workspace_bytes(rx.ptr, rw.ptr, ctypes.byref(a.conv))
     shadow = packed = sums = patch = shadow_out = None
