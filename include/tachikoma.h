@@ -241,6 +241,10 @@ int tk_clip(const tk_tensor* data, tk_tensor* out, int64_t a_min, int64_t a_max,
 /* integer cast (truncating narrow / sign- or zero-extending widen). */
 int tk_cast(const tk_tensor* data, tk_tensor* out, void* stream);
 int tk_max_pool2d(const tk_tensor* data, tk_tensor* out, const tk_pool2d_attrs* attrs, void* stream);
+/* nn.max_pool2d of an 8-bit NCHW tensor read from its conv shadow (tk_conv2d_make_shadow
+ * layout): writes the NCHW record and, when `out_shadow` is not NULL, the output's shadow. */
+int tk_max_pool2d_shadow(const tk_tensor* data, const void* data_shadow, tk_tensor* out,
+                         const tk_pool2d_attrs* attrs, void* out_shadow, void* stream);
 int tk_avg_pool2d(const tk_tensor* data, tk_tensor* out, const tk_pool2d_attrs* attrs, void* stream);
 int tk_global_avg_pool2d(const tk_tensor* data, tk_tensor* out, void* stream);
 /* batch_flatten / reshape: byte copy (kept as a node so it is traced). */
@@ -260,7 +264,7 @@ enum {
   TK_NODE_CLIP = 5,
   TK_NODE_CAST = 6,
   TK_NODE_QNN_ADD = 7,
-  TK_NODE_MAX_POOL2D = 8,
+  TK_NODE_MAX_POOL2D = 8,   /* ext[0]: input shadow (optional), ext[4]: output shadow (optional) */
   TK_NODE_AVG_POOL2D = 9,
   TK_NODE_GLOBAL_AVG_POOL2D = 10,
   TK_NODE_COPY = 11,       /* batch_flatten / reshape */

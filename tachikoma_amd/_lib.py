@@ -209,6 +209,7 @@ SIGNATURES = {
     "tk_clip": (ctypes.c_int, [_PT, _PT, _I64, _I64, _VP]),
     "tk_cast": (ctypes.c_int, [_PT, _PT, _VP]),
     "tk_max_pool2d": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_pool2d_attrs), _VP]),
+    "tk_max_pool2d_shadow": (ctypes.c_int, [_PT, _VP, _PT, ctypes.POINTER(tk_pool2d_attrs), _VP, _VP]),
     "tk_avg_pool2d": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_pool2d_attrs), _VP]),
     "tk_global_avg_pool2d": (ctypes.c_int, [_PT, _PT, _VP]),
     "tk_copy": (ctypes.c_int, [_PT, _PT, _VP]),

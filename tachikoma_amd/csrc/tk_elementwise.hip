@@ -458,6 +458,62 @@ int max_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hi
   });
 }
 
+// nn.max_pool2d of an 8-bit tensor read from its conv shadow ([C/16][N*H*W][16], uint8
+// stored xor 0x80, so signed byte order = value order): one thread per (16 channels,
+// output pixel) with lanes along the output row, 16-byte tap loads, the record written
+// NCHW and, for a following MFMA conv, the output shadow written directly.
+__global__ __launch_bounds__(kBlock) void max_pool_shadow_kernel(const uint8_t* __restrict__ sin, uint8_t* __restrict__ y,
+                                                                 uint8_t* __restrict__ sout, PoolGeom g, int G,
+                                                                 uint32_t xr) {
+  const int64_t pin = (int64_t)g.N * g.H * g.W, pout = (int64_t)g.N * g.OH * g.OW;
+  const int64_t total = (int64_t)G * pout;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < total; t += (int64_t)gridDim.x * kBlock) {
+    const int64_t q = t % pout;  // output pixel (n, oh, ow)
+    const int grp = (int)(t / pout);
+    const int ow = (int)(q % g.OW);
+    const int64_t r = q / g.OW;
+    const int oh = (int)(r % g.OH);
+    const int n = (int)(r / g.OH);
+    int8_t m[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) m[j] = -128;
+    for (int kh = 0; kh < g.kh; ++kh) {
+      const int ih = oh * g.sh - g.pt + kh * g.dh;
+      if (ih < 0 || ih >= g.H) continue;
+      for (int kw = 0; kw < g.kw; ++kw) {
+        const int iw = ow * g.sw - g.pl + kw * g.dw;
+        if (iw < 0 || iw >= g.W) continue;
+        int8_t v[16];
+        __builtin_memcpy(v, sin + ((int64_t)grp * pin + ((int64_t)n * g.H + ih) * g.W + iw) * 16, 16);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m[j] = v[j] > m[j] ? v[j] : m[j];
+      }
+    }
+    const int cvalid = g.C - grp * 16;
+    uint8_t sh[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      sh[j] = j < cvalid ? (uint8_t)m[j] : 0;  // padded channels of the shadow stay 0
+      if (j < cvalid)
+        y[(((int64_t)n * g.C + grp * 16 + j) * g.OH + oh) * g.OW + ow] = (uint8_t)((uint8_t)m[j] ^ (uint8_t)xr);
+    }
+    if (sout) __builtin_memcpy(sout + ((int64_t)grp * pout + q) * 16, sh, 16);
+  }
+}
+
+int max_pool_shadow_impl(const tk_tensor* x, const void* x_shadow, tk_tensor* y, const tk_pool2d_attrs* a,
+                         void* y_shadow, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a && x_shadow && dt_of(x) == dt_of(y) && is_int8ish(x), "bad arguments");
+  PoolGeom g;
+  if (pool_geom(x, y, a, &g)) { set_error("tk_max_pool2d_shadow: shape mismatch"); return TK_ERR_SHAPE; }
+  const int G = (g.C + 15) / 16;
+  const int64_t units = (int64_t)G * g.N * g.OH * g.OW;
+  hipLaunchKernelGGL(max_pool_shadow_kernel, dim3(grid_for(units)), dim3(kBlock), 0, s, (const uint8_t*)x_shadow,
+                     (uint8_t*)ptr(y), (uint8_t*)y_shadow, g, G, is_uint(x, 8) ? 0x80u : 0u);
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
 int avg_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s) {
   TK_CHECK_ARG(x && y && a && dt_of(x) == dt_of(y), "bad arguments");
   PoolGeom g;

@@ -202,6 +202,16 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, const EpiRow& r, in
   }
 }
 
+// 16-byte rows of every byte value: the LDS-DMA source of out-of-bounds im2col taps
+// (the input zero point) and of padding rows (0); constant-initialised in device memory.
+struct FillRows {
+  uint8_t v[256 * 16];
+  constexpr FillRows() : v{} {
+    for (int i = 0; i < 256 * 16; ++i) v[i] = (uint8_t)(i >> 4);
+  }
+};
+__device__ FillRows tk_fill_rows{};
+
 // Workgroup barrier that only drains this wave's LDS traffic.  __syncthreads() also waits
 // vmcnt(0), i.e. for every outstanding global store of the epilogue to complete, which
 // serialises the store latency once per barrier; the epilogue's barriers only order LDS.
@@ -219,7 +229,9 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   constexpr int BN = 128;       // rows of B per block (2 waves along N, 2 32-col tiles each)
   constexpr int A_CHUNKS = BM * kBK / 16 / kGemmThreads;  // 16-byte loads per thread per stage
   constexpr int B_CHUNKS = BN * kBK / 16 / kGemmThreads;
-  constexpr int kStage = 2 * (BM + BN) * kBK;
+  constexpr int kStageBytes = (BM + BN) * kBK;
+  constexpr int kRing = 3;  // LDS-DMA stages (im2col path); the plain path double-buffers
+  constexpr int kStage = (kIm2col ? kRing : 2) * kStageBytes;
   constexpr int kEpi = BM * kEpiStride * 4 + BM * (int)sizeof(EpiRow) + (kBlock ? 512 * 4 : 0);
   __shared__ __attribute__((aligned(16))) int8_t smem[kStage > kEpi ? kStage : kEpi];
   int8_t* As = smem;
@@ -340,16 +352,8 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
     kt0 = blockIdx.z * g.kper;
     nk = min(nk, kt0 + g.kper);
   }
-  if constexpr (kMode != 2) {
-  load_stage(kt0 * kBK);
-  store_stage(0);
-  __syncthreads();
-
-  for (int kt = kt0; kt < nk; ++kt) {
-    const int buf = (kt - kt0) & 1;
-    if (kt + 1 < nk) load_stage((kt + 1) * kBK);  // issue early, land under the MFMAs
-    const int8_t* a = As + buf * BM * kBK;
-    const int8_t* b = Bs + buf * BN * kBK;
+  // MFMAs of one staged K step (2 x K=32) from LDS
+  auto mma_stage = [&](const int8_t* a, const int8_t* b) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = 2 * ks + (lane >> 5);
@@ -369,10 +373,91 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
+  };
+
+  if constexpr (kMode != 2 && kIm2col) {
+    // ---- LDS-DMA pipeline (conv): a 3-stage ring filled by global_load_lds_dwordx4 with the
+    // stage two steps ahead in flight across the barrier (counted vmcnt + raw s_barrier).
+    // The LDS image is lane-linear (lane l of a wave-instruction lands at base + 16 l =
+    // row l/4, slot l%4), so the bank swizzle of lds_off goes on the SOURCE: slot s of row r
+    // holds chunk s ^ ((r >> 2) & 3), i.e. lane l loads chunk (l & 3) ^ ((l >> 4) & 3).
+    // Out-of-bounds taps read a row of the input zero point, rows past N a row of zeros.
+    const int cl = (lane & 3) ^ ((lane >> 4) & 3);
+    const int8_t* fill_src = reinterpret_cast<const int8_t*>(tk_fill_rows.v + 16 * (g.fill & 0xFFu));
+    const int8_t* zero_src = reinterpret_cast<const int8_t*>(tk_fill_rows.v);
+    // per-thread walk over K: the thread's chunk is (tap, channel offset c0) with the
+    // taps in (kh, kw) order; advanced 64 bytes per stage without divisions
+    int c0, kh, kw;
+    {
+      const int kg = kt0 * kBK + cl * 16;
+      const int tap = kg / g.cin_pad;
+      c0 = kg - tap * g.cin_pad;
+      kh = tap / g.KW;
+      kw = tap - kh * g.KW;
+    }
+    const int8_t* a_src[A_CHUNKS];
+#pragma unroll
+    for (int t = 0; t < A_CHUNKS; ++t)
+      a_src[t] = g.A + (int64_t)(m0 + (tid >> 2) + t * (kGemmThreads / 4)) * g.lda + kt0 * kBK + cl * 16;
+    int b_pix[B_CHUNKS];
+#pragma unroll
+    for (int t = 0; t < B_CHUNKS; ++t) b_pix[t] = (b_img[t] * g.H + b_ih0[t]) * g.W + b_iw0[t];
+    auto issue = [&](int slot) {
+      int8_t* sa = smem + slot * kStageBytes;
+      int8_t* sb = sa + BM * kBK;
+#pragma unroll
+      for (int t = 0; t < A_CHUNKS; ++t) {
+        __builtin_amdgcn_global_load_lds((const void*)a_src[t], (void*)(sa + (16 * wave + 64 * t) * kBK), 16, 0, 0);
+        a_src[t] += kBK;
+      }
+      const bool tap_ok = kh < g.KH;
+      const int dy = kh * g.dh, dx = kw * g.dw;
+      const int64_t plane = (int64_t)(c0 >> 4) * g.in_pix;
+#pragma unroll
+      for (int t = 0; t < B_CHUNKS; ++t) {
+        const int ih = b_ih0[t] + dy;
+        const int iw = b_iw0[t] + dx;
+        const bool inb = ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        const int8_t* src = g.B + (plane + b_pix[t] + dy * g.W + dx) * 16;
+        src = (b_valid[t] && tap_ok) ? (inb ? src : fill_src) : zero_src;
+        __builtin_amdgcn_global_load_lds((const void*)src, (void*)(sb + (16 * wave + 64 * t) * kBK), 16, 0, 0);
+      }
+      c0 += kBK;
+      while (c0 >= g.cin_pad) {
+        c0 -= g.cin_pad;
+        if (++kw == g.KW) kw = 0, ++kh;
+      }
+    };
+    const int nst = nk - kt0;
+    issue(0);
+    if (nst > 1) issue(1);
+    for (int it = 0; it < nst; ++it) {
+      // retire stage it (each stage is A_CHUNKS + B_CHUNKS LDS-DMAs per thread); stage it+1 stays in flight
+      if (it + 1 < nst) {
+        if constexpr (A_CHUNKS + B_CHUNKS == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      lds_barrier();  // stage it visible to all waves; slot (it+2)%3 (read in step it-1) is free
+      if (it + 2 < nst) issue((it + 2) % kRing);
+      const int8_t* a = smem + (it % kRing) * kStageBytes;
+      mma_stage(a, a + BM * kBK);
+    }
+  }
+  if constexpr (kMode != 2 && !kIm2col) {
+  load_stage(kt0 * kBK);
+  store_stage(0);
+  __syncthreads();
+
+  for (int kt = kt0; kt < nk; ++kt) {
+    const int buf = (kt - kt0) & 1;
+    if (kt + 1 < nk) load_stage((kt + 1) * kBK);  // issue early, land under the MFMAs
+    mma_stage(As + buf * BM * kBK, Bs + buf * BN * kBK);
     if (kt + 1 < nk) store_stage(buf ^ 1);
     __syncthreads();
   }
-  }  // kMode != 2
+  }  // plain path
   if constexpr (kMode == 1) {
     v4i* dst = reinterpret_cast<v4i*>(g.ws + (tile * gridDim.z + blockIdx.z) * kTileInts);
 #pragma unroll

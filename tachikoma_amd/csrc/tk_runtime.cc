@@ -23,6 +23,8 @@ int qnn_add_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* y, const tk_
 int add_block_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* const* outs, int n_outs,
                    const tk_add_block_attrs* at, void* shadow, hipStream_t s);
 int max_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s);
+int max_pool_shadow_impl(const tk_tensor* x, const void* x_shadow, tk_tensor* y, const tk_pool2d_attrs* a,
+                         void* y_shadow, hipStream_t s);
 int avg_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s);
 int global_avg_pool_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
 int copy_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
@@ -103,6 +105,11 @@ static int run_node(Node& n, hipStream_t s) {
     case TK_NODE_ADD_BLOCK:
       return add_block_impl(i0, i1, n.outp, d.n_outputs, &d.attrs.add_block, d.ext[4], s);
     case TK_NODE_MAX_POOL2D:
+      if (d.ext[0]) return max_pool_shadow_impl(i0, d.ext[0], o, &d.attrs.pool2d, d.ext[4], s);
+      if (d.ext[4]) {
+        int rc = max_pool_impl(i0, o, &d.attrs.pool2d, s);
+        return rc ? rc : make_shadow_impl(o, d.ext[4], s);
+      }
       return max_pool_impl(i0, o, &d.attrs.pool2d, s);
     case TK_NODE_AVG_POOL2D:
       return avg_pool_impl(i0, o, &d.attrs.pool2d, s);
@@ -200,6 +207,10 @@ int tk_cast(const tk_tensor* data, tk_tensor* out, void* stream) {
 }
 int tk_max_pool2d(const tk_tensor* data, tk_tensor* out, const tk_pool2d_attrs* attrs, void* stream) {
   return tk::max_pool_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_max_pool2d_shadow(const tk_tensor* data, const void* data_shadow, tk_tensor* out,
+                         const tk_pool2d_attrs* attrs, void* out_shadow, void* stream) {
+  return tk::max_pool_shadow_impl(data, data_shadow, out, attrs, out_shadow, tk::as_stream(stream));
 }
 int tk_avg_pool2d(const tk_tensor* data, tk_tensor* out, const tk_pool2d_attrs* attrs, void* stream) {
   return tk::avg_pool_impl(data, out, attrs, tk::as_stream(stream));

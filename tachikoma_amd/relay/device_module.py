@@ -131,10 +131,16 @@ class DeviceModule:
         conv_ops = [g.ops[0] for g in self.groups if g.ops[0].op == "qnn.conv2d"]
         mfma = {op.name: self._is_mfma_conv(op) for op in conv_ops}
         shadow_bufs: Dict[str, object] = {}
-        for op in conv_ops:
-            if mfma[op.name] and op.inputs[0] not in shadow_bufs:
-                x = self._ref(op.inputs[0])
-                shadow_bufs[op.inputs[0]] = self._scratch(self.lib.tk_conv2d_shadow_bytes(x.ptr), zero=True)
+        # 8-bit max pools read their input's shadow too (16 channels per load) and write
+        # their own output's shadow when an MFMA conv reads it
+        pool_ops = [g.ops[0] for g in self.groups if g.ops[0].op == "nn.max_pool2d" and
+                    g.ops[0].out.dtype in ("int8", "uint8") and len(g.ops[0].out.shape) == 4]
+        need = [op.inputs[0] for op in conv_ops if mfma[op.name]] + [op.inputs[0] for op in pool_ops]
+        for name in need:
+            if name not in shadow_bufs:
+                x = self._ref(name)
+                shadow_bufs[name] = self._scratch(self.lib.tk_conv2d_shadow_bytes(x.ptr), zero=True)
+        pool_names = {op.name for op in pool_ops}
         shadow_ready = set()
 
         def emit(n, kind, records):
@@ -229,6 +235,12 @@ class DeviceModule:
                     n.kind = _lib.NODE_KINDS["cast"]
                 elif kind in ("nn.max_pool2d", "nn.avg_pool2d"):
                     n.kind = _lib.NODE_KINDS[kind]
+                    if op.name in pool_names:
+                        ensure_shadow(op.inputs[0])
+                        n.ext[0] = shadow_bufs[op.inputs[0]].data_ptr()
+                        if op.name in shadow_bufs:
+                            n.ext[4] = shadow_bufs[op.name].data_ptr()
+                            shadow_ready.add(op.name)
                     pa = n.attrs.pool2d
                     pa.pool_size[:] = list(a["pool_size"])
                     pa.strides[:] = list(a["strides"])

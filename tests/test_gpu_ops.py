@@ -208,6 +208,17 @@ def test_elementwise_random(tk):
     np.testing.assert_array_equal(tk.unary("tk_cast", x8, "int32"), ref.cast(x8, "int32"))
 
 
+@pytest.mark.parametrize("shape,dt,k,st,pad", [((2, 64, 19, 17), "int8", 3, 2, 1), ((1, 40, 12, 12), "uint8", 3, 2, 1),
+                                               ((2, 24, 9, 9), "int8", 2, 2, 0)])
+def test_max_pool_from_shadow(tk, shape, dt, k, st, pad):
+    rng = np.random.default_rng(shape[1] + k)
+    x = _rand(rng, shape, dt)
+    rec, sh = tk.max_pool_shadow(x, (k, k), (st, st), (pad,) * 4)
+    exp = ref.max_pool2d(x, (k, k), (st, st), (pad,) * 4)
+    np.testing.assert_array_equal(rec, exp)
+    np.testing.assert_array_equal(sh, blocked_shadow(exp))
+
+
 def test_pools(tk):
     rng = np.random.default_rng(4)
     x8 = _rand(rng, (2, 5, 13, 11), "int8")

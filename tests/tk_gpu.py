@@ -203,6 +203,30 @@ def pool(name, x, pool_size, strides, padding, dilation=(1, 1), count_include_pa
     return out.cpu().numpy()
 
 
+def max_pool_shadow(x, pool_size, strides, padding, dilation=(1, 1)):
+    """tk_max_pool2d_shadow: input read from its conv shadow; returns (record, output shadow)."""
+    lib = _lib.load()
+    n, c, h, w = x.shape
+    kh, kw = pool_size
+    oh = (h + padding[0] + padding[2] - dilation[0] * (kh - 1) - 1) // strides[0] + 1
+    ow = (w + padding[1] + padding[3] - dilation[1] * (kw - 1) - 1) // strides[1] + 1
+    a = _lib.tk_pool2d_attrs()
+    a.pool_size[:] = list(pool_size)
+    a.strides[:] = list(strides)
+    a.padding[:] = list(padding)
+    a.dilation[:] = list(dilation)
+    xd = dev(x)
+    rx = ref(xd)
+    torch = _torch()
+    sin = torch.empty(lib.tk_conv2d_shadow_bytes(rx.ptr), dtype=torch.uint8, device="cuda")
+    _lib.check(lib.tk_conv2d_make_shadow(rx.ptr, ctypes.c_void_p(sin.data_ptr()), stream()))
+    out = empty((n, c, oh, ow), str(x.dtype))
+    sout = torch.full(((c + 15) // 16, n * oh * ow, 16), 0x5A, dtype=torch.uint8, device="cuda")
+    _sync_check(lib.tk_max_pool2d_shadow(rx.ptr, ctypes.c_void_p(sin.data_ptr()), ref(out).ptr, ctypes.byref(a),
+                                         ctypes.c_void_p(sout.data_ptr()), stream()), "tk_max_pool2d_shadow")
+    return out.cpu().numpy(), sout.cpu().numpy()
+
+
 def global_avg_pool(x):
     lib = _lib.load()
     xd = dev(x)
