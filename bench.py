@@ -77,8 +77,9 @@ def pmc_traffic(model: str, batch: int, launches: int):
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_block.json")), reverse=True):
         with open(path) as f:
             doc = json.load(f)
-        if doc.get("model") == model and doc.get("batch") == batch and doc.get("launches_per_step") == launches:
-            return doc["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+        if doc.get("model") == model and doc.get("batch") == batch:
+            # per layer-block node (split-K layers dispatch two kernels per node)
+            return doc["hbm_bytes_per_step"] / max(launches, 1), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -166,9 +167,10 @@ def main():
     node_ms /= max(args.steps, 1)
 
     # ---- roofline of the dominant kernel: the fused MFMA conv/dense layer block
-    # (qnn.conv2d|dense -> bias_add -> requantize [-> clip] in one kernel).  It is bound by
-    # HBM: every op output of the block is a trace record that must be written
-    # (int32 conv + int32 bias_add + int8 requantize + int8 clip per output element).
+    # (qnn.conv2d|dense -> bias_add -> requantize [-> qnn.add(residual)] [-> clip] in one
+    # kernel).  It is bound by HBM: every op output of the block is a trace record that must
+    # be written (int32 conv + int32 bias_add + int8 requantize [+ int8 add] + int8 clip per
+    # output element); algorithmic bytes = input + weights + bias [+ residual] + records.
     blk_ops, blk_bytes, blk_ms, n_launch = 0.0, 0.0, 0.0, 0
     ops_by_name = {o.name: o for o in m.plan.ops}
     for i, recs in enumerate(m.module.node_records):
@@ -185,7 +187,9 @@ def main():
         else:
             macs = op.out.shape[0] * w.shape[0] * w.shape[1]
         rec_bytes = sum(ops_by_name[r].out.nbytes for r in recs)
-        blk_bytes += x.nbytes + w.nbytes + (4 * op.out.shape[1] if len(recs) > 1 else 0) + rec_bytes
+        # a fused residual join also reads the other qnn.add operand
+        res_bytes = sum(ops_by_name[r].out.nbytes for r in recs if ops_by_name[r].op == "qnn.add")
+        blk_bytes += x.nbytes + w.nbytes + (4 * op.out.shape[1] if len(recs) > 1 else 0) + rec_bytes + res_bytes
         blk_ops += 2.0 * macs
         blk_ms += node_ms[i]
         n_launch += 1
@@ -237,11 +241,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_bw / 1e9, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved_bw / 1e9 / HBM_PEAK_GBPS, 4),
                          "traffic": None if traffic is None else int(traffic),
-                         "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_unit": "HBM bytes per layer-block node (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per step / nodes)",
                          "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": int(blk_bytes / max(n_launch, 1)),
+                         "algorithmic_bytes_per_node": int(blk_bytes / max(n_launch, 1)),
                          "kernel": "gemm_i8_kernel<*,*,block> fused conv/dense layer block (v_mfma_i32_32x32x32_i8)",
-                         "launches_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
+                         "nodes_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
                          "algorithmic_bytes_per_step": int(blk_bytes),
                          "mfma_tops": round(achieved_ops / 1e12, 1),
                          "mfma_frac": round(achieved_ops / INT8_MFMA_PEAK_OPS, 4)},

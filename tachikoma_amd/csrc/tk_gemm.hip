@@ -67,6 +67,8 @@ struct GemmArgs {
   // kMode 2 sums `splits` of them and runs the epilogue
   int32_t* ws;
   int32_t splits, kper;
+  // tile grid: 1-D launch of mtiles * ntiles8 workgroups (ntiles rounded up to 8), see tile_of
+  int32_t mtiles, ntiles, ntiles8, xcd_order;
   // residual join (conv blocks): add = RQ(requantize) + RQ(residual) - zp, via 256-entry LUTs
   int32_t has_add, add_zp, add_up_b, add_up_r;
   const uint8_t* add_res;
@@ -221,6 +223,21 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // the 16-lane groups of ds_read_b128 then hit 16 distinct bank slots.
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * kBK + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
+// XCD-aware tile order: workgroup L runs on XCD L % 8, so XCD x takes the N tiles x, x+8,
+// x+16, ... and for each of them all M tiles back to back: the workgroups that share an
+// N tile (the same im2col B rows) run close together on one XCD and hit its L2.
+__device__ __forceinline__ void tile_of(const GemmArgs& g, int& mt, int& nt) {
+  const int L = blockIdx.x;
+  if (!g.xcd_order) {  // plain order (N tiles fastest), for A/B measurements
+    mt = L / g.ntiles8;
+    nt = L - mt * g.ntiles8;
+    return;
+  }
+  const int local = L >> 3;
+  mt = local % g.mtiles;
+  nt = (local / g.mtiles) * 8 + (L & 7);
+}
+
 // kMode: 0 = whole K + epilogue; 1 = split-K partial (raw accumulators to g.ws);
 //        2 = sum the split-K partials of this tile + epilogue (no main loop).
 template <int MT, bool kIm2col, bool kBlock, int kMode = 0>
@@ -241,8 +258,11 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * BM;
-  const int n0 = blockIdx.x * BN;
+  int mtile, ntile;
+  tile_of(g, mtile, ntile);
+  if (ntile >= g.ntiles) return;  // padding of the N-tile count to a multiple of 8
+  const int m0 = mtile * BM;
+  const int n0 = ntile * BN;
   const int kc = tid & 3;  // this thread's 16-byte chunk within a K stage
 
   // ---- per-thread im2col state for the B rows it loads
@@ -329,7 +349,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
 
   // partial tiles live in g.ws in register order: v4i r4 of fragment (i, j) of thread tid
   constexpr int kTileInts = MT * 2 * 16 * kGemmThreads;
-  const int64_t tile = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t tile = (int64_t)mtile * g.ntiles + ntile;
   if constexpr (kMode == 2) {
     for (int sp = 0; sp < g.splits; ++sp) {
       const v4i* src = reinterpret_cast<const v4i*>(g.ws + (tile * g.splits + sp) * kTileInts);
@@ -955,6 +975,11 @@ static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out
   return TK_OK;
 }
 
+static int xcd_order() {
+  const char* e = getenv("TK_XCD");
+  return e ? atoi(e) : 1;
+}
+
 static int nt_stores() {
   const char* e = getenv("TK_NT");
   return e ? atoi(e) : 1;
@@ -1033,6 +1058,7 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   ga.ch_is_row = 1;
   ga.ablate = ablate_flags();
   ga.nt = nt_stores();
+  ga.xcd_order = xcd_order();
   int rc = setup_block(ga, blk, out, g.O, 1);
   if (rc) return rc;
   if (!use_mfma_conv(g, a->groups)) {
@@ -1095,14 +1121,17 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     ga.zA_vec = a->kernel_zero_points;
   }
   const bool mt1 = g.O <= 64 || (blk && !getenv("TK_MT2"));
-  dim3 grid((unsigned)((P + 127) / 128), (unsigned)((g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128)));
+  ga.ntiles = (int32_t)((P + 127) / 128);
+  ga.ntiles8 = (ga.ntiles + 7) / 8 * 8;
+  ga.mtiles = (g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128);
+  dim3 grid((unsigned)((int64_t)ga.mtiles * ga.ntiles8));
   const SplitPlan sp = conv_split_plan(g, mt1);
   if (sp.splits > 1) {
     TK_CHECK_ARG(sc, "split-K conv needs scratch (tk_conv2d_scratch_bytes)");
     ga.ws = (int32_t*)sc;
     ga.splits = sp.splits;
     ga.kper = sp.kper;
-    dim3 pgrid(grid.x, grid.y, (unsigned)sp.splits);
+    dim3 pgrid(grid.x, 1, (unsigned)sp.splits);
     hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1>), pgrid, dim3(kGemmThreads), 0, s, ga);
     TK_LAUNCH_CHECK();
     if (blk) hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 2>), grid, dim3(kGemmThreads), 0, s, ga);
@@ -1230,7 +1259,10 @@ static int dense_run(const tk_tensor* data, const tk_tensor* weight, tk_tensor* 
   int rc = setup_block(ga, blk, out, Nn, 1);
   if (rc) return rc;
   ga.shadow_out = nullptr;
-  dim3 grid((unsigned)((Nn + 127) / 128), (unsigned)((M + 127) / 128));
+  ga.ntiles = (int32_t)((Nn + 127) / 128);
+  ga.ntiles8 = (ga.ntiles + 7) / 8 * 8;
+  ga.mtiles = (M + 127) / 128;
+  dim3 grid((unsigned)((int64_t)ga.mtiles * ga.ntiles8));
   if (blk)
     hipLaunchKernelGGL((gemm_i8_kernel<2, false, true>), grid, dim3(kGemmThreads), 0, s, ga);
   else

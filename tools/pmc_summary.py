@@ -6,7 +6,8 @@ is doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  The last
 ``launches`` dispatches of each pass are one step (the bench runs warmup + steps
 with the same node list).
 
-usage: python tools/pmc_summary.py <pmc outdir> [launches] [--json out.json]
+usage: python tools/pmc_summary.py <pmc outdir> [launches] [--runs R] [--json out.json]
+(`bench.py --steps 2 --warmup 1 --no-trace` runs 1 + 3*2 + 1 = 8 steps)
 """
 import argparse
 import csv
@@ -31,9 +32,14 @@ def load(d):
     return per, meta
 
 
-def summarise(d, launches):
+def summarise(d, launches=None, runs=None):
+    """launches: block-kernel dispatches per step; or runs: how many steps the traced command
+    executed (launches = dispatches per pass / runs)."""
     per, meta = load(d)
     passes = sorted({k[0] for k in per})
+    if launches is None:
+        counts = {p: sum(1 for k in per if k[0] == p) for p in passes}
+        launches = min(counts.values()) // runs
     steps = defaultdict(dict)
     for p in passes:
         keys = sorted(k for k in per if k[0] == p)[-launches:]
@@ -61,11 +67,12 @@ def summarise(d, launches):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("launches", type=int, nargs="?", default=54)
+    ap.add_argument("launches", type=int, nargs="?", default=None)
+    ap.add_argument("--runs", type=int, default=8, help="steps the profiled bench command ran")
     ap.add_argument("--json")
     ap.add_argument("--workload", default="", help="extra bench args the passes ran with")
     a = ap.parse_args()
-    s = summarise(a.dir, a.launches)
+    s = summarise(a.dir, a.launches, a.runs)
     wl = a.workload.split()
     s["bench_args"] = wl
     s["model"] = wl[wl.index("--model") + 1] if "--model" in wl else "resnet50"

@@ -4,10 +4,11 @@ rocprofv3 --stats averages every dispatch of a kernel over the whole command.  T
 bench runs traced steps (D2H capture concurrent with the kernels) and compute-only
 steps (kernels alone; the roofline is measured on these), so this prints per-kernel
 average durations per phase from <dir>/run_kernel_trace.csv.  A step = one run of the
-node list (``launches`` block-kernel dispatches); it is "traced" when device copy
+node list (block-kernel dispatches per step = all of them / runs); it is "traced" when device copy
 kernels ran inside its window.
 
-usage: python tools/prof_phases.py <rocprof dir> [launches=54]
+usage: python tools/prof_phases.py <rocprof dir> [runs]
+runs = steps the bench executed: warmup + 3 x steps + 1 (default command: 2 + 15 + 1 = 18)
 """
 import csv
 import glob
@@ -16,10 +17,11 @@ import sys
 from collections import defaultdict
 
 
-def main(d, launches=54):
+def main(d, runs=18):
     path = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     gemm = [r for r in rows if "gemm_i8_kernel" in r["Kernel_Name"]]
+    launches = len(gemm) // runs
     copies = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if "copyBuffer" in r["Kernel_Name"]]
     phases = defaultdict(lambda: defaultdict(list))
     steps = defaultdict(int)
@@ -45,4 +47,4 @@ def main(d, launches=54):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 54)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 18)
