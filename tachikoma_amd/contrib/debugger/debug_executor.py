@@ -1,0 +1,197 @@
+"""Debug executor with the reference's per-node dump layout
+(python/tvm/contrib/debugger/debug_executor.py:37-347, debug_result.py:25-292).
+
+    m = debug_executor.create(lib, tachikoma_amd.rocm(0), dump_root="/tmp/tkdbg")
+    m.set_input("data", x)
+    m.run()          # per-node timing + every node output dumped
+    # /tmp/tkdbg/_tvmdbg_device_ROCM_0/{_tvmdbg_graph_dump.json, output_tensors.params,
+    #                                   _tvmdbg_execution_trace.json}
+
+Files, as the reference writes them:
+  * ``_tvmdbg_graph_dump.json`` — the executor graph (``nodes``, ``arg_nodes``,
+    ``node_row_ptr``, ``heads``, ``attrs`` with dltype/shape/storage_id), written at
+    creation, nodes rewritten like DebugResult._update_graph_json (input names, ``op``,
+    ``attrs.T``, ``shape``);
+  * ``output_tensors.params`` — NDArray-list (file_utils.cc:210-236) of every node's output,
+    keyed ``{name}____topo-index:{i}____output-num:{j}`` (debug_result.py:124), graph
+    inputs and params included as ``param`` nodes;
+  * ``_tvmdbg_execution_trace.json`` — Chrome trace, B/E events per node, pid = tid = 1,
+    ``displayTimeUnit`` "ns" (debug_result.py:151-189).
+
+Granularity: one graph node per Relay op (MRT names ``%N``), i.e. finer than the
+reference's FuseOps-fused nodes; a fused device block's ops each get their own node,
+with the block's device time attributed to its first op and 0 to the rest.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import tempfile
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ... import trace_format as tf
+from ..graph_executor import GraphModule
+
+DUMP_ROOT_PREFIX = "tvmdbg_"
+DUMP_PATH_PREFIX = "_tvmdbg_"
+GRAPH_DUMP_FILE_NAME = "_tvmdbg_graph_dump.json"
+CHROME_TRACE_FILE_NAME = "_tvmdbg_execution_trace.json"
+OUTPUT_TENSORS_FILE_NAME = "output_tensors.params"
+
+
+def executor_graph_json(plan) -> dict:
+    """The plan as a graph-executor JSON graph (graph_executor.h:226-340 layout): null nodes
+    for graph inputs and params, one tvm_op node per op, in topological order."""
+    nodes: List[dict] = []
+    index: Dict[str, int] = {}
+    dltype: List[str] = []
+    shapes: List[List[int]] = []
+    for t in list(plan.inputs) + list(plan.params):
+        index[t.name] = len(nodes)
+        nodes.append({"op": "null", "name": t.name, "inputs": []})
+        dltype.append(t.dtype)
+        shapes.append([int(d) for d in t.shape])
+    arg_nodes = list(range(len(nodes)))
+    for op in plan.ops:
+        index[op.name] = len(nodes)
+        nodes.append({
+            "op": "tvm_op", "name": op.name,
+            "inputs": [[index[x], 0, 0] for x in op.inputs],
+            "attrs": {"func_name": "tachikoma_" + op.op.replace(".", "_"), "num_inputs": str(len(op.inputs)),
+                      "num_outputs": "1", "flatten_data": "0"},
+        })
+        dltype.append(op.out.dtype)
+        shapes.append([int(d) for d in op.out.shape])
+    return {
+        "nodes": nodes,
+        "arg_nodes": arg_nodes,
+        "node_row_ptr": list(range(len(nodes) + 1)),
+        "heads": [[index[o], 0, 0] for o in plan.outputs],
+        "attrs": {"dltype": ["list_str", dltype], "shape": ["list_shape", shapes],
+                  "storage_id": ["list_int", list(range(len(nodes)))]},
+    }
+
+
+def _debug_nodes(graph: dict) -> List[dict]:
+    """DebugResult._update_graph_json: input names, op = func_name or "param", attrs.T, shape."""
+    nodes = json.loads(json.dumps(graph["nodes"]))
+    dtypes = graph["attrs"]["dltype"][1]
+    shapes = graph["attrs"]["shape"][1]
+    for i, node in enumerate(nodes):
+        node["inputs"] = [nodes[x[0]]["name"] for x in node["inputs"]]
+        if "attrs" not in node:
+            node["attrs"] = {}
+            node["op"] = "param"
+        else:
+            node["op"] = node["attrs"]["func_name"]
+        node["attrs"].update({"T": "type: " + dtypes[i]})
+        node["shape"] = shapes[i]
+    return nodes
+
+
+class GraphModuleDebug(GraphModule):
+    """GraphModule + the debug executor's dump (debug_executor.py:89-347)."""
+
+    def __init__(self, module, device_name: str, dump_root: Optional[str] = None):
+        super().__init__(module)
+        self._dump_root = dump_root or tempfile.mkdtemp(prefix=DUMP_ROOT_PREFIX)
+        folder = DUMP_PATH_PREFIX + "device_" + device_name.upper().replace("(", ":").replace(")", "").replace(":", "_")
+        self._dump_path = os.path.join(self._dump_root, folder)
+        os.makedirs(self._dump_path, 0o700, exist_ok=True)
+        self._graph = executor_graph_json(self.plan)
+        self._nodes = _debug_nodes(self._graph)
+        with open(os.path.join(self._dump_path, GRAPH_DUMP_FILE_NAME), "w") as f:
+            json.dump({**self._graph, "nodes": self._nodes}, f, indent=4, sort_keys=False)
+        self._times_s: List[List[float]] = []
+        self._outputs: Dict[str, np.ndarray] = {}
+
+    @property
+    def dump_path(self) -> str:
+        return self._dump_path
+
+    def _node_times(self, repeat: int) -> Dict[str, List[float]]:
+        """Device seconds per plan op: each device node's time goes to its first op."""
+        per_op: Dict[str, List[float]] = {n["name"]: [] for n in self._nodes}
+        for _ in range(max(1, repeat)):
+            times = self.module.run_profiled()  # ms per device node, keyed by "+".join(records)
+            seen = set()
+            for key, ms in times.items():
+                if key.startswith("<"):
+                    continue  # shadow nodes carry no op
+                recs = key.split("+")
+                for k, name in enumerate(recs):
+                    per_op[name].append(ms * 1e-3 if k == 0 else 0.0)
+                    seen.add(name)
+            for name in per_op:
+                if name not in seen:
+                    per_op[name].append(0.0)
+        return per_op
+
+    def run(self, repeat: int = 1, sort_by_time: bool = True, **inputs):  # noqa: D401  (debug_executor.run)
+        """Execute, time every node, dump the output tensors and the Chrome trace, print the table."""
+        if inputs:
+            self.set_input(**inputs)
+        per_op = self._node_times(repeat)
+        self._times_s = [per_op[n["name"]] for n in self._nodes]
+        self._outputs = {n["name"]: self.module.buffers[n["name"]].detach().cpu().numpy() for n in self._nodes}
+        self.dump_output_tensor()
+        self.dump_chrome_trace()
+        self.display_debug_result(sort_by_time)
+
+    def get_output_tensors(self) -> Dict[str, np.ndarray]:
+        return {f"{n['name']}____topo-index:{i}____output-num:0": self._outputs[n["name"]]
+                for i, n in enumerate(self._nodes)}
+
+    def dump_output_tensor(self) -> None:
+        with open(os.path.join(self._dump_path, OUTPUT_TENSORS_FILE_NAME), "wb") as f:
+            f.write(tf.save_ndarray_list(self.get_output_tensors()))
+
+    def dump_chrome_trace(self) -> None:
+        starts = np.zeros(len(self._times_s) + 1)
+        starts[1:] = np.cumsum([np.mean(t) for t in self._times_s])
+        events = []
+        for node, times, t0 in zip(self._nodes, self._times_s, starts):
+            events.append({"ts": t0 * 1e6, "tid": 1, "pid": 1, "name": node["name"], "ph": "B"})
+            events.append({"ts": (np.mean(times) + t0) * 1e6, "tid": 1, "pid": 1, "name": node["name"], "ph": "E"})
+        with open(os.path.join(self._dump_path, CHROME_TRACE_FILE_NAME), "w") as f:
+            json.dump({"displayTimeUnit": "ns", "traceEvents": events}, f)
+
+    def get_debug_result(self, sort_by_time: bool = True) -> str:
+        header = ["Node Name", "Ops", "Time(us)", "Time(%)", "Shape", "Inputs", "Outputs", "Measurements(us)"]
+        lines = ["---------", "---", "--------", "-------", "-----", "------", "-------", "----------------"]
+        total = sum(float(np.mean(t)) for t in self._times_s)
+        data = []
+        for node, times in zip(self._nodes, self._times_s):
+            if node["op"] == "param":
+                continue
+            mean = float(np.mean(times))
+            data.append([node["name"], node["op"], round(mean * 1e6, 3),
+                         round(mean / total * 100, 3) if total else 0.0, str(tuple(node["shape"])),
+                         node["attrs"]["num_inputs"], node["attrs"]["num_outputs"],
+                         str([round(t * 1e6, 3) for t in times])])
+        if sort_by_time:
+            data = sorted(data, key=lambda r: r[2], reverse=True)
+            data.append(["Total_time", "-", round(total * 1e6, 3), "-", "-", "-", "-", "-", "-"])
+        widths = [max(len(header[i]), *(len(str(r[i])) for r in data)) + 2 for i in range(len(header))]
+        fmt = "".join("{:<" + str(w) + "}" for w in widths)
+        out = [fmt.format(*header), fmt.format(*lines)]
+        out += [fmt.format(*r[:len(header)]) for r in data]
+        return "\n".join(out)
+
+    def display_debug_result(self, sort_by_time: bool = True) -> None:
+        print(self.get_debug_result(sort_by_time))
+
+    def exit(self) -> None:
+        """Remove the dump root (debug_executor.py:505-510)."""
+        if os.path.isdir(self._dump_root):
+            shutil.rmtree(self._dump_root)
+
+
+def create(lib_factory, dev=None, dump_root: Optional[str] = None) -> GraphModuleDebug:
+    """``debug_executor.create`` analogue taking what ``relay.build`` returns."""
+    module = lib_factory["default"](dev)
+    dev_id = int(module.device.index or 0)
+    return GraphModuleDebug(module, f"rocm({dev_id})", dump_root)

@@ -84,6 +84,25 @@ class TraceLayout:
                                               ctypes.c_void_p(image_ptr), image_size), "tk_trace_write_headers")
 
 
+def save_ndarray_list(arrays: Dict[str, np.ndarray]) -> bytes:
+    """NDArray-list blob (``SaveParams``, src/runtime/file_utils.cc:210-236) of host arrays, in
+    insertion order, written through the C ABI (tk_ndlist_layout / tk_ndlist_write_headers)."""
+    lib = _lib.load()
+    items = [(k, tuple(np.asarray(v).shape), str(np.asarray(v).dtype)) for k, v in arrays.items()]
+    metas, keep = _metas(items)
+    offs = (ctypes.c_int64 * max(1, len(items)))()
+    total = lib.tk_ndlist_layout(metas, len(items), offs)
+    if total < 0:
+        _lib.check(int(total), "tk_ndlist_layout")
+    blob = bytearray(int(total))
+    buf = (ctypes.c_char * len(blob)).from_buffer(blob)
+    _lib.check(lib.tk_ndlist_write_headers(metas, len(items), buf, len(blob)), "tk_ndlist_write_headers")
+    for i, v in enumerate(arrays.values()):
+        raw = np.ascontiguousarray(v).reshape(-1).view(np.uint8)
+        blob[offs[i]:offs[i] + raw.size] = raw.tobytes()
+    return bytes(blob)
+
+
 def header_json(meta: Dict[str, Any]) -> str:
     text = json.dumps(meta, separators=(",", ":"), sort_keys=False)
     return text + " " * JSON_SLACK

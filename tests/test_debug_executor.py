@@ -1,0 +1,85 @@
+"""Debug-executor dump: the reference's on-disk layout
+(python/tvm/contrib/debugger/debug_result.py; checks mirror
+tests/python/unittest/test_runtime_graph_debug.py:105-191)."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tachikoma_amd import zoo
+from tachikoma_amd.contrib.debugger.debug_executor import _debug_nodes, executor_graph_json
+from tachikoma_amd.relay.build_module import lower
+
+
+def test_executor_graph_json_layout():
+    m = zoo.lenet5(batch=1)
+    plan = lower(m.mod, m.params)
+    g = executor_graph_json(plan)
+    for k in ("nodes", "arg_nodes", "node_row_ptr", "heads", "attrs"):
+        assert k in g
+    n_args = len(plan.inputs) + len(plan.params)
+    assert len(g["nodes"]) == n_args + len(plan.ops)
+    assert g["arg_nodes"] == list(range(n_args))
+    assert all(g["nodes"][i]["op"] == "null" for i in g["arg_nodes"])
+    for i, node in enumerate(g["nodes"][n_args:], start=n_args):
+        assert node["op"] == "tvm_op"
+        assert all(src[0] < i for src in node["inputs"])  # topological
+    assert g["node_row_ptr"] == list(range(len(g["nodes"]) + 1))
+    assert len(g["attrs"]["dltype"][1]) == len(g["attrs"]["shape"][1]) == len(g["nodes"])
+    nodes = _debug_nodes(g)
+    assert nodes[0]["op"] == "param" and nodes[-1]["op"].startswith("tachikoma_")
+    assert nodes[-1]["attrs"]["T"].startswith("type: ")
+
+
+@pytest.mark.gpu
+def test_debug_dump_matches_oracle(device, tmp_path):
+    import tachikoma_amd
+    from oracle import graph_ref
+    from tachikoma_amd import relay, trace_format as tf
+    from tachikoma_amd.contrib.debugger import debug_executor
+
+    model = zoo.lenet5(batch=2)
+    x = model.sample_inputs(0, 2)
+    lib = relay.build(model.mod, target="mi355x", params=model.params)
+    mod = debug_executor.create(lib, tachikoma_amd.rocm(0), dump_root=str(tmp_path / "dbg"))
+    mod.set_input("data", x)
+    directory = mod.dump_path
+    assert os.path.basename(directory) == "_tvmdbg_device_ROCM_0"
+    assert os.listdir(directory) == ["_tvmdbg_graph_dump.json"]
+    with open(os.path.join(directory, "_tvmdbg_graph_dump.json")) as f:
+        dumped = json.load(f)
+    for k in ("nodes", "arg_nodes", "node_row_ptr", "heads", "attrs"):
+        assert k in dumped
+    mod.run()
+    assert len(os.listdir(directory)) == 3
+
+    with open(os.path.join(directory, "output_tensors.params"), "rb") as f:
+        tensors = tf.parse_ndarray_list(f.read(), copy=True)
+    exp = graph_ref.calibrate(model.mod, model.params, {"data": x})
+    pattern = re.compile(r"^(.+)____topo-index:(\d+)____output-num:0$")
+    seen = 0
+    for i, (key, arr) in enumerate(tensors.items()):
+        mt = pattern.match(key)
+        assert mt and int(mt.group(2)) == i
+        name = mt.group(1)
+        want = exp[name] if name in exp else model.params[name]
+        np.testing.assert_array_equal(arr, want)
+        seen += 1
+    assert seen == len(dumped["nodes"])
+
+    with open(os.path.join(directory, "_tvmdbg_execution_trace.json")) as f:
+        trace = json.load(f)
+    assert trace["displayTimeUnit"] == "ns"
+    events = trace["traceEvents"]
+    assert len(events) == 2 * len(dumped["nodes"])
+    assert all(e["ph"] in ("B", "E") and e["pid"] == 1 and e["tid"] == 1 for e in events)
+    assert events[0]["ts"] == 0 and events[0]["ph"] == "B"
+
+    lines = mod.get_debug_result().split("\n")
+    assert re.split(r"  [ ]*", lines[0])[:-1] == ["Node Name", "Ops", "Time(us)", "Time(%)", "Shape", "Inputs",
+                                                   "Outputs", "Measurements(us)"]
+    assert lines[-1].startswith("Total_time")
+    mod.exit()
+    assert not os.path.exists(directory)
