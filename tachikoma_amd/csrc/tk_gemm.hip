@@ -141,9 +141,32 @@ __device__ __forceinline__ void st_i8(uint8_t* dst, const int32_t* v, bool nt) {
 // soon as it is complete, transforming v in place (conv → bias_add → requantize →
 // clip); mirrors nn.bias_add (int32 wrap), RequantizeLowerInt + clip/cast
 // (src/relay/qnn/op/requantize.cc:195-273) and clip (python/tvm/topi/math.py:615-640).
+// requantize core of one element (mode is uniform; used where constants vary per element)
+__device__ __forceinline__ int32_t rq_core(int32_t t, int mode, int32_t m, int32_t sh) {
+  switch (mode) {
+    case TK_RQ_IDENTITY: return t;
+    case TK_RQ_TENSOR_POW2: return qms_pow2(t, sh);
+    case TK_RQ_TENSOR_TONEAREST:
+    case TK_RQ_AXIS_TONEAREST: return qms_tonearest(t, m, sh);
+    default: return qms_upward(t, m, sh);
+  }
+}
+
+// Column constants of a dense block (channel = column), loaded once per thread.
+__device__ __forceinline__ EpiRow col_consts(const GemmArgs& g, int col) {
+  EpiRow c{};
+  const int ch = min(col, g.N - 1);
+  c.bias = g.bias[ch];
+  const bool axis = g.rq.mode >= TK_RQ_AXIS_UPWARD;
+  c.m = axis ? g.rq.ms[ch] : g.rq.multiplier;
+  c.s = axis ? g.rq.ss[ch] : g.rq.shift;
+  c.zp = g.rq.zps ? g.rq.zps[ch] : g.rq.zp_in;
+  return c;
+}
+
 template <int V, bool kBlock>
 __device__ __forceinline__ void epi_apply(const GemmArgs& g, const EpiRow& r, int32_t* v, int64_t off, bool st,
-                                          int col, uint32_t resid, const int32_t* lut) {
+                                          int col, uint32_t resid, const int32_t* lut, const EpiRow* cc) {
   if (st && !(g.ablate & 8)) st_i32<V>(g.C + off, v, g.nt);
   if (!kBlock) return;
   const int qmin = (int)g.rq.qmin, qmax = (int)g.rq.qmax;
@@ -178,12 +201,16 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, const EpiRow& r, in
 #pragma unroll
     for (int q = 0; q < V; ++q) v[q] = min(max((int32_t)((uint32_t)g.rq.zp_out + (uint32_t)v[q]), qmin), qmax);
   } else {
-    // channel = column (dense blocks)
+    // channel = column (dense blocks): per-column constants from registers
 #pragma unroll
-    for (int q = 0; q < V; ++q) v[q] = (int32_t)((uint32_t)v[q] + (uint32_t)g.bias[col + q]);
+    for (int q = 0; q < V; ++q) v[q] = (int32_t)((uint32_t)v[q] + (uint32_t)cc[q].bias);
     if (st && !(g.ablate & 16)) st_i32<V>(g.bias_out + off, v, g.nt);
+    const int mode = g.rq.mode;
 #pragma unroll
-    for (int q = 0; q < V; ++q) v[q] = min(max(rq_apply(v[q], col + q, g.rq), qmin), qmax);
+    for (int q = 0; q < V; ++q) {
+      const int32_t t = rq_core((int32_t)((uint32_t)v[q] - (uint32_t)cc[q].zp), mode, cc[q].m, cc[q].s);
+      v[q] = min(max((int32_t)((uint32_t)g.rq.zp_out + (uint32_t)t), qmin), qmax);
+    }
   }
   if (st && !(g.ablate & 32)) st_i8<V>(g.rq_out + off, v, g.nt);
   if (g.has_add) {
@@ -351,20 +378,41 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   constexpr int kTileInts = MT * 2 * 16 * kGemmThreads;
   const int64_t tile = (int64_t)mtile * g.ntiles + ntile;
   if constexpr (kMode == 2) {
-    for (int sp = 0; sp < g.splits; ++sp) {
-      const v4i* src = reinterpret_cast<const v4i*>(g.ws + (tile * g.splits + sp) * kTileInts);
+    // sum the partial tiles; two splits' loads are issued together (MT = 1: 16 x 16 B
+    // in flight per lane) so the reduction pays the L2 latency once per pair
+    constexpr int kPair = MT == 1 ? 2 : 1;
+    auto add_tile = [&](const v4i* t) {
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int r4 = 0; r4 < 4; ++r4) {
-            const v4i t = src[((i * 2 + j) * 4 + r4) * kGemmThreads + tid];
-            acc[i][j][4 * r4] += t.x;
-            acc[i][j][4 * r4 + 1] += t.y;
-            acc[i][j][4 * r4 + 2] += t.z;
-            acc[i][j][4 * r4 + 3] += t.w;
+            const v4i u = t[(i * 2 + j) * 4 + r4];
+            acc[i][j][4 * r4] += u.x;
+            acc[i][j][4 * r4 + 1] += u.y;
+            acc[i][j][4 * r4 + 2] += u.z;
+            acc[i][j][4 * r4 + 3] += u.w;
           }
+    };
+    int sp = 0;
+    for (; sp + kPair <= g.splits; sp += kPair) {
+      v4i t[kPair][MT * 2 * 4];
+#pragma unroll
+      for (int p = 0; p < kPair; ++p) {
+        const v4i* src = reinterpret_cast<const v4i*>(g.ws + (tile * g.splits + sp + p) * kTileInts);
+#pragma unroll
+        for (int f = 0; f < MT * 2 * 4; ++f) t[p][f] = src[f * kGemmThreads + tid];
+      }
+#pragma unroll
+      for (int p = 0; p < kPair; ++p) add_tile(t[p]);
+    }
+    for (; sp < g.splits; ++sp) {
+      const v4i* src = reinterpret_cast<const v4i*>(g.ws + (tile * g.splits + sp) * kTileInts);
+      v4i t[MT * 2 * 4];
+#pragma unroll
+      for (int f = 0; f < MT * 2 * 4; ++f) t[f] = src[f * kGemmThreads + tid];
+      add_tile(t);
     }
   }
   int kt0 = 0, nk = g.k_pad / kBK;
@@ -573,6 +621,9 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
       cbase = col;
       rstride = g.ldc;
     }
+    EpiRow cc[4] = {};
+    if (kBlock && !g.ch_is_row)
+      for (int q = 0; q < 4; ++q) cc[q] = col_consts(g, col + q);
     // residual bytes of every row this thread will write, issued up front so their
     // latency is paid once (the loads are in flight during the tile dump)
     uint32_t resid_all[BM / 8];
@@ -595,7 +646,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
       const v4i t = *reinterpret_cast<const v4i*>(slot);
       int32_t v[4] = {t.x, t.y, t.z, t.w};
       fold(v, r, col, 4);
-      epi_apply<4, kBlock>(g, r, v, off, store_on && ok, col, resid, lut);
+      epi_apply<4, kBlock>(g, r, v, off, store_on && ok, col, resid, lut, cc);
       if (kBlock && g.shadow_out) *reinterpret_cast<v4i*>(slot) = v4i{v[0], v[1], v[2], v[3]};
     }
   } else {
@@ -603,6 +654,8 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
     const int lc = tid & (BN - 1);
     const int col = n0 + lc;
     const bool colok = col < g.N;
+    EpiRow cc1{};
+    if (kBlock && !g.ch_is_row) cc1 = col_consts(g, col);
     int64_t cbase = col, rstride = g.ldc;
     if (g.out_nchw) {
       const int img = col / hw;
@@ -621,7 +674,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
       int32_t* slot = tileI + lr * kEpiStride + lc;
       int32_t v[1] = {*slot};
       fold(v, r, col, 1);
-      epi_apply<1, kBlock>(g, r, v, off, store_on && ok, col, resid, lut);
+      epi_apply<1, kBlock>(g, r, v, off, store_on && ok, col, resid, lut, &cc1);
       if (kBlock && g.shadow_out) *slot = v[0];
     }
   }
@@ -1201,13 +1254,31 @@ int conv2d_impl(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, 
 }
 
 // ---------------------------------------------------------------- dense
+// Split-K of a dense GEMM (MT = 2 tiles, 128 x 128): classifier heads have a handful of
+// tiles and a long K (ResNet-50 fc: 8 tiles, 32 k-steps), so split until ~512 workgroups
+// run, keeping >= 2 k-steps per split.
+static SplitPlan dense_split_plan(int64_t M, int64_t Nn, int64_t K) {
+  const int64_t tiles = ((M + 127) / 128) * ((Nn + 127) / 128);
+  const int nk = (int)((K + kBK - 1) / kBK);
+  SplitPlan sp{1, nk, tiles};
+  if (tiles >= 256) return sp;
+  // the reduce pass reads splits sequentially: a few splits already fill the chip
+  int want = (int)std::min<int64_t>(std::min<int64_t>((512 + tiles - 1) / tiles, nk / 2), 4);
+  if (want <= 1) return sp;
+  sp.kper = (nk + want - 1) / want;
+  sp.splits = (nk + sp.kper - 1) / sp.kper;
+  return sp;
+}
+
 int64_t dense_workspace_bytes(const tk_tensor* data, const tk_tensor* weight) {
   if (!data || !weight || data->ndim != 2 || weight->ndim != 2) return -1;
   int64_t M = data->shape[0], K = data->shape[1], Nn = weight->shape[0];
   int64_t k_pad = (K + kBK - 1) / kBK * kBK;
   int64_t mrows = (M + 127) / 128 * 128, nrows = (Nn + 127) / 128 * 128;
   auto al = [](int64_t v) { return (v + 255) / 256 * 256; };
-  return al(mrows * k_pad) + al(nrows * k_pad) + al(mrows * 4) + al(nrows * 4);
+  const SplitPlan sp = dense_split_plan(M, Nn, K);
+  const int64_t partial = sp.splits > 1 ? sp.tiles * sp.splits * (int64_t)(2 * 2 * 16 * kGemmThreads) * 4 : 0;
+  return al(mrows * k_pad) + al(nrows * k_pad) + al(mrows * 4) + al(nrows * 4) + al(partial);
 }
 
 static int dense_run(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_dense_attrs* a,
@@ -1228,6 +1299,8 @@ static int dense_run(const tk_tensor* data, const tk_tensor* weight, tk_tensor* 
   int32_t* dsum = (int32_t*)ws;
   ws += al((int64_t)mrows * 4);
   int32_t* wsum = (int32_t*)ws;
+  ws += al((int64_t)nrows * 4);
+  int32_t* partial = (int32_t*)ws;
   int du = is_uint(data, 8), wu = is_uint(weight, 8);
   TK_CHECK_ARG(!(wu && a->kernel_zero_points), "per-unit zero points with uint8 weights are not supported");
   hipLaunchKernelGGL(pad_rows_kernel, dim3(mrows), dim3(256), 0, s, (const uint8_t*)ptr(data), dpad, dsum, M, K, k_pad, du);
@@ -1263,10 +1336,20 @@ static int dense_run(const tk_tensor* data, const tk_tensor* weight, tk_tensor* 
   ga.ntiles8 = (ga.ntiles + 7) / 8 * 8;
   ga.mtiles = (M + 127) / 128;
   dim3 grid((unsigned)((int64_t)ga.mtiles * ga.ntiles8));
-  if (blk)
+  const SplitPlan sp = dense_split_plan(M, Nn, K);
+  if (sp.splits > 1) {
+    ga.ws = partial;
+    ga.splits = sp.splits;
+    ga.kper = sp.kper;
+    hipLaunchKernelGGL((gemm_i8_kernel<2, false, false, 1>), dim3(grid.x, 1, sp.splits), dim3(kGemmThreads), 0, s, ga);
+    TK_LAUNCH_CHECK();
+    if (blk) hipLaunchKernelGGL((gemm_i8_kernel<2, false, true, 2>), grid, dim3(kGemmThreads), 0, s, ga);
+    else hipLaunchKernelGGL((gemm_i8_kernel<2, false, false, 2>), grid, dim3(kGemmThreads), 0, s, ga);
+  } else if (blk) {
     hipLaunchKernelGGL((gemm_i8_kernel<2, false, true>), grid, dim3(kGemmThreads), 0, s, ga);
-  else
+  } else {
     hipLaunchKernelGGL((gemm_i8_kernel<2, false, false>), grid, dim3(kGemmThreads), 0, s, ga);
+  }
   TK_LAUNCH_CHECK();
   return TK_OK;
 }

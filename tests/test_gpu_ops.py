@@ -124,6 +124,7 @@ def test_conv2d_per_channel_kernel_zp(tk):
     (64, 2048, 1000, "int8", "int8", -7, 0),
     (5, 77, 13, "uint8", "uint8", 120, 131),
     (130, 70, 129, "int8", "uint8", 0, 128),
+    (16, 1024, 200, "int8", "int8", 5, -3),          # split-K with both zero points
 ])
 def test_dense_random(tk, m, k, n, dx, dw_, za, zw):
     rng = np.random.default_rng(m * 1000 + k)
