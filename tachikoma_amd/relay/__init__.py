@@ -6,6 +6,7 @@ from .expr import (Call, Constant, Expr, Function, IRModule, TensorType, Var, co
 from .op import (avg_pool2d, batch_flatten, bias_add, cast, clip, global_avg_pool2d, max_pool2d,  # noqa: F401
                  relu, reshape)
 from . import op as _op
+from .parser import ParseError, astext, fromtext, parse  # noqa: F401  (tvm.parser.parse / fromtext)
 
 
 class _NN:

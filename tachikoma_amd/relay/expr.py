@@ -89,6 +89,11 @@ class IRModule:
     def __getitem__(self, name: str) -> Function:
         return self.functions[name]
 
+    def astext(self, show_meta_data: bool = True) -> str:
+        """Relay text (IRModule.astext); parse it back with ``relay.parse``."""
+        from .parser import astext
+        return astext(self, show_meta_data)
+
 
 def var(name_hint: str, shape: Sequence[int] = (), dtype: str = "float32") -> Var:
     return Var(name_hint, shape, dtype)
