@@ -46,6 +46,8 @@ def parse():
                    help="memory: trace image complete in pinned host RAM; file: also write each step to disk")
     p.add_argument("--out-dir", default="/tmp")
     p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse N>1 on one GPU")
     return p.parse_args()
 
 
@@ -92,9 +94,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            torch.cuda.set_device(local_rank % torch.cuda.device_count())
+            dist.init_process_group(backend="gloo")
+    device = torch.device("cuda", torch.cuda.current_device())
+    coll_dev = device if args.dist_backend == "nccl" else torch.device("cpu")
 
     from tachikoma_amd import relay, shard, zoo
     from tachikoma_amd.contrib import graph_executor
@@ -104,7 +111,7 @@ def main():
     model = model_fn(batch=B)
     _log(f"rank {rank}/{world}: building {args.model} batch {B} on {device}")
     lib = relay.build(model.mod, target="mi355x", params=model.params)
-    m = graph_executor.GraphModule(lib["default"](local_rank))
+    m = graph_executor.GraphModule(lib["default"](device.index))
     # weak scaling: B samples per GPU; this rank traces samples [offset, offset + B) of the global batch
     offset, count = shard.shard_range(B * world, world, rank)
     x = model.sample_inputs(offset, count)
@@ -146,7 +153,9 @@ def main():
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tc = t.to(coll_dev)
+        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        t = tc
     elapsed_max = float(t.item())
 
     # ---- compute-only steps (no capture): the kernels alone, each node bracketed by HIP
@@ -203,7 +212,7 @@ def main():
     m.run(trace=not args.no_trace)
     if not args.no_trace:
         cap.synchronize()
-    digests = shard.gather_digests(m.module.records_digest(stream))
+    digests = shard.gather_digests(m.module.records_digest(stream).to(coll_dev))
     if args.sink == "file" and not args.no_trace:
         path = shard.shard_file(args.out_dir, rank)
         cap.write(path)
@@ -216,7 +225,7 @@ def main():
         traces = B * world * args.steps
         value = traces / elapsed_max
         cpu = None
-        if not args.skip_cpu:
+        if not args.skip_cpu and world == 1:  # reported on rank 0 at N = 1 only
             _log("cpu baseline (oracle port) ...")
             cpu = cpu_baseline(model_fn, B, args.cpu_budget_s)
         macs_per_sample = zoo.macs_per_sample(model_fn(batch=1))
