@@ -15,6 +15,7 @@
 // python/tvm/relay/qnn/op/legalizations.py:195-226 pads with zeros after the shift).
 // The epilogue writes int32 NCHW directly (lanes run along pixels: coalesced).
 #include <algorithm>
+#include <type_traits>
 #include <climits>
 #include <cstdlib>
 #include <cstring>
@@ -25,6 +26,7 @@ namespace tk {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 64;          // bytes of K per stage
 constexpr int kGemmThreads = 256;
@@ -74,9 +76,20 @@ struct GemmArgs {
   const uint8_t* add_res;
   uint8_t* add_out;
   RqParams add_pb, add_pr;
+  // lean im2col walk (unitap): every 64-byte K stage lies in one tap (cin_pad % 64 == 0, or a
+  // 1x1 conv), so the stage's source offset is uniform and each lane only tests its row's
+  // tap bitmask (taps <= 64); cgroups = cin_pad / 16
+  int32_t unitap, cgroups;
+  // p / (OH*OW) and p / OW as (p * magic) >> 40 (0: plain division), exact for p * d < 2^40
+  uint64_t mg_hw, mg_ow;
+  // fast block epilogue (conv blocks, 4-column vectors, requantize UPWARD): every record
+  // byte offset fits 32 bits, so stores go through buffer descriptors (out_bytes32 = 1)
+  int32_t fast_epi;
+  uint32_t out_elems;   // N * M: elements of each record
   int32_t nt;           // nontemporal record stores
   int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
-                       // 8/16/32/64 skip the conv / bias_add / requantize / clip record
+                       // 8/16/32/64 skip the conv / bias_add / requantize / clip record,
+                       // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs
 };
 
 // Writes one element of every output of a fused block.  Mirrors, per element:
@@ -240,6 +253,7 @@ struct FillRows {
   }
 };
 __device__ FillRows tk_fill_rows{};
+__device__ int32_t tk_zero_words[4] = {0, 0, 0, 0};
 
 // Workgroup barrier that only drains this wave's LDS traffic.  __syncthreads() also waits
 // vmcnt(0), i.e. for every outstanding global store of the epilogue to complete, which
@@ -267,17 +281,70 @@ __device__ __forceinline__ void tile_of(const GemmArgs& g, int& mt, int& nt) {
 
 // kMode: 0 = whole K + epilogue; 1 = split-K partial (raw accumulators to g.ws);
 //        2 = sum the split-K partials of this tile + epilogue (no main loop).
-template <int MT, bool kIm2col, bool kBlock, int kMode = 0>
-__global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(GemmArgs g) {
+// load through a global-address-space pointer (struct members are generic pointers: flat
+// loads would wait on both vmcnt and lgkmcnt)
+template <typename T>
+__device__ __forceinline__ T ldg(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
+
+// per-tensor requantize core (no per-channel arrays): the qnn.add operand tables
+__device__ __forceinline__ int32_t rq_tensor(int32_t t, const RqParams& p) {
+  t = (int32_t)((uint32_t)t - (uint32_t)p.zp_in);
+  switch (p.mode) {
+    case TK_RQ_TENSOR_POW2: t = qms_pow2(t, p.shift); break;
+    case TK_RQ_TENSOR_UPWARD: t = qms_upward(t, p.multiplier, p.shift); break;
+    case TK_RQ_TENSOR_TONEAREST: t = qms_tonearest(t, p.multiplier, p.shift); break;
+    default: break;
+  }
+  return (int32_t)((uint32_t)p.zp_out + (uint32_t)t);
+}
+
+// ---- fast conv-block epilogue helpers
+// buffer descriptor of a record (uniform base and size): stores at offsets >= bytes are
+// dropped by the range check, which masks the tile edges without branches
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+constexpr int kAuxNT = 2;  // cache policy: nontemporal
+constexpr uint32_t kOffDrop = 0x3FFFFFF0u;  // element offset of a masked lane (x4 + 15 stays out of range)
+
+__device__ __forceinline__ uint32_t pack4u(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  // low bytes of a, b, c, d -> one dword (two v_perm_b32 + v_or)
+  const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0c0c0400u);
+  const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x04000c0cu);
+  return lo | hi;
+}
+
+__device__ __forceinline__ int32_t clamp_i32(int32_t x, int32_t lo, int32_t hi) { return min(max(x, lo), hi); }
+
+// counted wait for this wave's global loads (vmcnt immediate): at most n outstanding
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <int MT, bool kIm2col, bool kBlock, int kMode = 0, int kRing = 3>
+__global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 4 ? 3 : 2) : 2) void gemm_i8_kernel(
+    GemmArgs g) {
   constexpr int BM = 64 * MT;   // rows of A per block (2 waves along M, MT 32-row tiles each)
   constexpr int BN = 128;       // rows of B per block (2 waves along N, 2 32-col tiles each)
   constexpr int A_CHUNKS = BM * kBK / 16 / kGemmThreads;  // 16-byte loads per thread per stage
   constexpr int B_CHUNKS = BN * kBK / 16 / kGemmThreads;
   constexpr int kStageBytes = (BM + BN) * kBK;
-  constexpr int kRing = 3;  // LDS-DMA stages (im2col path); the plain path double-buffers
+  // kRing: LDS-DMA stages of the im2col path (kRing - 1 in flight); the plain path double-buffers
   constexpr int kStage = (kIm2col ? kRing : 2) * kStageBytes;
   constexpr int kEpi = BM * kEpiStride * 4 + BM * (int)sizeof(EpiRow) + (kBlock ? 512 * 4 : 0);
   __shared__ __attribute__((aligned(16))) int8_t smem[kStage > kEpi ? kStage : kEpi];
+  __shared__ int s_fast;  // tile-uniform: every row's requantize takes the mul_hi form (shift <= -2)
   int8_t* As = smem;
   int8_t* Bs = smem + 2 * BM * kBK;
 
@@ -285,11 +352,30 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  if (kBlock && tid == 0) s_fast = 1;  // visible after the first barrier; only cleared later
   int mtile, ntile;
   tile_of(g, mtile, ntile);
   if (ntile >= g.ntiles) return;  // padding of the N-tile count to a multiple of 8
   const int m0 = mtile * BM;
   const int n0 = ntile * BN;
+  // per-row epilogue constants (threads < BM, one row each), loaded up front: they land
+  // during the main loop
+  // (raw loads from a dummy word where an array is absent: the per-row/scalar choice is
+  // made at the epilogue, so no path waits for the loads here)
+  EpiRow row_pre{};
+  const bool rq_axis = g.rq.mode >= TK_RQ_AXIS_UPWARD;
+  if (kMode != 1 && tid < BM) {
+    const int row = min(m0 + tid, g.M - 1);
+    auto raw = [&](const int32_t* p, bool use) { return ldg(use ? p + row : tk_zero_words); };
+    row_pre.ra = (uint32_t)raw(g.RA, g.RA != nullptr);
+    row_pre.za = (uint32_t)raw(g.zA_vec, g.zA_vec != nullptr);
+    if (kBlock && g.ch_is_row) {
+      row_pre.bias = raw(g.bias, true);
+      row_pre.m = raw(g.rq.ms, rq_axis);
+      row_pre.s = raw(g.rq.ss, rq_axis);
+      row_pre.zp = raw(g.rq.zps, g.rq.zps != nullptr);
+    }
+  }
   const int kc = tid & 3;  // this thread's 16-byte chunk within a K stage
 
   // ---- per-thread im2col state for the B rows it loads
@@ -301,12 +387,12 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
     int p = n0 + row;
     b_valid[t] = p < g.N;
     if (kIm2col) {
-      int pp = b_valid[t] ? p : 0;
-      int hw = g.OH * g.OW;
-      int img = pp / hw;
-      int rem = pp - img * hw;
-      int oh = rem / g.OW;
-      int ow = rem - oh * g.OW;
+      const uint32_t pp = b_valid[t] ? p : 0;
+      const int hw = g.OH * g.OW;
+      const int img = g.mg_hw ? (int)(((uint64_t)pp * g.mg_hw) >> 40) : (int)(pp / (uint32_t)hw);
+      const uint32_t rem = pp - img * hw;
+      const int oh = g.mg_ow ? (int)(((uint64_t)rem * g.mg_ow) >> 40) : (int)(rem / (uint32_t)g.OW);
+      const int ow = rem - oh * g.OW;
       b_img[t] = img;
       b_ih0[t] = oh * g.sh - g.pt;
       b_iw0[t] = ow * g.sw - g.pl;
@@ -444,73 +530,133 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   };
 
   if constexpr (kMode != 2 && kIm2col) {
-    // ---- LDS-DMA pipeline (conv): a 3-stage ring filled by global_load_lds_dwordx4 with the
-    // stage two steps ahead in flight across the barrier (counted vmcnt + raw s_barrier).
+    // ---- LDS-DMA pipeline (conv): a kRing-stage ring filled by global_load_lds_dwordx4 with
+    // kRing - 1 stages in flight across the barrier (counted vmcnt + raw s_barrier).
     // The LDS image is lane-linear (lane l of a wave-instruction lands at base + 16 l =
     // row l/4, slot l%4), so the bank swizzle of lds_off goes on the SOURCE: slot s of row r
     // holds chunk s ^ ((r >> 2) & 3), i.e. lane l loads chunk (l & 3) ^ ((l >> 4) & 3).
-    // Out-of-bounds taps read a row of the input zero point, rows past N a row of zeros.
+    // Out-of-bounds taps read a row of the input zero point; rows past N and K padding
+    // (whose weights are 0) read it too.
     const int cl = (lane & 3) ^ ((lane >> 4) & 3);
     const int8_t* fill_src = reinterpret_cast<const int8_t*>(tk_fill_rows.v + 16 * (g.fill & 0xFFu));
-    const int8_t* zero_src = reinterpret_cast<const int8_t*>(tk_fill_rows.v);
-    // per-thread walk over K: the thread's chunk is (tap, channel offset c0) with the
-    // taps in (kh, kw) order; advanced 64 bytes per stage without divisions
-    int c0, kh, kw;
-    {
-      const int kg = kt0 * kBK + cl * 16;
-      const int tap = kg / g.cin_pad;
-      c0 = kg - tap * g.cin_pad;
-      kh = tap / g.KW;
-      kw = tap - kh * g.KW;
-    }
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     const int8_t* a_src[A_CHUNKS];
 #pragma unroll
     for (int t = 0; t < A_CHUNKS; ++t)
       a_src[t] = g.A + (int64_t)(m0 + (tid >> 2) + t * (kGemmThreads / 4)) * g.lda + kt0 * kBK + cl * 16;
-    int b_pix[B_CHUNKS];
+    const int nst = nk - kt0;
+    auto pipeline = [&](auto&& issue) {
 #pragma unroll
-    for (int t = 0; t < B_CHUNKS; ++t) b_pix[t] = (b_img[t] * g.H + b_ih0[t]) * g.W + b_iw0[t];
-    auto issue = [&](int slot) {
-      int8_t* sa = smem + slot * kStageBytes;
-      int8_t* sb = sa + BM * kBK;
-#pragma unroll
-      for (int t = 0; t < A_CHUNKS; ++t) {
-        __builtin_amdgcn_global_load_lds((const void*)a_src[t], (void*)(sa + (16 * wave + 64 * t) * kBK), 16, 0, 0);
-        a_src[t] += kBK;
-      }
-      const bool tap_ok = kh < g.KH;
-      const int dy = kh * g.dh, dx = kw * g.dw;
-      const int64_t plane = (int64_t)(c0 >> 4) * g.in_pix;
-#pragma unroll
-      for (int t = 0; t < B_CHUNKS; ++t) {
-        const int ih = b_ih0[t] + dy;
-        const int iw = b_iw0[t] + dx;
-        const bool inb = ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-        const int8_t* src = g.B + (plane + b_pix[t] + dy * g.W + dx) * 16;
-        src = (b_valid[t] && tap_ok) ? (inb ? src : fill_src) : zero_src;
-        __builtin_amdgcn_global_load_lds((const void*)src, (void*)(sb + (16 * wave + 64 * t) * kBK), 16, 0, 0);
-      }
-      c0 += kBK;
-      while (c0 >= g.cin_pad) {
-        c0 -= g.cin_pad;
-        if (++kw == g.KW) kw = 0, ++kh;
+      for (int st = 0; st < kRing - 1; ++st)
+        if (st < nst) issue(st);
+      for (int it = 0; it < nst; ++it) {
+        // retire stage it (A_CHUNKS + B_CHUNKS LDS-DMAs per thread and stage); the later
+        // stages already issued stay in flight
+        wait_vm(min(nst - 1 - it, kRing - 2) * (A_CHUNKS + B_CHUNKS));
+        lds_barrier();  // stage it visible to all waves; the slot read in step it-1 is free
+        if (it + kRing - 1 < nst) issue((it + kRing - 1) % kRing);
+        const int8_t* a = smem + (it % kRing) * kStageBytes;
+        if (!(g.ablate & 512)) mma_stage(a, a + BM * kBK);
       }
     };
-    const int nst = nk - kt0;
-    issue(0);
-    if (nst > 1) issue(1);
-    for (int it = 0; it < nst; ++it) {
-      // retire stage it (each stage is A_CHUNKS + B_CHUNKS LDS-DMAs per thread); stage it+1 stays in flight
-      if (it + 1 < nst) {
-        if constexpr (A_CHUNKS + B_CHUNKS == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    auto issue_a = [&](int8_t* sa) {
+#pragma unroll
+      for (int t = 0; t < A_CHUNKS; ++t) {
+        if (!(g.ablate & 128))
+          __builtin_amdgcn_global_load_lds((const void*)a_src[t], (void*)(sa + (16 * wave_u + 64 * t) * kBK), 16, 0, 0);
+        a_src[t] += kBK;
       }
-      lds_barrier();  // stage it visible to all waves; slot (it+2)%3 (read in step it-1) is free
-      if (it + 2 < nst) issue((it + 2) % kRing);
-      const int8_t* a = smem + (it % kRing) * kStageBytes;
-      mma_stage(a, a + BM * kBK);
+    };
+    if (g.unitap) {
+      // lane-constant part of the source (pixel + the lane's channel group) and the taps
+      // that are in bounds for the lane's rows; the stage part (channel group, tap) is uniform
+      const int8_t* lane_base[B_CHUNKS];
+      uint64_t tmask[B_CHUNKS];
+#pragma unroll
+      for (int t = 0; t < B_CHUNKS; ++t) {
+        const int64_t pix = ((int64_t)b_img[t] * g.H + b_ih0[t]) * g.W + b_iw0[t];
+        lane_base[t] = g.B + (pix + (int64_t)cl * g.in_pix) * 16;
+        uint32_t rows = 0, cols = 0;
+        for (int kh = 0; kh < g.KH; ++kh) {
+          const int ih = b_ih0[t] + kh * g.dh;
+          rows |= (uint32_t)(ih >= 0 && ih < g.H) << kh;
+        }
+        for (int kw = 0; kw < g.KW; ++kw) {
+          const int iw = b_iw0[t] + kw * g.dw;
+          cols |= (uint32_t)(iw >= 0 && iw < g.W) << kw;
+        }
+        uint64_t m = 0;
+        for (int kh = 0; kh < g.KH; ++kh)
+          if ((rows >> kh) & 1) m |= (uint64_t)cols << (kh * g.KW);
+        tmask[t] = b_valid[t] ? m : 0;
+      }
+      int cg, kh, kw;  // uniform: channel group of the stage's first chunk, tap
+      {
+        const int k0 = kt0 * kBK;
+        const int tap = k0 / g.cin_pad;
+        cg = (k0 - tap * g.cin_pad) >> 4;
+        kh = tap / g.KW;
+        kw = tap - kh * g.KW;
+      }
+      const int64_t grp_bytes = g.in_pix * 16;
+      const int64_t row_bytes = (int64_t)g.dh * g.W * 16;
+      pipeline([&](int slot) {
+        int8_t* sa = smem + slot * kStageBytes;
+        issue_a(sa);
+        int8_t* sb = sa + BM * kBK;
+        const int tap = kh * g.KW + kw;
+        const int64_t soff = cg * grp_bytes + kh * row_bytes + (int64_t)(kw * g.dw) * 16;
+        const bool grp_ok = cg + cl < g.cgroups;  // K padding of a 1x1 conv with cin_pad % 64 != 0
+#pragma unroll
+        for (int t = 0; t < B_CHUNKS; ++t) {
+          const bool ok = ((tmask[t] >> tap) & 1) && grp_ok;
+          const int8_t* src = ok ? lane_base[t] + soff : fill_src;
+          if (!(g.ablate & 256))
+            __builtin_amdgcn_global_load_lds((const void*)src, (void*)(sb + (16 * wave_u + 64 * t) * kBK), 16, 0, 0);
+        }
+        cg += 4;
+        if (cg >= g.cgroups) {
+          cg = 0;
+          if (++kw == g.KW) kw = 0, ++kh;
+        }
+      });
+    } else {
+      // general walk: the thread's chunk is (tap, channel offset c0) with the taps in
+      // (kh, kw) order; advanced 64 bytes per stage without divisions
+      int c0, kh, kw;
+      {
+        const int kg = kt0 * kBK + cl * 16;
+        const int tap = kg / g.cin_pad;
+        c0 = kg - tap * g.cin_pad;
+        kh = tap / g.KW;
+        kw = tap - kh * g.KW;
+      }
+      int b_pix[B_CHUNKS];
+#pragma unroll
+      for (int t = 0; t < B_CHUNKS; ++t) b_pix[t] = (b_img[t] * g.H + b_ih0[t]) * g.W + b_iw0[t];
+      pipeline([&](int slot) {
+        int8_t* sa = smem + slot * kStageBytes;
+        issue_a(sa);
+        int8_t* sb = sa + BM * kBK;
+        const bool tap_ok = kh < g.KH;
+        const int dy = kh * g.dh, dx = kw * g.dw;
+        const int64_t plane = (int64_t)(c0 >> 4) * g.in_pix;
+#pragma unroll
+        for (int t = 0; t < B_CHUNKS; ++t) {
+          const int ih = b_ih0[t] + dy;
+          const int iw = b_iw0[t] + dx;
+          const bool inb = ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+          const int8_t* src = g.B + (plane + b_pix[t] + dy * g.W + dx) * 16;
+          src = (b_valid[t] && tap_ok && inb) ? src : fill_src;
+          if (!(g.ablate & 256))
+            __builtin_amdgcn_global_load_lds((const void*)src, (void*)(sb + (16 * wave_u + 64 * t) * kBK), 16, 0, 0);
+        }
+        c0 += kBK;
+        while (c0 >= g.cin_pad) {
+          c0 -= g.cin_pad;
+          if (++kw == g.KW) kw = 0, ++kh;
+        }
+      });
     }
   }
   if constexpr (kMode != 2 && !kIm2col) {
@@ -526,6 +672,10 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
     __syncthreads();
   }
   }  // plain path
+  // every load issued so far (LDS-DMA stages, the row constants) has landed: a wait the
+  // compiler sees (the ring's counted waits are inline asm), so that it does not add
+  // conservative vmcnt(0) waits before the epilogue's LDS reads
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   if constexpr (kMode == 1) {
     v4i* dst = reinterpret_cast<v4i*>(g.ws + (tile * gridDim.z + blockIdx.z) * kTileInts);
 #pragma unroll
@@ -555,29 +705,42 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   EpiRow* rowc = reinterpret_cast<EpiRow*>(smem + BM * kEpiStride * 4);
   int32_t* lut = reinterpret_cast<int32_t*>(smem + BM * kEpiStride * 4 + BM * sizeof(EpiRow));  // [2][256]
   const int hw = g.OH * g.OW;
+  // residual bytes of every row this thread writes (4-column paths), issued before the tile
+  // dump so that their latency overlaps it
+  uint32_t resid_pre[BM / 8];
+  if constexpr (kBlock) {
+    if (g.has_add && g.vecw >= 4) {
+      const int col = n0 + (tid & 31) * 4;
+      const int img = col / hw;
+      const int64_t cbase = (int64_t)img * g.M * hw + (col - img * hw);
+#pragma unroll
+      for (int k = 0; k < BM / 8; ++k) {
+        const int row = m0 + (tid >> 5) + 8 * k;
+        const bool ok = col < g.N && row < g.M;
+        resid_pre[k] = ldg(reinterpret_cast<const uint32_t*>(g.add_res + (ok ? cbase + (int64_t)row * hw : 0)));
+      }
+    }
+  }
   const bool zb_vec = g.zB_vec != nullptr, has_rb = g.RB != nullptr;
   const bool simple_fold = !zb_vec && !has_rb;
   lds_barrier();  // staging buffers are free
   if (tid < BM) {
-    const int row = min(m0 + tid, g.M - 1);
-    EpiRow r{};
-    r.ra = g.RA ? (uint32_t)g.RA[row] : 0u;
-    r.za = g.zA_vec ? (uint32_t)g.zA_vec[row] : (uint32_t)g.zA;
-    r.fold = (uint32_t)g.k_eff * r.za * (uint32_t)g.zB - (uint32_t)g.zB * r.ra;
+    EpiRow r = row_pre;
+    if (!g.RA) r.ra = 0;
+    if (!g.zA_vec) r.za = (uint32_t)g.zA;
     if (kBlock && g.ch_is_row) {
-      r.bias = g.bias[row];
-      const bool axis = g.rq.mode >= TK_RQ_AXIS_UPWARD;
-      r.m = axis ? g.rq.ms[row] : g.rq.multiplier;
-      r.s = axis ? g.rq.ss[row] : g.rq.shift;
-      r.zp = g.rq.zps ? g.rq.zps[row] : g.rq.zp_in;
+      if (!rq_axis) r.m = g.rq.multiplier, r.s = g.rq.shift;
+      if (!g.rq.zps) r.zp = g.rq.zp_in;
     }
+    r.fold = (uint32_t)g.k_eff * r.za * (uint32_t)g.zB - (uint32_t)g.zB * r.ra;
+    if (kBlock && g.ch_is_row && r.s > -2) s_fast = 0;
     rowc[tid] = r;
   }
   if (kBlock && g.has_add) {
     // RequantizeOrUpcast of every 8-bit value of both qnn.add operands (op_common.h:186-200)
     const int32_t x = g.rq.qmin == 0 ? tid : (int32_t)(int8_t)(uint8_t)tid;
-    lut[tid] = g.add_up_b ? x : rq_apply(x, 0, g.add_pb);
-    lut[256 + tid] = g.add_up_r ? x : rq_apply(x, 0, g.add_pr);
+    lut[tid] = g.add_up_b ? x : rq_tensor(x, g.add_pb);
+    lut[256 + tid] = g.add_up_r ? x : rq_tensor(x, g.add_pr);
   }
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -593,6 +756,83 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
   }
   lds_barrier();
 
+  bool done = false;
+  if constexpr (kBlock) {
+    if (g.fast_epi && simple_fold && s_fast && !g.ablate) {
+      // ---- fast path (tile-uniform): 4 consecutive columns x rows (tid>>5) + 8k, every
+      // record through a buffer descriptor (masked lanes get an out-of-range offset),
+      // requantize in the mul_hi form: ((x - zp)·m + 2^(sh2-1)) >> sh2 over the high word
+      done = true;
+      const int c4 = (tid & 31) * 4;
+      const int col = n0 + c4;
+      const bool colok = col < g.N;
+      const int img = col / hw;
+      const uint32_t cbase = (uint32_t)img * (uint32_t)g.M * (uint32_t)hw + (uint32_t)(col - img * hw);
+      const uint32_t n4 = g.out_elems * 4u;
+      const auto r_conv = rec_rsrc(g.C, n4), r_bias = rec_rsrc(g.bias_out, n4);
+      const auto r_rq = rec_rsrc(g.rq_out, g.out_elems);
+      const auto r_add = rec_rsrc(g.add_out, g.has_add ? g.out_elems : 0u);
+      const auto r_clip = rec_rsrc(g.clip_out, g.has_clip ? g.out_elems : 0u);
+      const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
+      uint32_t offs[BM / 8];
+#pragma unroll
+      for (int k = 0; k < BM / 8; ++k) {
+        const int row = m0 + (tid >> 5) + 8 * k;
+        offs[k] = (colok && row < g.M) ? cbase + (uint32_t)row * (uint32_t)hw : kOffDrop;
+      }
+      auto rows = [&](auto add_c, auto clip_c, auto aux_c) {
+        constexpr bool ADD = decltype(add_c)::value, CLIP = decltype(clip_c)::value;
+        constexpr int AUX = decltype(aux_c)::value;
+#pragma unroll
+        for (int k = 0; k < BM / 8; ++k) {
+          const int lr = (tid >> 5) + 8 * k;
+          const EpiRow r = rowc[lr];
+          int32_t* slot = tileI + lr * kEpiStride + c4;
+          const v4i t = *reinterpret_cast<const v4i*>(slot);
+          const uint32_t o = offs[k];
+          // int32 wrap-around arithmetic in unsigned lanes (the reference accumulates mod 2^32)
+          v4u v = __builtin_bit_cast(v4u, t) + r.fold;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, AUX);
+          v += (uint32_t)r.bias;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, AUX);
+          const int sh2 = -r.s - 1;
+          const uint32_t rnd = 1u << (sh2 - 1);
+          int32_t q[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            q[e] = clamp_i32(zpo + ((int32_t)((uint32_t)__mulhi((int32_t)(v[e] - (uint32_t)r.zp), r.m) + rnd) >> sh2),
+                             qmin, qmax);
+          __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, AUX);
+          if constexpr (ADD) {
+            // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((resid_pre[k] >> (8 * e)) & 0xFFu)] - g.add_zp, qmin, qmax);
+            __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, AUX);
+          }
+          if constexpr (CLIP) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], g.clip_lo, g.clip_hi);
+            __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, AUX);
+          }
+          if (g.shadow_out) *reinterpret_cast<v4i*>(slot) = v4i{q[0], q[1], q[2], q[3]};
+        }
+      };
+      using T = std::true_type;
+      using F = std::false_type;
+      auto dispatch = [&](auto aux_c) {
+        if (g.has_add) {
+          if (g.has_clip) rows(T{}, T{}, aux_c);
+          else rows(T{}, F{}, aux_c);
+        } else {
+          if (g.has_clip) rows(F{}, T{}, aux_c);
+          else rows(F{}, F{}, aux_c);
+        }
+      };
+      if (g.fast_epi == 2) dispatch(std::integral_constant<int, 0>{});
+      else dispatch(std::integral_constant<int, kAuxNT>{});
+    }
+  }
   // zero-point folding of V columns: acc - zB[col]*RA[row] - zA[row]*RB[col] + K*zA[row]*zB[col]
   auto fold = [&](int32_t* v, const EpiRow& r, int col, int V) {
     if (simple_fold) {
@@ -607,7 +847,8 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
     }
   };
   const bool store_on = !(g.ablate & 2);
-  if (g.vecw >= 4) {
+  if (done) {
+  } else if (g.vecw >= 4) {
     // 4 consecutive columns x rows (tid>>5) + 8k; the 4 never straddle an image plane
     const int c4 = (tid & 31) * 4;
     const int col = n0 + c4;
@@ -624,16 +865,6 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
     EpiRow cc[4] = {};
     if (kBlock && !g.ch_is_row)
       for (int q = 0; q < 4; ++q) cc[q] = col_consts(g, col + q);
-    // residual bytes of every row this thread will write, issued up front so their
-    // latency is paid once (the loads are in flight during the tile dump)
-    uint32_t resid_all[BM / 8];
-#pragma unroll
-    for (int k = 0; k < BM / 8; ++k) {
-      const int row = m0 + (tid >> 5) + 8 * k;
-      resid_all[k] = 0;
-      if (kBlock && g.has_add && colok && row < g.M)
-        resid_all[k] = *reinterpret_cast<const uint32_t*>(g.add_res + cbase + (int64_t)row * rstride);
-    }
 #pragma unroll
     for (int k = 0; k < BM / 8; ++k) {
       const int lr = (tid >> 5) + 8 * k;
@@ -641,7 +872,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? 4 : 2) void gemm_i8_kernel(
       const EpiRow r = rowc[lr];
       const bool ok = colok && row < g.M;
       const int64_t off = cbase + (int64_t)row * rstride;
-      const uint32_t resid = resid_all[k];
+      const uint32_t resid = (kBlock && g.has_add) ? resid_pre[k] : 0u;
       int32_t* slot = tileI + lr * kEpiStride + c4;
       const v4i t = *reinterpret_cast<const v4i*>(slot);
       int32_t v[4] = {t.x, t.y, t.z, t.w};
@@ -1038,12 +1269,20 @@ static int nt_stores() {
   return e ? atoi(e) : 1;
 }
 
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+static int ring_depth() {
+  const char* e = getenv("TK_RING");
+  const int r = e ? atoi(e) : 3;
+  return r >= 3 && r <= 5 ? r : 3;
+}
+
 static int ablate_flags() {
-  static int v = [] {
-    const char* e = getenv("TK_ABLATE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
+  const char* e = getenv("TK_ABLATE");
+  return e ? atoi(e) : 0;
 }
 
 // Split-K plan of an MFMA conv: layers whose tile grid cannot give every CU a workgroup
@@ -1156,7 +1395,25 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   ga.sh = a->strides[0]; ga.sw = a->strides[1]; ga.pt = a->padding[0]; ga.pl = a->padding[1];
   ga.dh = a->dilation[0]; ga.dw = a->dilation[1];
   ga.taps = g.KH * g.KW;
+  ga.cgroups = g.cin_pad / 16;
+  ga.unitap = ga.taps <= 64 && (g.cin_pad % kBK == 0 || ga.taps == 1) && env_int("TK_UNITAP", 1);
+  {
+    // (p * ceil(2^40 / d)) >> 40 == p / d while p * d < 2^40
+    const uint64_t hw = (uint64_t)g.OH * g.OW;
+    auto magic = [](uint64_t d, uint64_t pmax) -> uint64_t {
+      return pmax * d < (1ull << 40) ? ((1ull << 40) + d - 1) / d : 0;
+    };
+    ga.mg_hw = magic(hw, (uint64_t)P);
+    ga.mg_ow = magic((uint64_t)g.OW, hw);
+  }
   ga.fill = rep4(za);
+  {
+    const uint64_t elems = (uint64_t)P * g.O;
+    ga.out_elems = (uint32_t)std::min<uint64_t>(elems, 0xFFFFFFFFull);
+    const int mode = blk ? blk->attrs->requantize.mode : -1;
+    ga.fast_epi = blk && elems * 4 < 0xFFFFFFC0ull && (g.OH * g.OW) % 4 == 0 &&
+                  (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD) ? env_int("TK_FASTEPI", 1) : 0;
+  }
   ga.out_nchw = 1;
   {
     const int hwv = g.OH * g.OW;  // store vectors must not straddle an image plane
@@ -1179,19 +1436,31 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   ga.mtiles = (g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128);
   dim3 grid((unsigned)((int64_t)ga.mtiles * ga.ntiles8));
   const SplitPlan sp = conv_split_plan(g, mt1);
+  const int ring = ring_depth();
   if (sp.splits > 1) {
     TK_CHECK_ARG(sc, "split-K conv needs scratch (tk_conv2d_scratch_bytes)");
     ga.ws = (int32_t*)sc;
     ga.splits = sp.splits;
     ga.kper = sp.kper;
     dim3 pgrid(grid.x, 1, (unsigned)sp.splits);
-    hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1>), pgrid, dim3(kGemmThreads), 0, s, ga);
+    switch (ring) {
+      case 4: hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1, 4>), pgrid, dim3(kGemmThreads), 0, s, ga); break;
+      case 5: hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1, 5>), pgrid, dim3(kGemmThreads), 0, s, ga); break;
+      default: hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1>), pgrid, dim3(kGemmThreads), 0, s, ga);
+    }
     TK_LAUNCH_CHECK();
     if (blk) hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 2>), grid, dim3(kGemmThreads), 0, s, ga);
     else hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 2>), grid, dim3(kGemmThreads), 0, s, ga);
   } else if (mt1) {
-    if (blk) hipLaunchKernelGGL((gemm_i8_kernel<1, true, true>), grid, dim3(kGemmThreads), 0, s, ga);
-    else hipLaunchKernelGGL((gemm_i8_kernel<1, true, false>), grid, dim3(kGemmThreads), 0, s, ga);
+    if (blk) {
+      switch (ring) {
+        case 4: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 4>), grid, dim3(kGemmThreads), 0, s, ga); break;
+        case 5: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 5>), grid, dim3(kGemmThreads), 0, s, ga); break;
+        default: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true>), grid, dim3(kGemmThreads), 0, s, ga);
+      }
+    } else {
+      hipLaunchKernelGGL((gemm_i8_kernel<1, true, false>), grid, dim3(kGemmThreads), 0, s, ga);
+    }
   } else {
     if (blk) hipLaunchKernelGGL((gemm_i8_kernel<2, true, true>), grid, dim3(kGemmThreads), 0, s, ga);
     else hipLaunchKernelGGL((gemm_i8_kernel<2, true, false>), grid, dim3(kGemmThreads), 0, s, ga);
