@@ -238,10 +238,14 @@ _LIB: Optional[ctypes.CDLL] = None
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load the HIP library (fails loudly: there is no fallback path)."""
+    """Load the HIP library (fails loudly: there is no fallback path).
+
+    ``TK_LIB_PATH`` substitutes another build of the same library (A/B kernel timing in
+    tools/, one process per build on the same box)."""
     global _LIB
     if _LIB is not None:
         return _LIB
+    path = os.environ.get("TK_LIB_PATH", path)
     if not os.path.exists(path):
         raise TachikomaError(
             f"{path} not found: build it with `python tachikoma_amd/build.py` "

@@ -83,13 +83,19 @@ struct GemmArgs {
   // p / (OH*OW) and p / OW as (p * magic) >> 40 (0: plain division), exact for p * d < 2^40
   uint64_t mg_hw, mg_ow;
   // fast block epilogue (conv blocks, 4-column vectors, requantize UPWARD): every record
-  // byte offset fits 32 bits, so stores go through buffer descriptors (out_bytes32 = 1)
+  // byte offset fits 32 bits, so stores go through buffer descriptors; 1 = nontemporal
+  // record stores, 2 = plain ones
   int32_t fast_epi;
   uint32_t out_elems;   // N * M: elements of each record
   int32_t nt;           // nontemporal record stores
+  // image-aligned N tiles (conv blocks with planes of <= 64 pixels): a tile holds ipt whole
+  // images (tcols = ipt * OH*OW of its 128 columns are used), so that for every image the
+  // tile's 64 channels x OH*OW pixels are one contiguous NCHW run: see the flat epilogue
+  int32_t ipt, tcols;
   int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
                        // 8/16/32/64 skip the conv / bias_add / requantize / clip record,
-                       // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs
+                       // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs, 1024 main-loop
+                       // barrier without the lgkmcnt(0) drain
 };
 
 // Writes one element of every output of a fused block.  Mirrors, per element:
@@ -264,6 +270,14 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // the 16-lane groups of ds_read_b128 then hit 16 distinct bank slots.
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * kBK + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
+// Same for the wide stages (rows of SBK = 64 or 128 bytes).  128-byte rows: chunk c of row r
+// at chunk c ^ ((r >> 1) & 7) (two rows per 256-byte bank period, 8 row pairs per 16 lanes).
+template <int SBK>
+__device__ __forceinline__ int lds_off_w(int row, int chunk) {
+  if constexpr (SBK == 64) return lds_off(row, chunk);
+  else return row * SBK + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
 // XCD-aware tile order: workgroup L runs on XCD L % 8, so XCD x takes the N tiles x, x+8,
 // x+16, ... and for each of them all M tiles back to back: the workgroups that share an
 // N tile (the same im2col B rows) run close together on one XCD and hit its L2.
@@ -357,7 +371,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
   tile_of(g, mtile, ntile);
   if (ntile >= g.ntiles) return;  // padding of the N-tile count to a multiple of 8
   const int m0 = mtile * BM;
-  const int n0 = ntile * BN;
+  const int n0 = ntile * g.tcols;
   // per-row epilogue constants (threads < BM, one row each), loaded up front: they land
   // during the main loop
   // (raw loads from a dummy word where an array is absent: the per-row/scalar choice is
@@ -376,6 +390,36 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
       row_pre.zp = raw(g.rq.zps, g.rq.zps != nullptr);
     }
   }
+  // residual bytes of every row this thread writes (4-column epilogue paths), issued before
+  // the main loop: they are older than every stage load, so the first stage wait also
+  // covers them and the epilogue never waits on HBM latency
+  uint32_t resid_pre[BM / 8];
+  if constexpr (kBlock && kMode != 1) {
+    if (g.has_add && g.ipt) {
+      // flat epilogue: 4 consecutive elements of an image run per group (see there)
+      const int hw = g.OH * g.OW;
+      const int run = min(BM, g.M - m0) * hw;
+#pragma unroll
+      for (int k = 0; k < BM / 8; ++k) {
+        const int gi = tid + kGemmThreads * k;
+        const int kk = gi / (16 * hw), f = (gi - kk * 16 * hw) * 4;
+        const int img = n0 / hw + kk;
+        const bool ok = kk < g.ipt && img < g.N / hw && f < run;
+        resid_pre[k] = ok ? ldg(reinterpret_cast<const uint32_t*>(g.add_res + ((int64_t)img * g.M + m0) * hw + f)) : 0u;
+      }
+    } else if (g.has_add && g.vecw >= 4) {
+      const int hw = g.OH * g.OW;
+      const int col = n0 + (tid & 31) * 4;
+      const int img = col / hw;
+      const int64_t cbase = (int64_t)img * g.M * hw + (col - img * hw);
+#pragma unroll
+      for (int k = 0; k < BM / 8; ++k) {
+        const int row = m0 + (tid >> 5) + 8 * k;
+        const bool ok = col < g.N && row < g.M;
+        resid_pre[k] = ldg(reinterpret_cast<const uint32_t*>(g.add_res + (ok ? cbase + (int64_t)row * hw : 0)));
+      }
+    }
+  }
   const int kc = tid & 3;  // this thread's 16-byte chunk within a K stage
 
   // ---- per-thread im2col state for the B rows it loads
@@ -385,7 +429,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
   for (int t = 0; t < B_CHUNKS; ++t) {
     int row = (tid >> 2) + t * (kGemmThreads / 4);
     int p = n0 + row;
-    b_valid[t] = p < g.N;
+    b_valid[t] = p < g.N && row < g.tcols;
     if (kIm2col) {
       const uint32_t pp = b_valid[t] ? p : 0;
       const int hw = g.OH * g.OW;
@@ -507,26 +551,42 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
     nk = min(nk, kt0 + g.kper);
   }
   // MFMAs of one staged K step (2 x K=32) from LDS
-  auto mma_stage = [&](const int8_t* a, const int8_t* b) {
+  // every fragment of the stage is read before the first MFMA: one LDS round trip per
+  // stage instead of one per K=32 half (small grids run 1-2 workgroups per CU, so the
+  // LDS latency is not hidden by other waves)
+  struct Frags {
+    v4i a[2][MT], b[2][2];
+  };
+  auto read_frags = [&](const int8_t* a, const int8_t* b, Frags& f) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = 2 * ks + (lane >> 5);
-      v4i af[MT], bf[2];
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         int row = wm * 32 * MT + i * 32 + (lane & 31);
-        af[i] = *reinterpret_cast<const v4i*>(a + lds_off(row, chunk));
+        f.a[ks][i] = *reinterpret_cast<const v4i*>(a + lds_off(row, chunk));
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         int row = wn * 64 + j * 32 + (lane & 31);
-        bf[j] = *reinterpret_cast<const v4i*>(b + lds_off(row, chunk));
+        f.b[ks][j] = *reinterpret_cast<const v4i*>(b + lds_off(row, chunk));
       }
+    }
+  };
+  auto mfma_frags = [&](const Frags& f) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f.a[ks][i], f.b[ks][j], acc[i][j], 0, 0, 0);
+  };
+  auto mma_stage = [&](const int8_t* a, const int8_t* b) {
+    Frags f;
+    read_frags(a, b, f);
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs (the scheduler interleaves them)
+    mfma_frags(f);
   };
 
   if constexpr (kMode != 2 && kIm2col) {
@@ -553,10 +613,16 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
         // retire stage it (A_CHUNKS + B_CHUNKS LDS-DMAs per thread and stage); the later
         // stages already issued stay in flight
         wait_vm(min(nst - 1 - it, kRing - 2) * (A_CHUNKS + B_CHUNKS));
-        lds_barrier();  // stage it visible to all waves; the slot read in step it-1 is free
-        if (it + kRing - 1 < nst) issue((it + kRing - 1) % kRing);
+        if (g.ablate & 1024) asm volatile("s_barrier" ::: "memory");
+        else lds_barrier();  // stage it visible to all waves; the slot read in step it-1 is free
+        // fragments of stage it first, so that their LDS latency overlaps the next issue
         const int8_t* a = smem + (it % kRing) * kStageBytes;
-        if (!(g.ablate & 512)) mma_stage(a, a + BM * kBK);
+        Frags f;
+        read_frags(a, a + BM * kBK, f);
+        __builtin_amdgcn_sched_barrier(0);
+        if (it + kRing - 1 < nst) issue((it + kRing - 1) % kRing);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(g.ablate & 512)) mfma_frags(f);
       }
     };
     auto issue_a = [&](int8_t* sa) {
@@ -705,22 +771,6 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
   EpiRow* rowc = reinterpret_cast<EpiRow*>(smem + BM * kEpiStride * 4);
   int32_t* lut = reinterpret_cast<int32_t*>(smem + BM * kEpiStride * 4 + BM * sizeof(EpiRow));  // [2][256]
   const int hw = g.OH * g.OW;
-  // residual bytes of every row this thread writes (4-column paths), issued before the tile
-  // dump so that their latency overlaps it
-  uint32_t resid_pre[BM / 8];
-  if constexpr (kBlock) {
-    if (g.has_add && g.vecw >= 4) {
-      const int col = n0 + (tid & 31) * 4;
-      const int img = col / hw;
-      const int64_t cbase = (int64_t)img * g.M * hw + (col - img * hw);
-#pragma unroll
-      for (int k = 0; k < BM / 8; ++k) {
-        const int row = m0 + (tid >> 5) + 8 * k;
-        const bool ok = col < g.N && row < g.M;
-        resid_pre[k] = ldg(reinterpret_cast<const uint32_t*>(g.add_res + (ok ? cbase + (int64_t)row * hw : 0)));
-      }
-    }
-  }
   const bool zb_vec = g.zB_vec != nullptr, has_rb = g.RB != nullptr;
   const bool simple_fold = !zb_vec && !has_rb;
   lds_barrier();  // staging buffers are free
@@ -758,7 +808,85 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
 
   bool done = false;
   if constexpr (kBlock) {
-    if (g.fast_epi && simple_fold && s_fast && !g.ablate) {
+    if (g.ipt && !(g.ablate & 0x7F)) {
+      // ---- flat epilogue (image-aligned tiles, planes of 4..64 pixels): for image kk of the
+      // tile, its channels m0.. and all OH*OW pixels are one contiguous run of the NCHW
+      // records, `run` elements long.  Group gi = 4 consecutive elements of one run: b128
+      // stores of the int32 records and b32 stores of the 8-bit ones, contiguous across lanes
+      // (whole 128-byte lines), each element gathered from its (row, column) slot of the tile.
+      done = true;
+      const int hw = g.OH * g.OW;
+      const int run = min(BM, g.M - m0) * hw;
+      const int img0 = n0 / hw, nimg = g.N / hw;
+      const uint32_t n4 = g.out_elems * 4u;
+      const auto r_conv = rec_rsrc(g.C, n4), r_bias = rec_rsrc(g.bias_out, n4);
+      const auto r_rq = rec_rsrc(g.rq_out, g.out_elems);
+      const auto r_add = rec_rsrc(g.add_out, g.has_add ? g.out_elems : 0u);
+      const auto r_clip = rec_rsrc(g.clip_out, g.has_clip ? g.out_elems : 0u);
+      const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
+      const int32_t add_zp = g.add_zp, clip_lo = g.clip_lo, clip_hi = g.clip_hi;
+      const bool has_add = g.has_add, has_clip = g.has_clip;
+      const int mode = g.rq.mode;
+      const int ipt = g.ipt, Mrows = g.M;  // (the lambda must not reference g: that forces it to scratch)
+      auto groups = [&](auto fast_c) __attribute__((always_inline)) {
+        constexpr bool FAST = decltype(fast_c)::value;
+#pragma unroll
+        for (int k = 0; k < BM / 8; ++k) {
+          const int gi = tid + kGemmThreads * k;
+          const int kk = gi / (16 * hw), f = (gi - kk * 16 * hw) * 4;
+          if (!(kk < ipt && img0 + kk < nimg && f < run)) continue;  // past a run or the tile's images
+          const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0) * hw + f);
+          const int r0 = f / hw, p0 = f - r0 * hw;
+          int slot[4];
+          EpiRow rr[4];
+          v4u v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool wrap = p0 + e >= hw;  // hw >= 4: at most one row change per group
+            const int re = r0 + (wrap ? 1 : 0), pe = p0 + e - (wrap ? hw : 0);
+            slot[e] = re * kEpiStride + kk * hw + pe;
+            rr[e] = rowc[re];
+            v[e] = (uint32_t)tileI[slot[e]];
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += rr[e].fold;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (uint32_t)rr[e].bias;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
+          int32_t q[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int32_t t = (int32_t)(v[e] - (uint32_t)rr[e].zp);
+            int32_t y;
+            if constexpr (FAST) {
+              const int sh2 = -rr[e].s - 1;
+              y = (int32_t)((uint32_t)__mulhi(t, rr[e].m) + (1u << (sh2 - 1))) >> sh2;
+            } else {
+              y = rq_core(t, mode, rr[e].m, rr[e].s);
+            }
+            q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
+          }
+          __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
+          if (has_add) {
+            // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((resid_pre[k] >> (8 * e)) & 0xFFu)] - add_zp, qmin, qmax);
+            __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
+          }
+          if (has_clip) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
+            __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) tileI[slot[e]] = q[e];
+        }
+      };
+      if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) groups(std::true_type{});
+      else groups(std::false_type{});
+    } else if (g.fast_epi && simple_fold && s_fast && !(g.ablate & 0x7F)) {
       // ---- fast path (tile-uniform): 4 consecutive columns x rows (tid>>5) + 8k, every
       // record through a buffer descriptor (masked lanes get an out-of-range offset),
       // requantize in the mul_hi form: ((x - zp)·m + 2^(sh2-1)) >> sh2 over the high word
@@ -774,13 +902,17 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
       const auto r_add = rec_rsrc(g.add_out, g.has_add ? g.out_elems : 0u);
       const auto r_clip = rec_rsrc(g.clip_out, g.has_clip ? g.out_elems : 0u);
       const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
+      // kernel arguments the row loop needs, held in registers: read through `g` after a
+      // store, the compiler reloads them (s_load + lgkmcnt(0), which also drains the LDS reads)
+      const int32_t add_zp = g.add_zp, clip_lo = g.clip_lo, clip_hi = g.clip_hi;
+      const bool want_shadow = g.shadow_out != nullptr;
       uint32_t offs[BM / 8];
 #pragma unroll
       for (int k = 0; k < BM / 8; ++k) {
         const int row = m0 + (tid >> 5) + 8 * k;
         offs[k] = (colok && row < g.M) ? cbase + (uint32_t)row * (uint32_t)hw : kOffDrop;
       }
-      auto rows = [&](auto add_c, auto clip_c, auto aux_c) {
+      auto rows = [&](auto add_c, auto clip_c, auto aux_c) __attribute__((always_inline)) {
         constexpr bool ADD = decltype(add_c)::value, CLIP = decltype(clip_c)::value;
         constexpr int AUX = decltype(aux_c)::value;
 #pragma unroll
@@ -807,20 +939,22 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
             // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((resid_pre[k] >> (8 * e)) & 0xFFu)] - g.add_zp, qmin, qmax);
+              q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((resid_pre[k] >> (8 * e)) & 0xFFu)] - add_zp, qmin, qmax);
             __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, AUX);
           }
           if constexpr (CLIP) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], g.clip_lo, g.clip_hi);
+            for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
             __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, AUX);
           }
-          if (g.shadow_out) *reinterpret_cast<v4i*>(slot) = v4i{q[0], q[1], q[2], q[3]};
+          if (want_shadow) *reinterpret_cast<v4i*>(slot) = v4i{q[0], q[1], q[2], q[3]};
         }
       };
       using T = std::true_type;
       using F = std::false_type;
-      auto dispatch = [&](auto aux_c) {
+      // always_inline: the epilogue lambdas must not become calls, which would take the address
+      // of g and copy every kernel argument to scratch (a 4x slowdown measured)
+      auto dispatch = [&](auto aux_c) __attribute__((always_inline)) {
         if (g.has_add) {
           if (g.has_clip) rows(T{}, T{}, aux_c);
           else rows(T{}, F{}, aux_c);
@@ -919,7 +1053,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
       const int grp = it / BN;
       const int col = n0 + lc;
       const int ch0 = m0 + grp * 16;
-      if (col < g.N && ch0 < g.shadow_cpad) {
+      if (col < g.N && lc < g.tcols && ch0 < g.shadow_cpad) {
         uint32_t w[4];
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -1292,9 +1426,27 @@ struct SplitPlan {
   int splits, kper;
   int64_t tiles;
 };
-static SplitPlan conv_split_plan(const ConvGeom& g, bool mt1) {
-  const int64_t P = (int64_t)g.N * g.OH * g.OW;
-  const int64_t tiles = ((P + 127) / 128) * ((g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128));
+static bool conv_needs_patch(const tk_tensor* weight, const tk_conv2d_attrs* a) {
+  return (a->kernel_zero_point - (is_uint(weight, 8) ? 128 : 0)) != 0 || a->kernel_zero_points;
+}
+
+// Images per N tile of a conv block whose planes hold 4..64 pixels (0: plain 128-column
+// tiles).  Needs the flat epilogue's preconditions: no per-pixel zero-point patch, a channel
+// count that keeps every image run 16-byte aligned, and 32-bit record offsets.
+static int conv_image_tiles(const ConvGeom& g, bool block, bool patch) {
+  const int64_t hw = (int64_t)g.OH * g.OW;
+  if (!block || patch || hw < 4 || hw > 64 || g.O % 4 != 0 || (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll ||
+      !env_int("TK_IMGTILE", 1))
+    return 0;
+  return (int)(128 / hw);
+}
+
+static int64_t conv_ntiles(const ConvGeom& g, int ipt) {
+  return ipt ? ((int64_t)g.N + ipt - 1) / ipt : ((int64_t)g.N * g.OH * g.OW + 127) / 128;
+}
+
+static SplitPlan conv_split_plan(const ConvGeom& g, bool mt1, int ipt) {
+  const int64_t tiles = conv_ntiles(g, ipt) * ((g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128));
   const int nk = (int)(g.k_pad / kBK);
   SplitPlan sp{1, nk, tiles};
   // measured: splitting grids of >= 256 tiles (one per CU) loses more to the partial-tile
@@ -1307,9 +1459,6 @@ static SplitPlan conv_split_plan(const ConvGeom& g, bool mt1) {
   return sp;
 }
 
-static bool conv_needs_patch(const tk_tensor* weight, const tk_conv2d_attrs* a) {
-  return (a->kernel_zero_point - (is_uint(weight, 8) ? 128 : 0)) != 0 || a->kernel_zero_points;
-}
 
 static inline int64_t al256(int64_t v) { return (v + 255) / 256 * 256; }
 
@@ -1320,7 +1469,7 @@ int64_t conv_scratch_bytes(const tk_tensor* data, const tk_tensor* weight, const
   if (!use_mfma_conv(g, a->groups)) return 0;
   int64_t bytes = 0;
   if (conv_needs_patch(weight, a)) bytes += al256((int64_t)g.N * g.OH * g.OW * 4);
-  const SplitPlan sp = conv_split_plan(g, g.O <= 64 || block);
+  const SplitPlan sp = conv_split_plan(g, g.O <= 64 || block, conv_image_tiles(g, block, conv_needs_patch(weight, a)));
   if (sp.splits > 1) bytes += al256(sp.tiles * sp.splits * (int64_t)(2 * 16 * kGemmThreads) * 4);
   return bytes;
 }
@@ -1411,8 +1560,13 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     const uint64_t elems = (uint64_t)P * g.O;
     ga.out_elems = (uint32_t)std::min<uint64_t>(elems, 0xFFFFFFFFull);
     const int mode = blk ? blk->attrs->requantize.mode : -1;
-    ga.fast_epi = blk && elems * 4 < 0xFFFFFFC0ull && (g.OH * g.OW) % 4 == 0 &&
-                  (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD) ? env_int("TK_FASTEPI", 1) : 0;
+    // record stores are nontemporal (1) only where a plane's int32 rows are whole 128-byte
+    // lines (or planes are tiny): measured on ResNet-50, partial-line NT stores (28x28, 14x14
+    // planes) run up to 1.9x slower than plain ones, which the L2 merges before write-back
+    const int hwp = g.OH * g.OW;
+    const int epi = hwp % 32 == 0 || hwp <= 64 ? 1 : 2;
+    ga.fast_epi = blk && elems * 4 < 0xFFFFFFC0ull && hwp % 4 == 0 &&
+                  (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD) ? env_int("TK_FASTEPI", epi) : 0;
   }
   ga.out_nchw = 1;
   {
@@ -1431,11 +1585,14 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     ga.zA_vec = a->kernel_zero_points;
   }
   const bool mt1 = g.O <= 64 || (blk && !getenv("TK_MT2"));
-  ga.ntiles = (int32_t)((P + 127) / 128);
+  const int ipt = mt1 ? conv_image_tiles(g, blk != nullptr, conv_needs_patch(weight, a)) : 0;
+  ga.ipt = ipt;
+  ga.tcols = ipt ? ipt * g.OH * g.OW : 128;
+  ga.ntiles = (int32_t)conv_ntiles(g, ipt);
   ga.ntiles8 = (ga.ntiles + 7) / 8 * 8;
   ga.mtiles = (g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128);
   dim3 grid((unsigned)((int64_t)ga.mtiles * ga.ntiles8));
-  const SplitPlan sp = conv_split_plan(g, mt1);
+  const SplitPlan sp = conv_split_plan(g, mt1, ipt);
   const int ring = ring_depth();
   if (sp.splits > 1) {
     TK_CHECK_ARG(sc, "split-K conv needs scratch (tk_conv2d_scratch_bytes)");
@@ -1453,10 +1610,11 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     else hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 2>), grid, dim3(kGemmThreads), 0, s, ga);
   } else if (mt1) {
     if (blk) {
+      const unsigned pad = (unsigned)env_int("TK_LDS_PAD", 0);  // profiling: extra LDS per workgroup
       switch (ring) {
-        case 4: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 4>), grid, dim3(kGemmThreads), 0, s, ga); break;
-        case 5: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 5>), grid, dim3(kGemmThreads), 0, s, ga); break;
-        default: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true>), grid, dim3(kGemmThreads), 0, s, ga);
+        case 4: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 4>), grid, dim3(kGemmThreads), pad, s, ga); break;
+        case 5: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 5>), grid, dim3(kGemmThreads), pad, s, ga); break;
+        default: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true>), grid, dim3(kGemmThreads), pad, s, ga);
       }
     } else {
       hipLaunchKernelGGL((gemm_i8_kernel<1, true, false>), grid, dim3(kGemmThreads), 0, s, ga);
@@ -1601,6 +1759,7 @@ static int dense_run(const tk_tensor* data, const tk_tensor* weight, tk_tensor* 
   int rc = setup_block(ga, blk, out, Nn, 1);
   if (rc) return rc;
   ga.shadow_out = nullptr;
+  ga.tcols = 128;
   ga.ntiles = (int32_t)((Nn + 127) / 128);
   ga.ntiles8 = (ga.ntiles + 7) / 8 * 8;
   ga.mtiles = (M + 127) / 128;

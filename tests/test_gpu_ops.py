@@ -244,6 +244,8 @@ BLOCK_CASES = [
     (1, 1, 12, 12, 6, 5, 1, 2, 1, "int8", 0, "int8", (-1, 127)),      # tiny Cin (direct kernel)
     (2, 128, 7, 7, 256, 3, 1, 1, 1, "int8", -2, "int8", (0, 127)),    # split-K block, scalar-store epilogue
     (4, 256, 14, 14, 96, 1, 2, 0, 1, "int8", 5, "uint8", None),       # split-K strided 1x1, 7x7 out
+    (40, 32, 4, 4, 64, 3, 2, 1, 1, "int8", 1, "int8", (0, 127)),      # 2x2 planes: 32 images per tile
+    (7, 16, 5, 5, 36, 3, 1, 1, 1, "uint8", 128, "uint8", None),       # 5x5 planes, last tile partial
 ]
 
 

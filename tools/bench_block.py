@@ -18,12 +18,14 @@ SHAPES = [  # name, C, H, O, K, stride, pad
     ("3x3 128->128 28", 128, 28, 128, 3, 1, 1),
     ("3x3 256->256 14", 256, 14, 256, 3, 1, 1),
     ("1x1 1024->256 14", 1024, 14, 256, 1, 1, 0),
+    ("1x1 256->1024 14", 256, 14, 1024, 1, 1, 0),
     ("3x3 512->512 7", 512, 7, 512, 3, 1, 1),
     ("1x1 512->2048 7", 512, 7, 2048, 1, 1, 0),
+    ("1x1 2048->512 7", 2048, 7, 512, 1, 1, 0),
 ]
 
 
-def main(batch=64, iters=20, configs=None, reps=3):
+def main(batch=64, iters=20, configs=None, reps=3, only=None):
     """configs: list of env-var dicts (TK_ABLATE / TK_NT are read per launch); each layer is
     timed for every config, interleaved `reps` times, and the minimum is reported."""
     import os
@@ -33,6 +35,8 @@ def main(batch=64, iters=20, configs=None, reps=3):
     rng = np.random.default_rng(0)
     tot = [0.0] * len(configs)
     for name, C, H, O, K, S, P in SHAPES:
+        if only and not any(o in name for o in only.split(",")):
+            continue
         OH = (H + 2 * P - K) // S + 1
         x = torch.from_numpy(rng.integers(-128, 128, size=(batch, C, H, H)).astype(np.int8)).to(dev)
         w = torch.from_numpy(rng.integers(-128, 128, size=(O, C, K, K)).astype(np.int8)).to(dev)
@@ -101,4 +105,4 @@ def main(batch=64, iters=20, configs=None, reps=3):
 if __name__ == "__main__":
     import json
     cfgs = json.loads(sys.argv[1]) if len(sys.argv) > 1 else None
-    main(configs=cfgs)
+    main(configs=cfgs, only=sys.argv[2] if len(sys.argv) > 2 else None)
