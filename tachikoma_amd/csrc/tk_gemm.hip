@@ -270,13 +270,14 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // the 16-lane groups of ds_read_b128 then hit 16 distinct bank slots.
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * kBK + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-// Same for the wide stages (rows of SBK = 64 or 128 bytes).  128-byte rows: chunk c of row r
-// at chunk c ^ ((r >> 1) & 7) (two rows per 256-byte bank period, 8 row pairs per 16 lanes).
+// Same for stages of SBK = 64 or 128 bytes per row.  128-byte rows: chunk c of row r at
+// chunk c ^ ((r >> 1) & 7) (two rows per 256-byte bank period, 8 row pairs per 16 lanes).
 template <int SBK>
 __device__ __forceinline__ int lds_off_w(int row, int chunk) {
   if constexpr (SBK == 64) return lds_off(row, chunk);
   else return row * SBK + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
+
 
 // XCD-aware tile order: workgroup L runs on XCD L % 8, so XCD x takes the N tiles x, x+8,
 // x+16, ... and for each of them all M tiles back to back: the workgroups that share an
@@ -346,14 +347,22 @@ __device__ __forceinline__ void wait_vm(int n) {
   }
 }
 
-template <int MT, bool kIm2col, bool kBlock, int kMode = 0, int kRing = 3>
-__global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 4 ? 3 : 2) : 2) void gemm_i8_kernel(
-    GemmArgs g) {
+// kWide (im2col LDS-DMA path): 128-byte K stages instead of 64, i.e. half the
+// barrier-separated steps of long reductions (each step pays a fixed LDS / barrier / address
+// latency that the 1-2 workgroups per CU of the small-grid layers cannot hide).
+template <int MT, bool kIm2col, bool kBlock, int kMode = 0, int kRing = 3, bool kWide = false>
+__global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kWide ? 2 : kRing == 3 ? 4 : kRing == 4 ? 3 : 2) : 2) void
+gemm_i8_kernel(GemmArgs g) {
+  static_assert(!kWide || (kIm2col && MT == 1 && kRing == 3), "wide stages: im2col, MT = 1, ring 3");
   constexpr int BM = 64 * MT;   // rows of A per block (2 waves along M, MT 32-row tiles each)
   constexpr int BN = 128;       // rows of B per block (2 waves along N, 2 32-col tiles each)
-  constexpr int A_CHUNKS = BM * kBK / 16 / kGemmThreads;  // 16-byte loads per thread per stage
+  constexpr int A_CHUNKS = BM * kBK / 16 / kGemmThreads;  // 16-byte loads per thread per stage (plain path)
   constexpr int B_CHUNKS = BN * kBK / 16 / kGemmThreads;
-  constexpr int kStageBytes = (BM + BN) * kBK;
+  constexpr int SBK = kWide ? 2 * kBK : kBK;              // K bytes per stage
+  constexpr int CPR = SBK / 16;                           // 16-byte chunks per stage row
+  constexpr int RPP = kGemmThreads / CPR;                 // stage rows per pass of all threads
+  constexpr int A_DMA = BM / RPP, B_DMA = BN / RPP;       // LDS-DMA loads per thread per stage
+  constexpr int kStageBytes = (BM + BN) * SBK;
   // kRing: LDS-DMA stages of the im2col path (kRing - 1 in flight); the plain path double-buffers
   constexpr int kStage = (kIm2col ? kRing : 2) * kStageBytes;
   constexpr int kEpi = BM * kEpiStride * 4 + BM * (int)sizeof(EpiRow) + (kBlock ? 512 * 4 : 0);
@@ -423,11 +432,11 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
   const int kc = tid & 3;  // this thread's 16-byte chunk within a K stage
 
   // ---- per-thread im2col state for the B rows it loads
-  int b_img[B_CHUNKS], b_ih0[B_CHUNKS], b_iw0[B_CHUNKS];
-  bool b_valid[B_CHUNKS];
+  int b_img[B_DMA], b_ih0[B_DMA], b_iw0[B_DMA];
+  bool b_valid[B_DMA];
 #pragma unroll
-  for (int t = 0; t < B_CHUNKS; ++t) {
-    int row = (tid >> 2) + t * (kGemmThreads / 4);
+  for (int t = 0; t < B_DMA; ++t) {
+    int row = tid / CPR + t * RPP;
     int p = n0 + row;
     b_valid[t] = p < g.N && row < g.tcols;
     if (kIm2col) {
@@ -451,35 +460,10 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
       int row = (tid >> 2) + t * (kGemmThreads / 4);
       ra[t] = *reinterpret_cast<const v4i*>(g.A + (int64_t)(m0 + row) * g.lda + k0 + kc * 16);
     }
-    if (!kIm2col) {
 #pragma unroll
-      for (int t = 0; t < B_CHUNKS; ++t) {
-        int row = (tid >> 2) + t * (kGemmThreads / 4);
-        rb[t] = *reinterpret_cast<const v4i*>(g.B + (int64_t)(n0 + row) * g.ldb + k0 + kc * 16);
-      }
-    } else {
-      int kg = k0 + kc * 16;
-      int tap = kg / g.cin_pad;
-      int c0 = kg - tap * g.cin_pad;
-      int kh = tap / g.KW;
-      int kw = tap - kh * g.KW;
-      bool tap_ok = tap < g.taps;
-      const uint32_t fill = g.fill;
-#pragma unroll
-      for (int t = 0; t < B_CHUNKS; ++t) {
-        int ih = b_ih0[t] + kh * g.dh;
-        int iw = b_iw0[t] + kw * g.dw;
-        if (b_valid[t] && tap_ok) {
-          if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
-            const int8_t* src = g.B + ((int64_t)(c0 >> 4) * g.in_pix + ((int64_t)b_img[t] * g.H + ih) * g.W + iw) * 16;
-            rb[t] = *reinterpret_cast<const v4i*>(src);
-          } else {
-            rb[t] = v4i{(int)fill, (int)fill, (int)fill, (int)fill};
-          }
-        } else {
-          rb[t] = v4i{0, 0, 0, 0};
-        }
-      }
+    for (int t = 0; t < B_CHUNKS; ++t) {
+      int row = (tid >> 2) + t * (kGemmThreads / 4);
+      rb[t] = *reinterpret_cast<const v4i*>(g.B + (int64_t)(n0 + row) * g.ldb + k0 + kc * 16);
     }
   };
 
@@ -545,7 +529,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
       add_tile(t);
     }
   }
-  int kt0 = 0, nk = g.k_pad / kBK;
+  int kt0 = 0, nk = g.k_pad / SBK;
   if constexpr (kMode == 1) {
     kt0 = blockIdx.z * g.kper;
     nk = min(nk, kt0 + g.kper);
@@ -554,28 +538,29 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
   // every fragment of the stage is read before the first MFMA: one LDS round trip per
   // stage instead of one per K=32 half (small grids run 1-2 workgroups per CU, so the
   // LDS latency is not hidden by other waves)
+  constexpr int KS = SBK / 32;  // K = 32 MFMA steps per stage
   struct Frags {
-    v4i a[2][MT], b[2][2];
+    v4i a[KS][MT], b[KS][2];
   };
   auto read_frags = [&](const int8_t* a, const int8_t* b, Frags& f) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       const int chunk = 2 * ks + (lane >> 5);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         int row = wm * 32 * MT + i * 32 + (lane & 31);
-        f.a[ks][i] = *reinterpret_cast<const v4i*>(a + lds_off(row, chunk));
+        f.a[ks][i] = *reinterpret_cast<const v4i*>(a + lds_off_w<SBK>(row, chunk));
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         int row = wn * 64 + j * 32 + (lane & 31);
-        f.b[ks][j] = *reinterpret_cast<const v4i*>(b + lds_off(row, chunk));
+        f.b[ks][j] = *reinterpret_cast<const v4i*>(b + lds_off_w<SBK>(row, chunk));
       }
     }
   };
   auto mfma_frags = [&](const Frags& f) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -597,13 +582,14 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
     // holds chunk s ^ ((r >> 2) & 3), i.e. lane l loads chunk (l & 3) ^ ((l >> 4) & 3).
     // Out-of-bounds taps read a row of the input zero point; rows past N and K padding
     // (whose weights are 0) read it too.
-    const int cl = (lane & 3) ^ ((lane >> 4) & 3);
+    // (wide: 8 rows of 128 B per wave-instruction, slot s of row r holds chunk s ^ ((r >> 1) & 7))
+    const int cl = kWide ? ((lane & 7) ^ ((4 * wave + (lane >> 4)) & 7)) : ((lane & 3) ^ ((lane >> 4) & 3));
     const int8_t* fill_src = reinterpret_cast<const int8_t*>(tk_fill_rows.v + 16 * (g.fill & 0xFFu));
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-    const int8_t* a_src[A_CHUNKS];
+    const int8_t* a_src[A_DMA];
 #pragma unroll
-    for (int t = 0; t < A_CHUNKS; ++t)
-      a_src[t] = g.A + (int64_t)(m0 + (tid >> 2) + t * (kGemmThreads / 4)) * g.lda + kt0 * kBK + cl * 16;
+    for (int t = 0; t < A_DMA; ++t)
+      a_src[t] = g.A + (int64_t)(m0 + tid / CPR + t * RPP) * g.lda + kt0 * SBK + cl * 16;
     const int nst = nk - kt0;
     auto pipeline = [&](auto&& issue) {
 #pragma unroll
@@ -612,13 +598,13 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
       for (int it = 0; it < nst; ++it) {
         // retire stage it (A_CHUNKS + B_CHUNKS LDS-DMAs per thread and stage); the later
         // stages already issued stay in flight
-        wait_vm(min(nst - 1 - it, kRing - 2) * (A_CHUNKS + B_CHUNKS));
+        wait_vm(min(nst - 1 - it, kRing - 2) * (A_DMA + B_DMA));
         if (g.ablate & 1024) asm volatile("s_barrier" ::: "memory");
         else lds_barrier();  // stage it visible to all waves; the slot read in step it-1 is free
         // fragments of stage it first, so that their LDS latency overlaps the next issue
         const int8_t* a = smem + (it % kRing) * kStageBytes;
         Frags f;
-        read_frags(a, a + BM * kBK, f);
+        read_frags(a, a + BM * SBK, f);
         __builtin_amdgcn_sched_barrier(0);
         if (it + kRing - 1 < nst) issue((it + kRing - 1) % kRing);
         __builtin_amdgcn_sched_barrier(0);
@@ -627,19 +613,20 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
     };
     auto issue_a = [&](int8_t* sa) {
 #pragma unroll
-      for (int t = 0; t < A_CHUNKS; ++t) {
+      for (int t = 0; t < A_DMA; ++t) {
         if (!(g.ablate & 128))
-          __builtin_amdgcn_global_load_lds((const void*)a_src[t], (void*)(sa + (16 * wave_u + 64 * t) * kBK), 16, 0, 0);
-        a_src[t] += kBK;
+          __builtin_amdgcn_global_load_lds((const void*)a_src[t], (void*)(sa + ((RPP / 4) * wave_u + RPP * t) * SBK),
+                                           16, 0, 0);
+        a_src[t] += SBK;
       }
     };
-    if (g.unitap) {
+    if (kWide || g.unitap) {
       // lane-constant part of the source (pixel + the lane's channel group) and the taps
       // that are in bounds for the lane's rows; the stage part (channel group, tap) is uniform
-      const int8_t* lane_base[B_CHUNKS];
-      uint64_t tmask[B_CHUNKS];
+      const int8_t* lane_base[B_DMA];
+      uint64_t tmask[B_DMA];
 #pragma unroll
-      for (int t = 0; t < B_CHUNKS; ++t) {
+      for (int t = 0; t < B_DMA; ++t) {
         const int64_t pix = ((int64_t)b_img[t] * g.H + b_ih0[t]) * g.W + b_iw0[t];
         lane_base[t] = g.B + (pix + (int64_t)cl * g.in_pix) * 16;
         uint32_t rows = 0, cols = 0;
@@ -658,7 +645,7 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
       }
       int cg, kh, kw;  // uniform: channel group of the stage's first chunk, tap
       {
-        const int k0 = kt0 * kBK;
+        const int k0 = kt0 * SBK;
         const int tap = k0 / g.cin_pad;
         cg = (k0 - tap * g.cin_pad) >> 4;
         kh = tap / g.KW;
@@ -669,24 +656,25 @@ __global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kRing == 3 ? 4 : kRing == 
       pipeline([&](int slot) {
         int8_t* sa = smem + slot * kStageBytes;
         issue_a(sa);
-        int8_t* sb = sa + BM * kBK;
+        int8_t* sb = sa + BM * SBK;
         const int tap = kh * g.KW + kw;
         const int64_t soff = cg * grp_bytes + kh * row_bytes + (int64_t)(kw * g.dw) * 16;
         const bool grp_ok = cg + cl < g.cgroups;  // K padding of a 1x1 conv with cin_pad % 64 != 0
 #pragma unroll
-        for (int t = 0; t < B_CHUNKS; ++t) {
+        for (int t = 0; t < B_DMA; ++t) {
           const bool ok = ((tmask[t] >> tap) & 1) && grp_ok;
           const int8_t* src = ok ? lane_base[t] + soff : fill_src;
           if (!(g.ablate & 256))
-            __builtin_amdgcn_global_load_lds((const void*)src, (void*)(sb + (16 * wave_u + 64 * t) * kBK), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)src, (void*)(sb + ((RPP / 4) * wave_u + RPP * t) * SBK),
+                                             16, 0, 0);
         }
-        cg += 4;
+        cg += CPR;
         if (cg >= g.cgroups) {
           cg = 0;
           if (++kw == g.KW) kw = 0, ++kh;
         }
       });
-    } else {
+    } else if constexpr (!kWide) {
       // general walk: the thread's chunk is (tap, channel offset c0) with the taps in
       // (kh, kw) order; advanced 64 bytes per stage without divisions
       int c0, kh, kw;
@@ -1445,9 +1433,20 @@ static int64_t conv_ntiles(const ConvGeom& g, int ipt) {
   return ipt ? ((int64_t)g.N + ipt - 1) / ipt : ((int64_t)g.N * g.OH * g.OW + 127) / 128;
 }
 
-static SplitPlan conv_split_plan(const ConvGeom& g, bool mt1, int ipt) {
+// Wide (128-byte) K stages for conv blocks with long reductions on small grids: >= 8 steps of
+// 64 bytes, every stage within one tap (cin_pad % 128 == 0), and few enough tiles that the
+// 2 workgroups per CU the wide ring's LDS allows hold the whole grid (TK_WIDE_MAX_TILES).
+static bool conv_wide(const ConvGeom& g, bool block, int ipt) {
+  if (!block || g.KH * g.KW > 64 || g.cin_pad % 128 != 0 || g.k_pad / kBK < 8 || ring_depth() != 3 ||
+      !env_int("TK_WIDE", 1) || !env_int("TK_UNITAP", 1) || getenv("TK_MT2"))
+    return false;
+  const int64_t tiles = conv_ntiles(g, ipt) * ((g.O + 63) / 64);
+  return tiles <= env_int("TK_WIDE_MAX_TILES", 512);
+}
+
+static SplitPlan conv_split_plan(const ConvGeom& g, bool mt1, int ipt, int sbk = kBK) {
   const int64_t tiles = conv_ntiles(g, ipt) * ((g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128));
-  const int nk = (int)(g.k_pad / kBK);
+  const int nk = (int)(g.k_pad / sbk);
   SplitPlan sp{1, nk, tiles};
   // measured: splitting grids of >= 256 tiles (one per CU) loses more to the partial-tile
   // round trip than it gains in latency hiding
@@ -1469,7 +1468,9 @@ int64_t conv_scratch_bytes(const tk_tensor* data, const tk_tensor* weight, const
   if (!use_mfma_conv(g, a->groups)) return 0;
   int64_t bytes = 0;
   if (conv_needs_patch(weight, a)) bytes += al256((int64_t)g.N * g.OH * g.OW * 4);
-  const SplitPlan sp = conv_split_plan(g, g.O <= 64 || block, conv_image_tiles(g, block, conv_needs_patch(weight, a)));
+  const int ipt = conv_image_tiles(g, block, conv_needs_patch(weight, a));
+  const bool wide = (g.O <= 64 || block) && conv_wide(g, block, ipt);
+  const SplitPlan sp = conv_split_plan(g, g.O <= 64 || block, ipt, wide ? 2 * kBK : kBK);
   if (sp.splits > 1) bytes += al256(sp.tiles * sp.splits * (int64_t)(2 * 16 * kGemmThreads) * 4);
   return bytes;
 }
@@ -1592,7 +1593,8 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   ga.ntiles8 = (ga.ntiles + 7) / 8 * 8;
   ga.mtiles = (g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128);
   dim3 grid((unsigned)((int64_t)ga.mtiles * ga.ntiles8));
-  const SplitPlan sp = conv_split_plan(g, mt1, ipt);
+  const bool wide = mt1 && conv_wide(g, blk != nullptr, ipt);
+  const SplitPlan sp = conv_split_plan(g, mt1, ipt, wide ? 2 * kBK : kBK);
   const int ring = ring_depth();
   if (sp.splits > 1) {
     TK_CHECK_ARG(sc, "split-K conv needs scratch (tk_conv2d_scratch_bytes)");
@@ -1600,7 +1602,8 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     ga.splits = sp.splits;
     ga.kper = sp.kper;
     dim3 pgrid(grid.x, 1, (unsigned)sp.splits);
-    switch (ring) {
+    if (wide) hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1, 3, true>), pgrid, dim3(kGemmThreads), 0, s, ga);
+    else switch (ring) {
       case 4: hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1, 4>), pgrid, dim3(kGemmThreads), 0, s, ga); break;
       case 5: hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1, 5>), pgrid, dim3(kGemmThreads), 0, s, ga); break;
       default: hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 1>), pgrid, dim3(kGemmThreads), 0, s, ga);
@@ -1611,7 +1614,8 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   } else if (mt1) {
     if (blk) {
       const unsigned pad = (unsigned)env_int("TK_LDS_PAD", 0);  // profiling: extra LDS per workgroup
-      switch (ring) {
+      if (wide) hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 3, true>), grid, dim3(kGemmThreads), pad, s, ga);
+      else switch (ring) {
         case 4: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 4>), grid, dim3(kGemmThreads), pad, s, ga); break;
         case 5: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 5>), grid, dim3(kGemmThreads), pad, s, ga); break;
         default: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true>), grid, dim3(kGemmThreads), pad, s, ga);

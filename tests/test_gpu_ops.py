@@ -246,6 +246,9 @@ BLOCK_CASES = [
     (4, 256, 14, 14, 96, 1, 2, 0, 1, "int8", 5, "uint8", None),       # split-K strided 1x1, 7x7 out
     (40, 32, 4, 4, 64, 3, 2, 1, 1, "int8", 1, "int8", (0, 127)),      # 2x2 planes: 32 images per tile
     (7, 16, 5, 5, 36, 3, 1, 1, 1, "uint8", 128, "uint8", None),       # 5x5 planes, last tile partial
+    (2, 512, 7, 7, 64, 3, 1, 1, 1, "int8", -3, "int8", (0, 127)),     # 128-byte K stages + split-K
+    (2, 256, 14, 14, 128, 3, 1, 1, 1, "int8", 2, "int8", None),       # 128-byte K stages, 128-column tiles
+    (2, 128, 9, 9, 64, 3, 1, 1, 1, "uint8", 130, "uint8", (128, 255)),  # 128-byte K stages, uint8
 ]
 
 
