@@ -250,6 +250,30 @@ int tk_global_avg_pool2d(const tk_tensor* data, tk_tensor* out, void* stream);
 /* batch_flatten / reshape: byte copy (kept as a node so it is traced). */
 int tk_copy(const tk_tensor* data, tk_tensor* out, void* stream);
 
+/* tachikoma BYOC composite post-ops: the float32 tail of a tachikoma.qnn.conv2d /
+ * tachikoma.qnn.dense composite after LegalizeQnnOpForTachikoma
+ * (python/tvm/relay/op/contrib/tachikoma.py:1122-1306), executed by the reference's JSON
+ * runtime as oneDNN post-ops (src/runtime/contrib/tachikoma/tachikoma_json_runtime.cc:142-185).
+ * On the int32 contraction `acc` (zero zero points), per element of channel c along `axis`,
+ * in float32, each operation rounded separately and in this order:
+ *   t = (float(acc) + bias[c]) * o_scl[n_scales == 1 ? 0 : c]      output scales
+ *   t = min(max(t, clip_lo), clip_hi) * act_scl                       eltwise clip, scaled
+ *   t = sum_scl * float(sum_src) + t          (only when sum_src)     sum post-op
+ *   t = t + dst_zp                                                    linear eltwise
+ *   out = saturate(round_half_even(t))                                8-bit destination
+ * bias and o_scl are float32 device arrays.  Replaces the composite's Run
+ * (tachikoma_json_runtime.cc:93-106) for the post-op part; the contraction is tk_qnn_conv2d /
+ * tk_qnn_dense with zero zero points. */
+typedef struct {
+  int32_t axis;
+  int32_t n_scales;             /* 1: per-tensor output scale, else one per channel */
+  float clip_lo, clip_hi, act_scl, sum_scl, dst_zp;
+  const float* bias;            /* [channels] */
+  const float* o_scl;           /* [n_scales] */
+} tk_postops_attrs;
+int tk_tachikoma_postops(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* out,
+                         const tk_postops_attrs* attrs, void* stream);
+
 /* ---------------------------------------------------------------- executor
  * Native run loop replacing GraphExecutor::Run (graph_executor.cc:61-66) and
  * the debug executor's per-node copy-out (graph_executor_debug.cc:249-284).
@@ -272,6 +296,7 @@ enum {
   TK_NODE_CONV_BLOCK = 13, /* in: data, weight, bias, [residual]; outs: 3-5; ext: shadow, packed, weight_sums, scratch, shadow_out */
   TK_NODE_DENSE_BLOCK = 14,/* in: data, weight, bias; outs: 3-4; ext: workspace */
   TK_NODE_ADD_BLOCK = 15,  /* in: lhs, rhs; outs: 1-2 (add, clip); ext[4]: shadow_out */
+  TK_NODE_POSTOPS = 16,    /* tachikoma composite post-ops: in: acc int32, [sum_src]; out: dst */
 };
 
 #define TK_MAX_NODE_INPUTS 4
@@ -292,6 +317,7 @@ typedef struct {
     tk_pool2d_attrs pool2d;
     tk_block_attrs block;
     tk_add_block_attrs add_block;
+    tk_postops_attrs postops;
     struct { int64_t a_min, a_max; } clip;
     struct { int32_t axis; } bias_add;
   } attrs;

@@ -123,6 +123,18 @@ def eval_call(call, args, backend: str = "numpy", threads: int = 1):
         return ref.qnn_add(args[0], args[1], *c)
     if op == "nn.bias_add":
         return ref.bias_add(args[0], args[1], axis=a["axis"])
+    if op == "add":  # relay.add of a per-channel vector (broadcast_add, int32 wrap-around)
+        return ref.wrap_i32(args[0].astype(np.int64) + args[1].astype(np.int64)).astype(np.int32)
+    if op in ("tachikoma.qnn.conv2d", "tachikoma.qnn.dense"):
+        from . import tachikoma_ref
+        if op == "tachikoma.qnn.conv2d":
+            acc = ref.qnn_conv2d(args[0], args[1], 0, 0, strides=a["strides"], padding=a["padding"],
+                                 dilation=a["dilation"], groups=a["groups"])
+        else:
+            acc = ref.qnn_dense(args[0], args[1], 0, 0)
+        po = a["postops"]
+        return tachikoma_ref.postops(acc, po, call.dtype, sum_src=args[2] if len(args) > 2 else None,
+                                     channel_axis=1, clip=po["clip"])
     if op == "clip":
         return ref.clip(args[0], a["a_min"], a["a_max"])
     if op == "nn.relu":

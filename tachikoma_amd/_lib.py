@@ -109,6 +109,20 @@ class tk_add_block_attrs(ctypes.Structure):
     ]
 
 
+class tk_postops_attrs(ctypes.Structure):
+    _fields_ = [
+        ("axis", ctypes.c_int32),
+        ("n_scales", ctypes.c_int32),
+        ("clip_lo", ctypes.c_float),
+        ("clip_hi", ctypes.c_float),
+        ("act_scl", ctypes.c_float),
+        ("sum_scl", ctypes.c_float),
+        ("dst_zp", ctypes.c_float),
+        ("bias", ctypes.c_void_p),
+        ("o_scl", ctypes.c_void_p),
+    ]
+
+
 class tk_pool2d_attrs(ctypes.Structure):
     _fields_ = [
         ("pool_size", ctypes.c_int32 * 2),
@@ -136,6 +150,7 @@ class tk_node_attrs(ctypes.Union):
         ("pool2d", tk_pool2d_attrs),
         ("block", tk_block_attrs),
         ("add_block", tk_add_block_attrs),
+        ("postops", tk_postops_attrs),
         ("clip", _clip),
         ("bias_add", _bias_add),
     ]
@@ -171,7 +186,7 @@ TK_ROUND_UPWARD, TK_ROUND_TONEAREST = 0, 1
 NODE_KINDS = {
     "qnn.conv2d": 1, "qnn.dense": 2, "qnn.requantize": 3, "nn.bias_add": 4, "clip": 5, "cast": 6,
     "qnn.add": 7, "nn.max_pool2d": 8, "nn.avg_pool2d": 9, "nn.global_avg_pool2d": 10, "copy": 11, "shadow": 12,
-    "conv_block": 13, "dense_block": 14, "add_block": 15,
+    "conv_block": 13, "dense_block": 14, "add_block": 15, "postops": 16,
 }
 MAX_NODE_INPUTS = 4
 MAX_NODE_OUTPUTS = 6
@@ -213,6 +228,7 @@ SIGNATURES = {
     "tk_avg_pool2d": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_pool2d_attrs), _VP]),
     "tk_global_avg_pool2d": (ctypes.c_int, [_PT, _PT, _VP]),
     "tk_copy": (ctypes.c_int, [_PT, _PT, _VP]),
+    "tk_tachikoma_postops": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_postops_attrs), _VP]),
     "tk_module_create": (ctypes.c_int, [ctypes.POINTER(tk_node), ctypes.c_int, ctypes.POINTER(_VP)]),
     "tk_module_destroy": (ctypes.c_int, [_VP]),
     "tk_module_num_nodes": (ctypes.c_int, [_VP]),

@@ -585,4 +585,57 @@ int digest_impl(const void* data, int64_t nbytes, uint64_t* out, hipStream_t s) 
   return TK_OK;
 }
 
+// ---------------------------------------------------------------- tachikoma composite post-ops
+// The float32 post-op chain of a legalized tachikoma.qnn.conv2d / .dense composite
+// (tachikoma.py:1262-1276; tachikoma_json_runtime.cc:142-185), see tk_postops_attrs.  Every
+// operation is rounded on its own (__fmul_rn / __fadd_rn: no contraction into FMAs), so the
+// result is a fixed function of the inputs that oracle/tachikoma_ref.py restates.
+template <typename Tout, typename Tsum>
+__global__ __launch_bounds__(kBlock) void postops_kernel(const int32_t* __restrict__ acc, const Tsum* __restrict__ sum_src,
+                                                         Tout* __restrict__ y, int64_t n, int32_t inner, int32_t C,
+                                                         tk_postops_attrs a) {
+  const float lo = (float)std::numeric_limits<Tout>::min(), hi = (float)std::numeric_limits<Tout>::max();
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += stride) {
+    const int c = (int)((i / inner) % C);
+    float t = __fadd_rn((float)acc[i], a.bias[c]);
+    t = __fmul_rn(t, a.o_scl[a.n_scales == 1 ? 0 : c]);
+    t = __fmul_rn(fminf(fmaxf(t, a.clip_lo), a.clip_hi), a.act_scl);
+    if (sum_src) t = __fadd_rn(__fmul_rn(a.sum_scl, (float)sum_src[i]), t);
+    t = __fadd_rn(t, a.dst_zp);
+    t = fminf(fmaxf(__builtin_rintf(t), lo), hi);  // round half to even, saturate
+    y[i] = (Tout)(int)t;
+  }
+}
+
+int postops_impl(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* y, const tk_postops_attrs* a,
+                 hipStream_t s) {
+  TK_CHECK_ARG(acc && y && a && a->bias && a->o_scl, "null argument");
+  TK_CHECK_ARG(is_int(acc, 32) && is_int8ish(y), "acc must be int32, out int8/uint8");
+  TK_CHECK_ARG(compact(acc) && compact(y) && numel(acc) == numel(y), "shape mismatch");
+  TK_CHECK_ARG(!sum_src || (is_int8ish(sum_src) && compact(sum_src) && numel(sum_src) == numel(y)),
+               "sum source must be int8/uint8 shaped like the output");
+  int32_t inner, C;
+  TK_CHECK_ARG(axis_geometry(acc, a->axis, &inner, &C) == TK_OK, "bad axis");
+  TK_CHECK_ARG(a->n_scales == 1 || a->n_scales == C, "o_scl must be per-tensor or per-channel");
+  const int64_t n = numel(y);
+  if (n == 0) return TK_OK;
+  const int grid = grid_for(n);
+  const bool yu = is_uint(y, 8);
+  auto go = [&](auto tout, auto tsum) {
+    using To = decltype(tout);
+    using Ts = decltype(tsum);
+    hipLaunchKernelGGL((postops_kernel<To, Ts>), dim3(grid), dim3(kBlock), 0, s, (const int32_t*)ptr(acc),
+                       sum_src ? (const Ts*)ptr(sum_src) : nullptr, (To*)ptr(y), n, inner, C, *a);
+  };
+  const bool su = sum_src && is_uint(sum_src, 8);
+  if (yu) {
+    if (su) go(uint8_t{}, uint8_t{}); else go(uint8_t{}, int8_t{});
+  } else {
+    if (su) go(int8_t{}, uint8_t{}); else go(int8_t{}, int8_t{});
+  }
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
 }  // namespace tk

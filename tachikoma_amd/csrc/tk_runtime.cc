@@ -28,6 +28,8 @@ int max_pool_shadow_impl(const tk_tensor* x, const void* x_shadow, tk_tensor* y,
 int avg_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s);
 int global_avg_pool_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
 int copy_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
+int postops_impl(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* y, const tk_postops_attrs* a,
+                 hipStream_t s);
 int digest_impl(const void* data, int64_t nbytes, uint64_t* out, hipStream_t s);
 int64_t conv_packed_weight_bytes(const tk_tensor* weight, int groups);
 int conv_pack_weight(const tk_tensor* weight, int groups, void* packed, int32_t* sums, hipStream_t s);
@@ -119,6 +121,8 @@ static int run_node(Node& n, hipStream_t s) {
       return copy_impl(i0, o, s);
     case TK_NODE_SHADOW:
       return make_shadow_impl(i0, d.ext[0], s);
+    case TK_NODE_POSTOPS:
+      return postops_impl(i0, d.n_inputs > 1 ? i1 : nullptr, o, &d.attrs.postops, s);
   }
   set_error("tk_module: unknown node kind " + std::to_string(d.kind));
   return TK_ERR_INVALID_ARG;
@@ -220,6 +224,10 @@ int tk_global_avg_pool2d(const tk_tensor* data, tk_tensor* out, void* stream) {
 }
 int tk_copy(const tk_tensor* data, tk_tensor* out, void* stream) {
   return tk::copy_impl(data, out, tk::as_stream(stream));
+}
+int tk_tachikoma_postops(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* out,
+                         const tk_postops_attrs* attrs, void* stream) {
+  return tk::postops_impl(acc, sum_src, out, attrs, tk::as_stream(stream));
 }
 int tk_digest_bytes(const void* data, int64_t nbytes, uint64_t* out_device, void* stream) {
   return tk::digest_impl(data, nbytes, out_device, tk::as_stream(stream));

@@ -3,10 +3,11 @@
 from . import qnn  # noqa: F401
 from .expr import (Call, Constant, Expr, Function, IRModule, TensorType, Var, const, free_vars,  # noqa: F401
                    post_order, var)
-from .op import (avg_pool2d, batch_flatten, bias_add, cast, clip, global_avg_pool2d, max_pool2d,  # noqa: F401
+from .op import (add, avg_pool2d, batch_flatten, bias_add, cast, clip, global_avg_pool2d, max_pool2d,  # noqa: F401
                  relu, reshape)
 from . import op as _op
 from .parser import ParseError, astext, fromtext, parse  # noqa: F401  (tvm.parser.parse / fromtext)
+from . import contrib  # noqa: F401,E402  (relay.op.contrib.tachikoma analogue: contrib.tachikoma)
 
 
 class _NN:

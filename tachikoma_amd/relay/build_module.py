@@ -275,6 +275,23 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
         ins = _tensor_args(call, 2, names)
         nd = len(call.args[0].shape)
         a["axis"] = a["axis"] if a["axis"] >= 0 else nd + a["axis"]
+    elif op == "add":
+        # relay.add of a per-channel vector (relay.op.add validated the broadcast): the same
+        # int32 wrap-around addition as nn.bias_add along axis 1; the record keeps op "add"
+        ins = _tensor_args(call, 2, names)
+        a.update(axis=1, relay_op="add")
+        op = "nn.bias_add"
+    elif op in ("tachikoma.qnn.conv2d", "tachikoma.qnn.dense"):
+        # a tachikoma BYOC composite (relay/contrib/tachikoma.py): the contraction with zero
+        # zero points, then the float32 post-ops whose folded constants ride in the attrs
+        ins = _tensor_args(call, len(call.args), names)
+        a["input_zero_point"] = 0
+        a["kernel_zero_point"] = 0
+        po = a.pop("postops")
+        consts["postops_bias"] = np.asarray(po["bias"], np.float32).reshape(-1)
+        consts["postops_o_scl"] = np.asarray(po["o_scl"], np.float32).reshape(-1)
+        a.update(act_scl=float(po["act_scl"]), sum_scl=float(po["sum_scl"]), dst_zp=float(po["dst_zp"]),
+                 clip_lo=float(po["clip"][0]), clip_hi=float(po["clip"][1]), has_sum=int(len(ins) > 2))
     elif op == "clip":
         ins = _tensor_args(call, 1, names)
         a["lo"] = _clip_bound(a["a_min"], call.dtype)

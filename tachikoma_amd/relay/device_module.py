@@ -128,7 +128,7 @@ class DeviceModule:
         stream = _lib.stream_handle()
         nodes: List[_lib.tk_node] = []
         # tensors read by MFMA convs need a shadow
-        conv_ops = [g.ops[0] for g in self.groups if g.ops[0].op == "qnn.conv2d"]
+        conv_ops = [g.ops[0] for g in self.groups if g.ops[0].op in ("qnn.conv2d", "tachikoma.qnn.conv2d")]
         mfma = {op.name: self._is_mfma_conv(op) for op in conv_ops}
         shadow_bufs: Dict[str, object] = {}
         # 8-bit max pools read their input's shadow too (16 channels per load) and write
@@ -163,6 +163,9 @@ class DeviceModule:
         for g in self.groups:
             head = g.ops[0]
             n = _lib.tk_node()
+            if g.kind in ("tachikoma.qnn.conv2d", "tachikoma.qnn.dense"):
+                self._emit_composite(head, mfma, shadow_bufs, ensure_shadow, stream, emit)
+                continue
             if g.kind in ("conv_block", "dense_block"):
                 bias_op, rq_op = g.ops[1], g.ops[2]
                 ins = [self._ref(head.inputs[0]), self._ref(head.inputs[1]), self._ref(bias_op.inputs[1])]
@@ -266,6 +269,51 @@ class DeviceModule:
         _lib.check(self.lib.tk_module_create(arr, len(nodes), ctypes.byref(handle)), "tk_module_create")
         self.handle = handle
         self.n_nodes = len(nodes)
+
+    def _emit_composite(self, op: PlanOp, mfma, shadow_bufs, ensure_shadow, stream, emit):
+        """A tachikoma BYOC composite (relay/contrib/tachikoma.py) = two nodes: the contraction
+        with zero zero points into an untraced int32 buffer, then tk_tachikoma_postops writing
+        the composite's output (its one trace record, as the reference's composite function is
+        one graph node)."""
+        torch = _torch()
+        acc = torch.empty(op.out.shape, dtype=torch.int32, device=self.device)
+        self._keep.append(acc)
+        acc_ref = _lib.TensorRef.from_torch(acc)
+        self._keep.append(acc_ref)
+        ins = [self._ref(op.inputs[0]), self._ref(op.inputs[1])]
+        c = _lib.tk_node()
+        if op.op == "tachikoma.qnn.conv2d":
+            c.kind = _lib.NODE_KINDS["qnn.conv2d"]
+            self._conv_attrs(c.attrs.conv2d, op)
+            self._prep_conv(c, op, ins, mfma[op.name], shadow_bufs, ensure_shadow, stream)
+        else:
+            c.kind = _lib.NODE_KINDS["qnn.dense"]
+            self._dense_attrs(c.attrs.dense, op)
+            c.ext[0] = self._scratch(self.lib.tk_qnn_dense_workspace_bytes(ins[0].ptr, ins[1].ptr)).data_ptr()
+        c.n_inputs = 2
+        c.inputs[0], c.inputs[1] = ins[0].ptr, ins[1].ptr
+        c.n_outputs = 1
+        c.outputs[0] = acc_ref.ptr
+        emit(c, op.op + ":contraction", [])  # not a record
+        p = _lib.tk_node()
+        p.kind = _lib.NODE_KINDS["postops"]
+        pa = p.attrs.postops
+        a = op.attrs
+        pa.axis = 1
+        pa.clip_lo, pa.clip_hi = a["clip_lo"], a["clip_hi"]
+        pa.act_scl, pa.sum_scl, pa.dst_zp = a["act_scl"], a["sum_scl"], a["dst_zp"]
+        bias = torch.from_numpy(op.consts["postops_bias"]).to(self.device)
+        o_scl = torch.from_numpy(op.consts["postops_o_scl"]).to(self.device)
+        self._keep += [bias, o_scl]
+        pa.bias, pa.o_scl = bias.data_ptr(), o_scl.data_ptr()
+        pa.n_scales = int(o_scl.numel())
+        p.n_inputs = 1 + a["has_sum"]
+        p.inputs[0] = acc_ref.ptr
+        if a["has_sum"]:
+            p.inputs[1] = self._ref(op.inputs[2]).ptr
+        p.n_outputs = 1
+        p.outputs[0] = self._ref(op.name).ptr
+        emit(p, op.op, [op.name])
 
     def _prep_conv(self, n, op: PlanOp, ins, is_mfma: bool, shadow_bufs, ensure_shadow, stream):
         """MFMA path: shadow of the input + packed weight + weight sums (+ scratch: patch sums,

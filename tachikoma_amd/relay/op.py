@@ -53,6 +53,19 @@ def bias_add(data: Expr, bias: Expr, axis: int = 1) -> Call:
     return Call("nn.bias_add", [data, bias], {"axis": axis}, data.checked_type)
 
 
+def add(lhs: Expr, rhs: Expr) -> Call:
+    """``relay.add`` (python/tvm/relay/op/tensor.py; topi broadcast_add): on the integer trace
+    path the broadcast operand is a per-channel vector along axis 1 (a bias given as [C, 1, 1]
+    or [C], the way frontends and the reference's tachikoma tests write it)."""
+    if lhs.dtype != rhs.dtype:
+        raise TypeError("add: dtype mismatch")
+    nd, rs = len(lhs.shape), tuple(rhs.shape)
+    padded = (1,) * (nd - len(rs)) + rs if len(rs) <= nd else None
+    if nd < 2 or padded is None or padded[1] != lhs.shape[1] or any(d != 1 for i, d in enumerate(padded) if i != 1):
+        raise NotImplementedError(f"add: only a per-channel vector broadcast along axis 1 ({lhs.shape} + {rs})")
+    return Call("add", [lhs, rhs], {}, lhs.checked_type)
+
+
 def clip(a: Expr, a_min: float, a_max: float) -> Call:
     return Call("clip", [a], {"a_min": float(a_min), "a_max": float(a_max)}, a.checked_type)
 

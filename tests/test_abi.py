@@ -41,7 +41,8 @@ LAYOUT_C = r"""
 #define O(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
   P(tk_tensor) P(tk_requantize_attrs) P(tk_conv2d_attrs) P(tk_dense_attrs) P(tk_qnn_add_attrs)
-  P(tk_pool2d_attrs) P(tk_block_attrs) P(tk_node) P(tk_array_meta) P(tk_trace_header)
+  P(tk_pool2d_attrs) P(tk_block_attrs) P(tk_node) P(tk_array_meta) P(tk_trace_header) P(tk_postops_attrs)
+  O(tk_postops_attrs, dst_zp) O(tk_postops_attrs, bias) O(tk_postops_attrs, o_scl)
   O(tk_tensor, shape) O(tk_tensor, byte_offset) O(tk_node, inputs) O(tk_node, n_outputs) O(tk_node, outputs) O(tk_node, ext)
   O(tk_node, attrs) O(tk_qnn_add_attrs, rhs) O(tk_qnn_add_attrs, lhs_upcast) O(tk_requantize_attrs, output_zero_point)
   O(tk_conv2d_attrs, kernel_zero_points) O(tk_array_meta, dtype)
@@ -61,7 +62,10 @@ def test_ctypes_layout_matches_c(tmp_path):
         "tk_conv2d_attrs": ctypes.sizeof(_lib.tk_conv2d_attrs), "tk_dense_attrs": ctypes.sizeof(_lib.tk_dense_attrs),
         "tk_qnn_add_attrs": ctypes.sizeof(_lib.tk_qnn_add_attrs), "tk_pool2d_attrs": ctypes.sizeof(_lib.tk_pool2d_attrs),
         "tk_node": ctypes.sizeof(_lib.tk_node), "tk_block_attrs": ctypes.sizeof(_lib.tk_block_attrs), "tk_array_meta": ctypes.sizeof(_lib.tk_array_meta),
-        "tk_trace_header": 56,
+        "tk_trace_header": 56, "tk_postops_attrs": ctypes.sizeof(_lib.tk_postops_attrs),
+        "tk_postops_attrs.dst_zp": _lib.tk_postops_attrs.dst_zp.offset,
+        "tk_postops_attrs.bias": _lib.tk_postops_attrs.bias.offset,
+        "tk_postops_attrs.o_scl": _lib.tk_postops_attrs.o_scl.offset,
         "tk_tensor.shape": _lib.tk_tensor.shape.offset, "tk_tensor.byte_offset": _lib.tk_tensor.byte_offset.offset,
         "tk_node.inputs": _lib.tk_node.inputs.offset, "tk_node.n_outputs": _lib.tk_node.n_outputs.offset,
         "tk_node.outputs": _lib.tk_node.outputs.offset,
