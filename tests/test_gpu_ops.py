@@ -249,6 +249,8 @@ BLOCK_CASES = [
     (2, 512, 7, 7, 64, 3, 1, 1, 1, "int8", -3, "int8", (0, 127)),     # 128-byte K stages + split-K
     (2, 256, 14, 14, 128, 3, 1, 1, 1, "int8", 2, "int8", None),       # 128-byte K stages, 128-column tiles
     (2, 128, 9, 9, 64, 3, 1, 1, 1, "uint8", 130, "uint8", (128, 255)),  # 128-byte K stages, uint8
+    (2, 128, 12, 12, 128, 3, 1, 1, 1, "int8", 3, "int8", (0, 127)),   # 128 channels, K >= 512: 128-row tiles
+    (3, 512, 6, 6, 128, 1, 1, 0, 1, "uint8", 129, "uint8", None),     # 128-row tiles, 1x1, uint8
 ]
 
 
@@ -279,6 +281,7 @@ RESIDUAL_CASES = [
     (2, 64, 7, 7, 96, 3, 1, 1, "int8", (0.04, 0, 0.04, 0, 0.04, 0), None, False),     # both upcast, scalar stores
     (1, 48, 12, 12, 64, 3, 1, 1, "uint8", (0.1, 130, 0.2, 120, 0.15, 128), (128, 255), True),
     (2, 256, 7, 7, 128, 3, 1, 1, "int8", (0.05, -3, 0.06, 4, 0.08, -1), (-1, 127), False),  # split-K
+    (2, 512, 10, 10, 128, 1, 1, 0, "int8", (0.05, -3, 0.06, 4, 0.08, -1), (0, 127), True),  # 128-row tiles
 ]
 
 
