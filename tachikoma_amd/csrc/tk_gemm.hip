@@ -797,7 +797,7 @@ gemm_i8_kernel(GemmArgs g) {
   bool done = false;
   if constexpr (kBlock) {
     if (g.ipt && !(g.ablate & 0x7F)) {
-      // ---- flat epilogue (image-aligned tiles, planes of 4..64 pixels): for image kk of the
+      // ---- flat epilogue (image-aligned tiles, planes of 1..64 pixels): for image kk of the
       // tile, its channels m0.. and all OH*OW pixels are one contiguous run of the NCHW
       // records, `run` elements long.  Group gi = 4 consecutive elements of one run: b128
       // stores of the int32 records and b32 stores of the 8-bit ones, contiguous across lanes
@@ -830,8 +830,10 @@ gemm_i8_kernel(GemmArgs g) {
           v4u v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const bool wrap = p0 + e >= hw;  // hw >= 4: at most one row change per group
-            const int re = r0 + (wrap ? 1 : 0), pe = p0 + e - (wrap ? hw : 0);
+            int re = r0, pe = p0 + e;
+#pragma unroll
+            for (int w = 0; w < 3; ++w)  // one row change per group when hw >= 4, up to 3 below
+              if (pe >= hw) pe -= hw, ++re;
             slot[e] = re * kEpiStride + kk * hw + pe;
             rr[e] = rowc[re];
             v[e] = (uint32_t)tileI[slot[e]];
@@ -1427,12 +1429,12 @@ static bool conv_needs_patch(const tk_tensor* weight, const tk_conv2d_attrs* a) 
   return (a->kernel_zero_point - (is_uint(weight, 8) ? 128 : 0)) != 0 || a->kernel_zero_points;
 }
 
-// Images per N tile of a conv block whose planes hold 4..64 pixels (0: plain 128-column
+// Images per N tile of a conv block whose planes hold 1..64 pixels (0: plain 128-column
 // tiles).  Needs the flat epilogue's preconditions: no per-pixel zero-point patch, a channel
 // count that keeps every image run 16-byte aligned, and 32-bit record offsets.
 static int conv_image_tiles(const ConvGeom& g, bool block, bool patch) {
   const int64_t hw = (int64_t)g.OH * g.OW;
-  if (!block || patch || hw < 4 || hw > 64 || g.O % 4 != 0 || (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll ||
+  if (!block || patch || hw > 64 || g.O % 4 != 0 || (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll ||
       !env_int("TK_IMGTILE", 1))
     return 0;
   return (int)(128 / hw);

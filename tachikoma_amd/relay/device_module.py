@@ -191,6 +191,8 @@ class DeviceModule:
                         # the epilogue writes the shadow the next MFMA conv reads
                         n.ext[4] = shadow_bufs[g.last.name].data_ptr()
                         shadow_ready.add(g.last.name)
+                elif self._dense_as_conv(n, g, head, ins, outs, emit, stream):
+                    pass
                 else:
                     n.kind = _lib.NODE_KINDS["dense_block"]
                     self._dense_attrs(ba.dense, head)
@@ -269,6 +271,62 @@ class DeviceModule:
         _lib.check(self.lib.tk_module_create(arr, len(nodes), ctypes.byref(handle)), "tk_module_create")
         self.handle = handle
         self.n_nodes = len(nodes)
+
+    def _view_ref(self, name: str, shape) -> _lib.TensorRef:
+        r = _lib.TensorRef.from_torch(self.buffers[name].view(*shape))
+        self._keep.append(r)
+        return r
+
+    def _dense_as_conv(self, n, g: ExecGroup, head: PlanOp, ins, outs, emit, stream) -> bool:
+        """A dense block [M, K] x [U, K]^T runs as a 1x1 conv block over [M, K, 1, 1]: the NCHW
+        output [M, U, 1, 1] is the dense output's memory, requantize/bias stay on axis 1, and
+        the conv path's weight packing happens once here instead of padding both operands on
+        every run (the dense path's per-call pad_rows kernels).  Records are unchanged (same
+        buffers).  Returns False (plain dense block) when the conv would not take MFMA."""
+        import os
+        if os.environ.get("TK_DENSE_CONV", "1") == "0":
+            return False
+        m, k = head.out.shape[0], self.plan.tensor(head.inputs[0]).shape[1]
+        u = head.out.shape[1]
+        x4 = self._view_ref(head.inputs[0], (m, k, 1, 1))
+        w4 = self._view_ref(head.inputs[1], (u, k, 1, 1))
+        ca = n.attrs.block.conv
+        ca.strides[:] = [1, 1]
+        ca.padding[:] = [0, 0, 0, 0]
+        ca.dilation[:] = [1, 1]
+        ca.groups = 1
+        ca.input_zero_point = head.attrs["input_zero_point"]
+        ca.kernel_zero_point = head.attrs["kernel_zero_point"]
+        if "kernel_zero_points" in head.consts:
+            ca.kernel_zero_points = self._dev_i32(head.consts["kernel_zero_points"]).data_ptr()
+        if self.lib.tk_qnn_conv2d_workspace_bytes(x4.ptr, w4.ptr, ctypes.byref(ca)) <= 0:
+            n.attrs.block.conv = _lib.tk_conv2d_attrs()
+            return False
+        # shadow of the input (its producer is a flatten/copy node, which writes none)
+        shadow = self._scratch(self.lib.tk_conv2d_shadow_bytes(x4.ptr), zero=True)
+        sn = _lib.tk_node()
+        sn.kind = _lib.NODE_KINDS["shadow"]
+        sn.n_inputs = 1
+        sn.inputs[0] = x4.ptr
+        sn.n_outputs = 0
+        sn.ext[0] = shadow.data_ptr()
+        emit(sn, "shadow", [])
+        packed = self._scratch(self.lib.tk_conv2d_packed_weight_bytes(w4.ptr, 1))
+        sums = self._scratch(((u + 127) // 128 * 128) * 4)
+        _lib.check(self.lib.tk_conv2d_pack_weight(w4.ptr, 1, ctypes.c_void_p(packed.data_ptr()),
+                                                  ctypes.c_void_p(sums.data_ptr()), ctypes.c_void_p(stream)),
+                   f"{head.name} pack weight")
+        n.kind = _lib.NODE_KINDS["conv_block"]
+        n.ext[0], n.ext[1], n.ext[2] = shadow.data_ptr(), packed.data_ptr(), sums.data_ptr()
+        nbytes = self.lib.tk_conv2d_scratch_bytes(x4.ptr, w4.ptr, ctypes.byref(ca), 1)
+        if nbytes < 0:
+            _lib.check(-3, f"{head.name} conv scratch")
+        if nbytes > 0:
+            n.ext[3] = self._scratch(nbytes).data_ptr()
+        ins[0], ins[1] = x4, w4
+        for i, o in enumerate(g.ops):
+            outs[i] = self._view_ref(o.name, tuple(o.out.shape) + (1, 1))
+        return True
 
     def _emit_composite(self, op: PlanOp, mfma, shadow_bufs, ensure_shadow, stream, emit):
         """A tachikoma BYOC composite (relay/contrib/tachikoma.py) = two nodes: the contraction

@@ -251,6 +251,8 @@ BLOCK_CASES = [
     (2, 128, 9, 9, 64, 3, 1, 1, 1, "uint8", 130, "uint8", (128, 255)),  # 128-byte K stages, uint8
     (2, 128, 12, 12, 128, 3, 1, 1, 1, "int8", 3, "int8", (0, 127)),   # 128 channels, K >= 512: 128-row tiles
     (3, 512, 6, 6, 128, 1, 1, 0, 1, "uint8", 129, "uint8", None),     # 128-row tiles, 1x1, uint8
+    (150, 256, 1, 1, 200, 1, 1, 0, 1, "int8", 2, "int8", (0, 127)),   # 1x1 planes (a dense layer): 128 images per tile
+    (9, 64, 3, 3, 64, 3, 1, 1, 1, "int8", -1, "int8", None),          # 3x3 planes: up to 3 row changes per group
 ]
 
 
@@ -282,6 +284,7 @@ RESIDUAL_CASES = [
     (1, 48, 12, 12, 64, 3, 1, 1, "uint8", (0.1, 130, 0.2, 120, 0.15, 128), (128, 255), True),
     (2, 256, 7, 7, 128, 3, 1, 1, "int8", (0.05, -3, 0.06, 4, 0.08, -1), (-1, 127), False),  # split-K
     (2, 512, 10, 10, 128, 1, 1, 0, "int8", (0.05, -3, 0.06, 4, 0.08, -1), (0, 127), True),  # 128-row tiles
+    (70, 64, 1, 1, 96, 1, 1, 0, "uint8", (0.1, 130, 0.2, 120, 0.15, 128), (128, 255), True),  # 1x1 planes
 ]
 
 
