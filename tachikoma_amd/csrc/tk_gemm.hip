@@ -95,7 +95,8 @@ struct GemmArgs {
   int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
                        // 8/16/32/64 skip the conv / bias_add / requantize / clip record,
                        // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs, 1024 main-loop
-                       // barrier without the lgkmcnt(0) drain
+                       // barrier without the lgkmcnt(0) drain, 2048 skip the fragment reads, 4096 skip
+                       // the main-loop barrier (timing skeletons only: results are garbage)
 };
 
 // Writes one element of every output of a fused block.  Mirrors, per element:
@@ -575,6 +576,7 @@ gemm_i8_kernel(GemmArgs g) {
   };
 
   if constexpr (kMode != 2 && kIm2col) {
+    const int ablate = __builtin_amdgcn_readfirstlane(g.ablate);
     // ---- LDS-DMA pipeline (conv): a kRing-stage ring filled by global_load_lds_dwordx4 with
     // kRing - 1 stages in flight across the barrier (counted vmcnt + raw s_barrier).
     // The LDS image is lane-linear (lane l of a wave-instruction lands at base + 16 l =
@@ -599,22 +601,23 @@ gemm_i8_kernel(GemmArgs g) {
         // retire stage it (A_CHUNKS + B_CHUNKS LDS-DMAs per thread and stage); the later
         // stages already issued stay in flight
         wait_vm(min(nst - 1 - it, kRing - 2) * (A_DMA + B_DMA));
-        if (g.ablate & 1024) asm volatile("s_barrier" ::: "memory");
+        if (ablate & 4096) {
+        } else if (ablate & 1024) asm volatile("s_barrier" ::: "memory");
         else lds_barrier();  // stage it visible to all waves; the slot read in step it-1 is free
         // fragments of stage it first, so that their LDS latency overlaps the next issue
         const int8_t* a = smem + (it % kRing) * kStageBytes;
         Frags f;
-        read_frags(a, a + BM * SBK, f);
+        if (!(ablate & 2048)) read_frags(a, a + BM * SBK, f);
         __builtin_amdgcn_sched_barrier(0);
         if (it + kRing - 1 < nst) issue((it + kRing - 1) % kRing);
         __builtin_amdgcn_sched_barrier(0);
-        if (!(g.ablate & 512)) mfma_frags(f);
+        if (!(ablate & 512)) mfma_frags(f);
       }
     };
     auto issue_a = [&](int8_t* sa) {
 #pragma unroll
       for (int t = 0; t < A_DMA; ++t) {
-        if (!(g.ablate & 128))
+        if (!(ablate & 128))
           __builtin_amdgcn_global_load_lds((const void*)a_src[t], (void*)(sa + ((RPP / 4) * wave_u + RPP * t) * SBK),
                                            16, 0, 0);
         a_src[t] += SBK;
@@ -653,25 +656,29 @@ gemm_i8_kernel(GemmArgs g) {
       }
       const int64_t grp_bytes = g.in_pix * 16;
       const int64_t row_bytes = (int64_t)g.dh * g.W * 16;
+      const int KW = g.KW, cgroups = g.cgroups, dw16 = g.dw * 16;
+      int tap = kh * KW + kw;
+      int64_t soff = cg * grp_bytes + kh * row_bytes + (int64_t)kw * dw16;
       pipeline([&](int slot) {
         int8_t* sa = smem + slot * kStageBytes;
         issue_a(sa);
         int8_t* sb = sa + BM * SBK;
-        const int tap = kh * g.KW + kw;
-        const int64_t soff = cg * grp_bytes + kh * row_bytes + (int64_t)(kw * g.dw) * 16;
-        const bool grp_ok = cg + cl < g.cgroups;  // K padding of a 1x1 conv with cin_pad % 64 != 0
+        const bool grp_ok = cg + cl < cgroups;  // K padding of a 1x1 conv with cin_pad % 64 != 0
 #pragma unroll
         for (int t = 0; t < B_DMA; ++t) {
           const bool ok = ((tmask[t] >> tap) & 1) && grp_ok;
           const int8_t* src = ok ? lane_base[t] + soff : fill_src;
-          if (!(g.ablate & 256))
+          if (!(ablate & 256))
             __builtin_amdgcn_global_load_lds((const void*)src, (void*)(sb + ((RPP / 4) * wave_u + RPP * t) * SBK),
                                              16, 0, 0);
         }
         cg += CPR;
-        if (cg >= g.cgroups) {
+        soff += CPR * grp_bytes;
+        if (cg >= cgroups) {
           cg = 0;
-          if (++kw == g.KW) kw = 0, ++kh;
+          ++tap;
+          if (++kw == KW) kw = 0, ++kh;
+          soff = kh * row_bytes + (int64_t)kw * dw16;
         }
       });
     } else if constexpr (!kWide) {
@@ -702,7 +709,7 @@ gemm_i8_kernel(GemmArgs g) {
           const bool inb = ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
           const int8_t* src = g.B + (plane + b_pix[t] + dy * g.W + dx) * 16;
           src = (b_valid[t] && tap_ok && inb) ? src : fill_src;
-          if (!(g.ablate & 256))
+          if (!(ablate & 256))
             __builtin_amdgcn_global_load_lds((const void*)src, (void*)(sb + (16 * wave_u + 64 * t) * kBK), 16, 0, 0);
         }
         c0 += kBK;
