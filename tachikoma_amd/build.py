@@ -8,7 +8,9 @@ exported symbols are exactly the ``extern "C"`` entry points of
 from __future__ import annotations
 
 import concurrent.futures
+import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -38,13 +40,37 @@ def _newer(target: str, deps) -> bool:
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
-def _compile(src: str, obj: str, extra) -> None:
+RESOURCES = os.path.join(BUILD, "kernel_resources.json")
+_REMARK = re.compile(r"remark:\s+(Function Name|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|"
+                     r"LDS Size \[bytes/block\]):\s*(\S+)")
+
+
+def _resources(stderr: str):
+    """Per-kernel register / scratch / LDS / occupancy from -Rpass-analysis=kernel-resource-usage."""
+    out, cur = {}, None
+    for key, val in _REMARK.findall(stderr):
+        if key == "Function Name":
+            cur = out.setdefault(val, {})
+        elif cur is not None:
+            cur[key.split(" [")[0]] = int(val) if val.lstrip("-").isdigit() else val
+    return out
+
+
+def _compile(src: str, obj: str, extra):
     hipcc = _hipcc()
     cmd = [hipcc, "-std=c++17", "-O3", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}",
            "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function", "-c", src, "-o", obj] + extra
     if src.endswith(".cc"):
         cmd[1:1] = ["-x", "hip"]
-    subprocess.run(cmd, check=True)
+    else:
+        cmd += ["-Rpass-analysis=kernel-resource-usage", "-fno-caret-diagnostics"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    noise = [ln for ln in r.stderr.splitlines() if "kernel-resource-usage" not in ln and ln.strip()]
+    if noise:
+        sys.stderr.write("\n".join(noise) + "\n")
+    if r.returncode != 0:
+        raise subprocess.CalledProcessError(r.returncode, cmd)
+    return _resources(r.stderr)
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
@@ -60,10 +86,23 @@ def build(force: bool = False, verbose: bool = True) -> str:
             jobs.append((src, obj))
     if jobs:
         workers = min(len(jobs), int(os.environ.get("MAX_JOBS", "8")))
+        res = {}
+        if os.path.exists(RESOURCES):
+            with open(RESOURCES) as f:
+                res = json.load(f)
         with concurrent.futures.ThreadPoolExecutor(max_workers=workers) as ex:
-            futs = [ex.submit(_compile, s, o, []) for s, o in jobs]
-            for f in futs:
-                f.result()
+            futs = [(os.path.basename(s), ex.submit(_compile, s, o, [])) for s, o in jobs]
+            for name, f in futs:
+                r = f.result()
+                if name.endswith(".hip"):
+                    res[name] = r
+        with open(RESOURCES, "w") as f:
+            json.dump(res, f, indent=1, sort_keys=True)
+        # a kernel that spills to scratch (or copies its arguments there) runs several times
+        # slower: fail the build instead of shipping it
+        bad = [k for unit in res.values() for k, v in unit.items() if v.get("ScratchSize", 0)]
+        if bad:
+            raise RuntimeError(f"kernels using scratch memory: {bad[:5]} (see {RESOURCES})")
     if force or jobs or not _newer(LIB, objs):
         tmp = LIB + ".tmp"
         subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs, check=True)

@@ -175,7 +175,14 @@ __global__ __launch_bounds__(kThreads) void add_block_plane_kernel(AddBlockArgs 
       }
       store_nt<16>(g.add_out + base + 16 * v, vo);
       if (g.has_clip) store_nt<16>(g.clip_out + base + 16 * v, vc);
-      if (g.shadow) __builtin_memcpy(tile + 16 * v, g.has_clip ? vc : vo, 16);
+      if (g.shadow) {
+        // element-wise select: a pointer chosen between two local arrays would force both
+        // into scratch memory
+        uint8_t vs[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) vs[q] = g.has_clip ? vc[q] : vo[q];
+        __builtin_memcpy(tile + 16 * v, vs, 16);
+      }
     }
     if (!g.shadow) continue;
     __syncthreads();
