@@ -1224,6 +1224,127 @@ __global__ __launch_bounds__(256) void direct_conv_kernel(const Tx* __restrict__
   }
 }
 
+// Depthwise 3x3 conv (groups == C == O, the MobileNetV2 layers) with the fused block epilogue.
+// One workgroup = one image x 16 channels x a band of BH output rows:
+//   * the input band plus halo is staged planar in LDS ([16][rows][cols], bytes, taps outside
+//     the image hold the input zero point so they contribute 0, legalizations.py:195-226), the
+//     per-channel weights minus their zero point as int32;
+//   * lanes run along output columns, V consecutive pixels each, so every record store is a
+//     contiguous row segment of an NCHW plane (b128 int32 / b32 int8 when V = 4);
+//   * the final 8-bit values are parked in LDS and written to the next conv's channel-blocked
+//     shadow as one 16-byte chunk (the 16 channels) per pixel.
+// Same arithmetic as direct_conv_kernel / epilogue_store (int32 wrap-around accumulation).
+template <typename Tx, typename Tw, int V>
+__global__ __launch_bounds__(256) void dw3x3_kernel(const Tx* __restrict__ x, const Tw* __restrict__ w, int C, int H,
+                                                    int W, int OH, int OW, int sh, int sw, int pt, int pl, int32_t za,
+                                                    int32_t zw, const int32_t* __restrict__ zw_vec, int BH, int bands,
+                                                    int Wp, GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int bid = blockIdx.x;
+  const int band = bid % bands;
+  bid /= bands;
+  const int cgroups = C / 16;
+  const int cgrp = bid % cgroups, n = bid / cgroups;
+  const int c0 = cgrp * 16;
+  const int oh0 = band * BH;
+  const int bh = min(BH, OH - oh0);
+  const int rows_in = (bh - 1) * sh + 3;
+  const int ih0 = oh0 * sh - pt;
+  uint8_t* tin = dsm;
+  const int tin_bytes = (16 * rows_in * Wp + 15) & ~15;
+  int32_t* wts = reinterpret_cast<int32_t*>(dsm + tin_bytes);
+  uint8_t* tout = dsm + tin_bytes + 16 * 9 * 4;
+  // ---- stage the band: (channel, input row) rows, lanes along columns (Wp <= 192: 3 column
+  // slots per lane); 8 rows per wave at a time so that 8-24 loads per lane are in flight
+  const uint8_t fillb = (uint8_t)za;
+  const uint8_t* xb = reinterpret_cast<const uint8_t*>(x);
+  const int nrows = 16 * rows_in;
+  for (int r0 = wave; r0 < nrows; r0 += 32) {
+    uint8_t v[8][3];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = r0 + 4 * u;
+      const int c = r / rows_in, lr = r - c * rows_in;
+      const int ih = ih0 + lr;
+      const bool row_ok = r < nrows && ih >= 0 && ih < H;
+      const uint8_t* src = xb + (((int64_t)n * C + c0 + c) * H + (row_ok ? ih : 0)) * W;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int iw = lane + 64 * k - pl;
+        v[u][k] = (row_ok && iw >= 0 && iw < W) ? src[iw] : fillb;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = r0 + 4 * u;
+      if (r < nrows) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (lane + 64 * k < Wp) tin[r * Wp + lane + 64 * k] = v[u][k];
+      }
+    }
+  }
+  if (tid < 16 * 9) {
+    const int c = tid / 9;
+    wts[tid] = (int32_t)w[(int64_t)(c0 + c) * 9 + (tid - c * 9)] - (zw_vec ? zw_vec[c0 + c] : zw);
+  }
+  __syncthreads();
+  // ---- 9 taps + epilogue, V pixels of one channel row per item
+  const int owv = OW / V;
+  const int items = 16 * bh * owv;
+  const int qmin = (int)g.rq.qmin, qmax = (int)g.rq.qmax;
+  for (int it = tid; it < items; it += 256) {
+    const int vv = it % owv;
+    const int t = it / owv;
+    const int row = t % bh, c = t / bh;
+    const int ch = c0 + c;
+    int32_t acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const uint8_t* base = tin + (c * rows_in + row * sh + r) * Wp;
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const int32_t wv = wts[c * 9 + r * 3 + s2];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const int32_t a = (int32_t)(Tx)base[(vv * V + e) * sw + s2] - za;
+          acc[e] = (int32_t)((uint32_t)acc[e] + (uint32_t)(a * wv));
+        }
+      }
+    }
+    const int oh = oh0 + row, ow = vv * V;
+    const int64_t off = (((int64_t)n * C + ch) * OH + oh) * OW + ow;
+    int32_t v[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = acc[e];
+    st_i32<V>(g.C + off, v, false);
+    const int32_t bias = g.bias[ch];
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = (int32_t)((uint32_t)v[e] + (uint32_t)bias);
+    st_i32<V>(g.bias_out + off, v, false);
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = min(max(rq_apply(v[e], ch, g.rq), qmin), qmax);
+    st_i8<V>(g.rq_out + off, v, false);
+    if (g.has_clip) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[e] = min(max(v[e], g.clip_lo), g.clip_hi);
+      st_i8<V>(g.clip_out + off, v, false);
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) tout[((row * OW) + ow + e) * 16 + c] = (uint8_t)((uint32_t)v[e] ^ g.shadow_xor);
+  }
+  if (!g.shadow_out) return;
+  __syncthreads();
+  // ---- shadow: 16 channels of one pixel per 16-byte store, contiguous across lanes
+  const int64_t pix0 = ((int64_t)n * OH + oh0) * OW;
+  for (int p = tid; p < bh * OW; p += 256)
+    *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)cgrp * g.N + pix0 + p) * 16) =
+        *reinterpret_cast<const v4i*>(tout + p * 16);
+}
+
 // ---------------------------------------------------------------- host wrappers
 
 struct ConvGeom {
@@ -1524,6 +1645,41 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   if (rc) return rc;
   if (!use_mfma_conv(g, a->groups)) {
     TK_CHECK_ARG(!(blk && blk->attrs->has_add), "residual join needs an MFMA conv block");
+    // depthwise 3x3 blocks: the LDS-staged band kernel (see dw3x3_kernel)
+    // (large planes only: on 7x7 / 14x14 planes and strided 28x28 ones the generic kernel measured
+    // faster, the band staging does not amortise; MobileNetV2 dw layers 1.2-2x faster otherwise)
+    const int64_t ohw = (int64_t)g.OH * g.OW;
+    if (blk && a->groups == g.C && g.C == g.O && g.C % 16 == 0 && g.KH == 3 && g.KW == 3 && a->dilation[0] == 1 &&
+        a->dilation[1] == 1 && ((a->strides[0] == 1 && ohw >= 784) || ohw >= 3136) && env_int("TK_DW", 1)) {
+      const int sh = a->strides[0], sw = a->strides[1];
+      const int budget = sh == 1 ? 1024 : 512;  // output pixels per workgroup and channel
+      const int BH = g.OH * g.OW <= budget ? g.OH : std::max(1, budget / g.OW);
+      const int bands = (g.OH + BH - 1) / BH;
+      const int Wp = (g.OW - 1) * sw + 3;
+      const int rows_max = (BH - 1) * sh + 3;
+      const size_t lds = (size_t)((16 * rows_max * Wp + 15) & ~15) + 16 * 9 * 4 + (size_t)BH * g.OW * 16;
+      if (lds <= 64 * 1024 && Wp <= 192) {
+        const unsigned grid = (unsigned)((int64_t)g.N * (g.C / 16) * bands);
+        const bool v4 = g.OW % 4 == 0;
+#define TK_DW(TX, TW)                                                                                              \
+  if (v4)                                                                                                          \
+    hipLaunchKernelGGL((dw3x3_kernel<TX, TW, 4>), dim3(grid), dim3(256), lds, s, (const TX*)ptr(data),            \
+                       (const TW*)ptr(weight), g.C, g.H, g.W, g.OH, g.OW, sh, sw, a->padding[0], a->padding[1],     \
+                       a->input_zero_point, a->kernel_zero_point, a->kernel_zero_points, BH, bands, Wp, ga);      \
+  else                                                                                                             \
+    hipLaunchKernelGGL((dw3x3_kernel<TX, TW, 1>), dim3(grid), dim3(256), lds, s, (const TX*)ptr(data),            \
+                       (const TW*)ptr(weight), g.C, g.H, g.W, g.OH, g.OW, sh, sw, a->padding[0], a->padding[1],     \
+                       a->input_zero_point, a->kernel_zero_point, a->kernel_zero_points, BH, bands, Wp, ga)
+        const bool du = is_uint(data, 8), wu = is_uint(weight, 8);
+        if (du && wu) { TK_DW(uint8_t, uint8_t); }
+        else if (du) { TK_DW(uint8_t, int8_t); }
+        else if (wu) { TK_DW(int8_t, uint8_t); }
+        else { TK_DW(int8_t, int8_t); }
+#undef TK_DW
+        TK_LAUNCH_CHECK();
+        return TK_OK;
+      }
+    }
     // grouped / depthwise / tiny channel counts: direct VALU kernel on NCHW
     int64_t total = (int64_t)g.N * g.O * g.OH * g.OW;
     int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));

@@ -253,6 +253,9 @@ BLOCK_CASES = [
     (3, 512, 6, 6, 128, 1, 1, 0, 1, "uint8", 129, "uint8", None),     # 128-row tiles, 1x1, uint8
     (150, 256, 1, 1, 200, 1, 1, 0, 1, "int8", 2, "int8", (0, 127)),   # 1x1 planes (a dense layer): 128 images per tile
     (9, 64, 3, 3, 64, 3, 1, 1, 1, "int8", -1, "int8", None),          # 3x3 planes: up to 3 row changes per group
+    (2, 64, 56, 56, 64, 3, 1, 1, 64, "int8", 3, "int8", (0, 127)),    # depthwise band kernel, 4-pixel vectors, last band partial
+    (1, 16, 112, 112, 16, 3, 2, 1, 16, "uint8", 130, "uint8", (128, 255)),  # depthwise stride 2, uint8
+    (3, 32, 14, 14, 32, 3, 1, 1, 32, "int8", -4, "int8", None),       # depthwise, whole plane per group, scalar pixels
 ]
 
 
