@@ -73,6 +73,26 @@ def _compile(src: str, obj: str, extra):
     return _resources(r.stderr)
 
 
+def build_ablation(verbose: bool = True) -> str:
+    """Profiling variant with the main-loop ablation switches compiled in (TK_ABLATE env, see
+    GemmArgs::ablate): tachikoma_amd/_ab/libtachikoma_ablate.so, loaded by the tools through
+    TK_LIB_PATH.  The product library has them compiled out."""
+    out_dir = os.path.join(HERE, "_ab")
+    obj_dir = os.path.join(BUILD, "ablate")
+    os.makedirs(out_dir, exist_ok=True)
+    os.makedirs(obj_dir, exist_ok=True)
+    objs = []
+    for s in SOURCES:
+        obj = os.path.join(obj_dir, s + ".o")
+        _compile(os.path.join(CSRC, s), obj, ["-DTK_ABLATION_BUILD"])
+        objs.append(obj)
+    lib = os.path.join(out_dir, "libtachikoma_ablate.so")
+    subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs, check=True)
+    if verbose:
+        print(f"[tachikoma] built {lib}")
+    return lib
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     os.makedirs(BUILD, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "tachikoma.h")]
@@ -113,4 +133,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--ablation" in sys.argv:
+        build_ablation()
+    else:
+        build(force="--force" in sys.argv)

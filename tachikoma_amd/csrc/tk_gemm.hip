@@ -576,7 +576,11 @@ gemm_i8_kernel(GemmArgs g) {
   };
 
   if constexpr (kMode != 2 && kIm2col) {
-    const int ablate = __builtin_amdgcn_readfirstlane(g.ablate);
+#ifdef TK_ABLATION_BUILD
+    const int ablate = __builtin_amdgcn_readfirstlane(g.ablate);  // profiling builds only
+#else
+    constexpr int ablate = 0;  // the main-loop ablation branches compile away
+#endif
     // ---- LDS-DMA pipeline (conv): a kRing-stage ring filled by global_load_lds_dwordx4 with
     // kRing - 1 stages in flight across the barrier (counted vmcnt + raw s_barrier).
     // The LDS image is lane-linear (lane l of a wave-instruction lands at base + 16 l =
@@ -597,22 +601,33 @@ gemm_i8_kernel(GemmArgs g) {
 #pragma unroll
       for (int st = 0; st < kRing - 1; ++st)
         if (st < nst) issue(st);
-      for (int it = 0; it < nst; ++it) {
-        // retire stage it (A_CHUNKS + B_CHUNKS LDS-DMAs per thread and stage); the later
-        // stages already issued stay in flight
-        wait_vm(min(nst - 1 - it, kRing - 2) * (A_DMA + B_DMA));
+      int cur = 0, nxt = kRing - 1;  // ring slots of stage it and of stage it + kRing - 1
+      // one step: retire stage it (A_DMA + B_DMA LDS-DMAs per thread and stage) with `pending`
+      // later stages still in flight, barrier (stage it visible to all waves; the slot read in
+      // step it-1 is free), fragments of stage it first so that their LDS latency overlaps the
+      // next issue, then the MFMAs
+      auto step = [&](int it, int pending) __attribute__((always_inline)) {
+        wait_vm(pending * (A_DMA + B_DMA));
         if (ablate & 4096) {
         } else if (ablate & 1024) asm volatile("s_barrier" ::: "memory");
-        else lds_barrier();  // stage it visible to all waves; the slot read in step it-1 is free
-        // fragments of stage it first, so that their LDS latency overlaps the next issue
-        const int8_t* a = smem + (it % kRing) * kStageBytes;
+        else lds_barrier();
+        const int8_t* a = smem + cur * kStageBytes;
         Frags f;
         if (!(ablate & 2048)) read_frags(a, a + BM * SBK, f);
         __builtin_amdgcn_sched_barrier(0);
-        if (it + kRing - 1 < nst) issue((it + kRing - 1) % kRing);
+        if (it + kRing - 1 < nst) {
+          issue(nxt);
+          nxt = nxt == kRing - 1 ? 0 : nxt + 1;
+        }
         __builtin_amdgcn_sched_barrier(0);
         if (!(ablate & 512)) mfma_frags(f);
-      }
+        cur = cur == kRing - 1 ? 0 : cur + 1;
+      };
+      // steady state with a compile-time wait count, then the last kRing - 2 stages
+      const int steady = nst - (kRing - 2);
+      int it = 0;
+      for (; it < steady; ++it) step(it, kRing - 2);
+      for (; it < nst; ++it) step(it, nst - 1 - it);
     };
     auto issue_a = [&](int8_t* sa) {
 #pragma unroll

@@ -2,6 +2,7 @@
 # Kernel durations (rocprofv3 kernel trace) of the conv block on selected layer shapes,
 # one process per (shape, TK_ABLATE config): tools/bench_block.py's own event timing
 # includes the host launch path, which hides kernels shorter than ~12 us.
+# Needs the ablation build: python tachikoma_amd/build.py --ablation
 # usage: tools/prof_split.sh <outdir> "<shape filters, ;-separated>" "<ablate flags, space-separated>"
 set -o pipefail
 export TMPDIR=/tmp
@@ -13,7 +14,7 @@ IFS=';' read -ra SH <<< "$SHAPES"
 for sh in "${SH[@]}"; do
   for ab in $FLAGS; do
     tag=$(echo "$sh" | tr -c 'a-zA-Z0-9' '_')_$ab
-    TK_ABLATE=$ab timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$tag" -o run -- \
+    TK_LIB_PATH=tachikoma_amd/_ab/libtachikoma_ablate.so TK_ABLATE=$ab timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$tag" -o run -- \
         python3 tools/bench_block.py '[{}]' "$sh" > "$OUT/$tag.log" 2>&1 || exit 1
   done
 done
