@@ -1270,33 +1270,31 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(const Tx* __restrict__ x, co
   const int tin_bytes = (16 * rows_in * Wp + 15) & ~15;
   int32_t* wts = reinterpret_cast<int32_t*>(dsm + tin_bytes);
   uint8_t* tout = dsm + tin_bytes + 16 * 9 * 4;
-  // ---- stage the band: (channel, input row) rows, lanes along columns (Wp <= 192: 3 column
-  // slots per lane); 8 rows per wave at a time so that 8-24 loads per lane are in flight
-  const uint8_t fillb = (uint8_t)za;
-  const uint8_t* xb = reinterpret_cast<const uint8_t*>(x);
+  // ---- stage the band: (channel, input row) rows of Wp = W + 8 bytes, input column iw at
+  // byte 4 + iw (4-byte aligned interior; the 4-byte halos hold the zero point); one dword
+  // per lane (W % 4 == 0, W <= 248), 8 rows per wave at a time so that 8 loads are in flight
+  const uint32_t fill4 = 0x01010101u * (uint8_t)za;
   const int nrows = 16 * rows_in;
+  const int words = W / 4;
   for (int r0 = wave; r0 < nrows; r0 += 32) {
-    uint8_t v[8][3];
+    uint32_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int r = r0 + 4 * u;
       const int c = r / rows_in, lr = r - c * rows_in;
       const int ih = ih0 + lr;
-      const bool row_ok = r < nrows && ih >= 0 && ih < H;
-      const uint8_t* src = xb + (((int64_t)n * C + c0 + c) * H + (row_ok ? ih : 0)) * W;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int iw = lane + 64 * k - pl;
-        v[u][k] = (row_ok && iw >= 0 && iw < W) ? src[iw] : fillb;
-      }
+      const bool ok = r < nrows && ih >= 0 && ih < H && lane < words;
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(
+          reinterpret_cast<const uint8_t*>(x) + (((int64_t)n * C + c0 + c) * H + (ok ? ih : 0)) * W);
+      v[u] = ok ? src[lane] : fill4;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int r = r0 + 4 * u;
       if (r < nrows) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          if (lane + 64 * k < Wp) tin[r * Wp + lane + 64 * k] = v[u][k];
+        uint32_t* row = reinterpret_cast<uint32_t*>(tin + r * Wp);
+        if (lane < words) row[1 + lane] = v[u];
+        else if (lane == words) row[0] = fill4, row[1 + words] = fill4;
       }
     }
   }
@@ -1325,7 +1323,7 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(const Tx* __restrict__ x, co
         const int32_t wv = wts[c * 9 + r * 3 + s2];
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-          const int32_t a = (int32_t)(Tx)base[(vv * V + e) * sw + s2] - za;
+          const int32_t a = (int32_t)(Tx)base[(vv * V + e) * sw + s2 + 4 - pl] - za;
           acc[e] = (int32_t)((uint32_t)acc[e] + (uint32_t)(a * wv));
         }
       }
@@ -1667,13 +1665,16 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     if (blk && a->groups == g.C && g.C == g.O && g.C % 16 == 0 && g.KH == 3 && g.KW == 3 && a->dilation[0] == 1 &&
         a->dilation[1] == 1 && ((a->strides[0] == 1 && ohw >= 784) || ohw >= 3136) && env_int("TK_DW", 1)) {
       const int sh = a->strides[0], sw = a->strides[1];
-      const int budget = sh == 1 ? 1024 : 512;  // output pixels per workgroup and channel
-      const int BH = g.OH * g.OW <= budget ? g.OH : std::max(1, budget / g.OW);
+      // output pixels per workgroup and channel: whole planes up to 1024 pixels, else bands of
+      // ~512 (stride 1) / ~256 (stride 2) pixels (measured on MobileNetV2's 112x112 and 56x56 layers)
+      const int budget = env_int("TK_DW_BUDGET", sh == 1 ? 512 : 256);
+      const int BH = g.OH * g.OW <= 1024 ? g.OH : std::max(1, budget / g.OW);
       const int bands = (g.OH + BH - 1) / BH;
-      const int Wp = (g.OW - 1) * sw + 3;
+      const int Wp = g.W + 8;  // input row + 4-byte halos (see dw3x3_kernel)
       const int rows_max = (BH - 1) * sh + 3;
       const size_t lds = (size_t)((16 * rows_max * Wp + 15) & ~15) + 16 * 9 * 4 + (size_t)BH * g.OW * 16;
-      if (lds <= 64 * 1024 && Wp <= 192) {
+      const bool fits = g.W % 4 == 0 && g.W <= 248 && a->padding[1] <= 4 && (g.OW - 1) * sw + 2 - a->padding[1] < g.W + 4;
+      if (lds <= 64 * 1024 && fits) {
         const unsigned grid = (unsigned)((int64_t)g.N * (g.C / 16) * bands);
         const bool v4 = g.OW % 4 == 0;
 #define TK_DW(TX, TW)                                                                                              \
