@@ -274,6 +274,42 @@ typedef struct {
 int tk_tachikoma_postops(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* out,
                          const tk_postops_attrs* attrs, void* stream);
 
+/* ---------------------------------------------------------------- relay.quantize-realized graphs
+ * The ops `relay.quantize.quantize` leaves beside the int8 contractions (SURVEY.md §8(f) row 4;
+ * src/relay/quantize/realize.cc:66-160 MulAndDiv / QuantizeRealize, realize.cc:300-345
+ * UnifyDTypeScale): the int32 add / left_shift / right_shift / fixed_point_multiply chain that
+ * moves activations between scales, the float32 input quantize (multiply, round, clip) and
+ * the float32 layers left unquantized.  Realized int8 nn.conv2d / nn.dense run through
+ * tk_qnn_conv2d / tk_qnn_dense with zero zero points; float casts go through tk_cast, float
+ * per-channel adds through tk_bias_add, float pools through tk_max_pool2d /
+ * tk_global_avg_pool2d.  Float contractions accumulate in a fixed order (conv: c, r, s;
+ * dense: k; pool: row-major), one rounding per multiply and add. */
+enum {
+  TK_EW_ADD = 0,                  /* x + rhs (int: wraps) */
+  TK_EW_MULTIPLY = 1,             /* x * rhs (int: wraps) */
+  TK_EW_LEFT_SHIFT = 2,           /* int: x << rhs */
+  TK_EW_RIGHT_SHIFT = 3,          /* int: x >> rhs (arithmetic) */
+  TK_EW_ROUND = 4,                /* float: llvm.round (halves away from zero) */
+  TK_EW_CLIP = 5,                 /* float: min(max(x, lo), hi) */
+  TK_EW_RELU = 6,                 /* max(x, 0) */
+  TK_EW_FIXED_POINT_MULTIPLY = 7, /* int: q_multiply_shift(x, multiplier, 31, shift), int32 result */
+};
+typedef struct {
+  int32_t op;                   /* TK_EW_* */
+  int32_t rhs_kind;             /* 0: unary, 1: scalar (scalar_f / scalar_i), 2: tensor of x's shape */
+  double scalar_f;              /* float32 tensors */
+  int64_t scalar_i;             /* integer tensors */
+  double lo, hi;                /* TK_EW_CLIP */
+  int32_t multiplier, shift;    /* TK_EW_FIXED_POINT_MULTIPLY */
+} tk_ewise_attrs;
+/* Elementwise op of a float32 / int8 / int32 / int64 tensor (topi broadcast ops with a scalar or
+ * same-shape rhs; relay.round; relay.fixed_point_multiply, topi/math.py:644-673). */
+int tk_ewise(const tk_tensor* x, const tk_tensor* rhs, tk_tensor* out, const tk_ewise_attrs* attrs, void* stream);
+/* float32 nn.conv2d NCHW/OIHW (the conv the quantizer skips, skip_conv_layers) and nn.dense. */
+int tk_conv2d_f32(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_conv2d_attrs* attrs,
+                  void* stream);
+int tk_dense_f32(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, void* stream);
+
 /* ---------------------------------------------------------------- executor
  * Native run loop replacing GraphExecutor::Run (graph_executor.cc:61-66) and
  * the debug executor's per-node copy-out (graph_executor_debug.cc:249-284).
@@ -297,6 +333,9 @@ enum {
   TK_NODE_DENSE_BLOCK = 14,/* in: data, weight, bias; outs: 3-4; ext: workspace */
   TK_NODE_ADD_BLOCK = 15,  /* in: lhs, rhs; outs: 1-2 (add, clip); ext[4]: shadow_out */
   TK_NODE_POSTOPS = 16,    /* tachikoma composite post-ops: in: acc int32, [sum_src]; out: dst */
+  TK_NODE_EWISE = 17,      /* in: x, [rhs tensor]; attrs.ewise */
+  TK_NODE_CONV2D_F32 = 18, /* in: data, weight (float32); attrs.conv2d */
+  TK_NODE_DENSE_F32 = 19,  /* in: data, weight (float32) */
 };
 
 #define TK_MAX_NODE_INPUTS 4
@@ -318,6 +357,7 @@ typedef struct {
     tk_block_attrs block;
     tk_add_block_attrs add_block;
     tk_postops_attrs postops;
+    tk_ewise_attrs ewise;
     struct { int64_t a_min, a_max; } clip;
     struct { int32_t axis; } bias_add;
   } attrs;

@@ -123,6 +123,23 @@ class tk_postops_attrs(ctypes.Structure):
     ]
 
 
+class tk_ewise_attrs(ctypes.Structure):
+    _fields_ = [
+        ("op", ctypes.c_int32),
+        ("rhs_kind", ctypes.c_int32),
+        ("scalar_f", ctypes.c_double),
+        ("scalar_i", ctypes.c_int64),
+        ("lo", ctypes.c_double),
+        ("hi", ctypes.c_double),
+        ("multiplier", ctypes.c_int32),
+        ("shift", ctypes.c_int32),
+    ]
+
+
+TK_EW = {"add": 0, "multiply": 1, "left_shift": 2, "right_shift": 3, "round": 4, "clip": 5, "relu": 6,
+         "fixed_point_multiply": 7}
+
+
 class tk_pool2d_attrs(ctypes.Structure):
     _fields_ = [
         ("pool_size", ctypes.c_int32 * 2),
@@ -151,6 +168,7 @@ class tk_node_attrs(ctypes.Union):
         ("block", tk_block_attrs),
         ("add_block", tk_add_block_attrs),
         ("postops", tk_postops_attrs),
+        ("ewise", tk_ewise_attrs),
         ("clip", _clip),
         ("bias_add", _bias_add),
     ]
@@ -187,6 +205,7 @@ NODE_KINDS = {
     "qnn.conv2d": 1, "qnn.dense": 2, "qnn.requantize": 3, "nn.bias_add": 4, "clip": 5, "cast": 6,
     "qnn.add": 7, "nn.max_pool2d": 8, "nn.avg_pool2d": 9, "nn.global_avg_pool2d": 10, "copy": 11, "shadow": 12,
     "conv_block": 13, "dense_block": 14, "add_block": 15, "postops": 16,
+    "ewise": 17, "conv2d_f32": 18, "dense_f32": 19,
 }
 MAX_NODE_INPUTS = 4
 MAX_NODE_OUTPUTS = 6
@@ -229,6 +248,9 @@ SIGNATURES = {
     "tk_global_avg_pool2d": (ctypes.c_int, [_PT, _PT, _VP]),
     "tk_copy": (ctypes.c_int, [_PT, _PT, _VP]),
     "tk_tachikoma_postops": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_postops_attrs), _VP]),
+    "tk_ewise": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_ewise_attrs), _VP]),
+    "tk_conv2d_f32": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_conv2d_attrs), _VP]),
+    "tk_dense_f32": (ctypes.c_int, [_PT, _PT, _PT, _VP]),
     "tk_module_create": (ctypes.c_int, [ctypes.POINTER(tk_node), ctypes.c_int, ctypes.POINTER(_VP)]),
     "tk_module_destroy": (ctypes.c_int, [_VP]),
     "tk_module_num_nodes": (ctypes.c_int, [_VP]),

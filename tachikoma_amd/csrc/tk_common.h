@@ -59,6 +59,9 @@ inline bool is_integer(const tk_tensor* t) {
   return (t->dtype.code == TK_DL_INT || t->dtype.code == TK_DL_UINT) && t->dtype.lanes == 1 &&
          (t->dtype.bits == 8 || t->dtype.bits == 16 || t->dtype.bits == 32 || t->dtype.bits == 64);
 }
+inline bool is_f32(const tk_tensor* t) {
+  return t->dtype.code == TK_DL_FLOAT && t->dtype.bits == 32 && t->dtype.lanes == 1;
+}
 inline bool compact(const tk_tensor* t) { return t->strides == nullptr; }
 
 // dtype id used as a template switch in kernels

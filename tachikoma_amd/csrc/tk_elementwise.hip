@@ -11,6 +11,12 @@
 
 namespace tk {
 
+// float32 variants of the shared ops (relay.quantize-realized graphs, tk_realize.hip)
+int cast_f32_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
+int bias_add_f32_impl(const tk_tensor* x, const tk_tensor* b, tk_tensor* y, int axis, hipStream_t s);
+int global_avg_pool_f32_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
+int max_pool_f32_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s);
+
 constexpr int kBlock = 256;
 
 static inline int grid_for(int64_t work_items) {
@@ -208,6 +214,7 @@ __global__ __launch_bounds__(kBlock) void bias_add_kernel(const T* __restrict__ 
 
 int bias_add_impl(const tk_tensor* x, const tk_tensor* b, tk_tensor* y, int axis, hipStream_t s) {
   TK_CHECK_ARG(x && b && y, "null argument");
+  if (is_f32(x)) return bias_add_f32_impl(x, b, y, axis, s);
   TK_CHECK_ARG(compact(x) && compact(y) && compact(b), "strided tensors are not supported");
   TK_CHECK_ARG(dt_of(x) == dt_of(b) && dt_of(x) == dt_of(y), "dtype mismatch");
   TK_CHECK_ARG(numel(x) == numel(y), "shape mismatch");
@@ -267,7 +274,8 @@ __global__ __launch_bounds__(kBlock) void cast_kernel(const Ti* __restrict__ x, 
 
 int cast_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s) {
   TK_CHECK_ARG(x && y && compact(x) && compact(y) && numel(x) == numel(y), "bad tensors");
-  TK_CHECK_ARG(is_integer(x) && is_integer(y), "integer cast only");
+  if (is_f32(x) || is_f32(y)) return cast_f32_impl(x, y, s);
+  TK_CHECK_ARG(is_integer(x) && is_integer(y), "integer or float32 casts only");
   int64_t n = numel(x);
   return dispatch_int(dt_of(x), [&](auto ti) -> int {
     return dispatch_int(dt_of(y), [&](auto to) -> int {
@@ -446,7 +454,9 @@ static int pool_geom(const tk_tensor* x, const tk_tensor* y, const tk_pool2d_att
 }
 
 int max_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s) {
-  TK_CHECK_ARG(x && y && a && dt_of(x) == dt_of(y), "bad arguments");
+  TK_CHECK_ARG(x && y && a, "bad arguments");
+  if (is_f32(x)) return max_pool_f32_impl(x, y, a, s);
+  TK_CHECK_ARG(dt_of(x) == dt_of(y), "bad arguments");
   PoolGeom g;
   if (pool_geom(x, y, a, &g)) { set_error("tk_max_pool2d: shape mismatch"); return TK_ERR_SHAPE; }
   int64_t n = (int64_t)g.N * g.C * g.OH * g.OW;
@@ -528,7 +538,9 @@ int avg_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hi
 }
 
 int global_avg_pool_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s) {
-  TK_CHECK_ARG(x && y && x->ndim == 4 && y->ndim == 4 && dt_of(x) == dt_of(y), "bad arguments");
+  TK_CHECK_ARG(x && y && x->ndim == 4 && y->ndim == 4, "bad arguments");
+  if (is_f32(x)) return global_avg_pool_f32_impl(x, y, s);
+  TK_CHECK_ARG(dt_of(x) == dt_of(y), "bad arguments");
   TK_CHECK_ARG(y->shape[0] == x->shape[0] && y->shape[1] == x->shape[1] && y->shape[2] == 1 && y->shape[3] == 1,
                "output must be [N,C,1,1]");
   int64_t planes = x->shape[0] * x->shape[1];

@@ -31,6 +31,9 @@ int copy_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
 int postops_impl(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* y, const tk_postops_attrs* a,
                  hipStream_t s);
 int digest_impl(const void* data, int64_t nbytes, uint64_t* out, hipStream_t s);
+int ewise_impl(const tk_tensor* x, const tk_tensor* r, tk_tensor* y, const tk_ewise_attrs* a, hipStream_t s);
+int conv2d_f32_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, const tk_conv2d_attrs* a, hipStream_t s);
+int dense_f32_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, hipStream_t s);
 int64_t conv_packed_weight_bytes(const tk_tensor* weight, int groups);
 int conv_pack_weight(const tk_tensor* weight, int groups, void* packed, int32_t* sums, hipStream_t s);
 int64_t conv_shadow_bytes(const tk_tensor* data);
@@ -123,6 +126,12 @@ static int run_node(Node& n, hipStream_t s) {
       return make_shadow_impl(i0, d.ext[0], s);
     case TK_NODE_POSTOPS:
       return postops_impl(i0, d.n_inputs > 1 ? i1 : nullptr, o, &d.attrs.postops, s);
+    case TK_NODE_EWISE:
+      return ewise_impl(i0, d.n_inputs > 1 ? i1 : nullptr, o, &d.attrs.ewise, s);
+    case TK_NODE_CONV2D_F32:
+      return conv2d_f32_impl(i0, i1, o, &d.attrs.conv2d, s);
+    case TK_NODE_DENSE_F32:
+      return dense_f32_impl(i0, i1, o, s);
   }
   set_error("tk_module: unknown node kind " + std::to_string(d.kind));
   return TK_ERR_INVALID_ARG;
@@ -228,6 +237,16 @@ int tk_copy(const tk_tensor* data, tk_tensor* out, void* stream) {
 int tk_tachikoma_postops(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* out,
                          const tk_postops_attrs* attrs, void* stream) {
   return tk::postops_impl(acc, sum_src, out, attrs, tk::as_stream(stream));
+}
+int tk_ewise(const tk_tensor* x, const tk_tensor* rhs, tk_tensor* out, const tk_ewise_attrs* attrs, void* stream) {
+  return tk::ewise_impl(x, rhs, out, attrs, tk::as_stream(stream));
+}
+int tk_conv2d_f32(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_conv2d_attrs* attrs,
+                  void* stream) {
+  return tk::conv2d_f32_impl(data, weight, out, attrs, tk::as_stream(stream));
+}
+int tk_dense_f32(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, void* stream) {
+  return tk::dense_f32_impl(data, weight, out, tk::as_stream(stream));
 }
 int tk_digest_bytes(const void* data, int64_t nbytes, uint64_t* out_device, void* stream) {
   return tk::digest_impl(data, nbytes, out_device, tk::as_stream(stream));

@@ -22,7 +22,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import numpy as np
 
 from .. import _lib
-from .expr import Call, Constant, Expr, IRModule, Var, post_order
+from .expr import Call, Constant, Expr, Function, IRModule, Var, post_order
 from .op import INT_DTYPES
 
 TARGETS = ("mi355x", "rocm", "hip", "gfx950")
@@ -275,12 +275,55 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
         ins = _tensor_args(call, 2, names)
         nd = len(call.args[0].shape)
         a["axis"] = a["axis"] if a["axis"] >= 0 else nd + a["axis"]
-    elif op == "add":
-        # relay.add of a per-channel vector (relay.op.add validated the broadcast): the same
-        # int32 wrap-around addition as nn.bias_add along axis 1; the record keeps op "add"
+    elif op in ("add", "multiply", "left_shift", "right_shift"):
+        lhs, rhs = call.args
+        if lhs.shape != call.shape:
+            raise UnsupportedError(f"{op}: the lhs must have the output shape ({lhs.shape} vs {call.shape})")
+        nd, rs = len(lhs.shape), tuple(rhs.shape)
+        padded = (1,) * (nd - len(rs)) + rs if len(rs) <= nd else None
+        if isinstance(rhs, Constant) and rhs.data.size == 1:
+            # a scalar operand (the realized graph's rounding bias, shift amounts, scales)
+            ins = _tensor_args(call, 1, names)
+            v = rhs.data.reshape(())
+            a.update(ew=op, rhs_kind=1, relay_op=op,
+                     scalar_f=float(v) if call.dtype == "float32" else 0.0,
+                     scalar_i=int(v) if call.dtype != "float32" else 0)
+            op = "ewise"
+        elif rs == tuple(lhs.shape):
+            ins = _tensor_args(call, 2, names)
+            a.update(ew=op, rhs_kind=2, relay_op=op)
+            op = "ewise"
+        elif op == "add" and nd >= 2 and padded is not None and padded[1] == lhs.shape[1] and \
+                all(d == 1 for i, d in enumerate(padded) if i != 1):
+            # a per-channel vector: the same wrap-around (or float32) addition as nn.bias_add
+            # along axis 1; the record keeps op "add"
+            ins = _tensor_args(call, 2, names)
+            a.update(axis=1, relay_op="add")
+            op = "nn.bias_add"
+        else:
+            raise UnsupportedError(f"{op}: {lhs.shape} with {rs}: scalar, same-shape or (add) per-channel "
+                                   "operands only")
+        if op == "ewise" and call.dtype not in ("float32", "int8", "int32", "int64"):
+            raise UnsupportedError(f"{call.op} on {call.dtype}")
+    elif op in ("round", "fixed_point_multiply"):
+        ins = _tensor_args(call, 1, names)
+        a.update(ew=op, rhs_kind=0, relay_op=op)
+        op = "ewise"
+    elif op in ("nn.conv2d", "nn.dense"):
+        # nn.conv2d / nn.dense of a realized quantized graph (int8 x int8 -> int32, realize.cc:
+        # 147-174, 207-235): the QNN contraction with zero zero points; float32 ones (layers the
+        # quantizer skips) run on the float kernels
         ins = _tensor_args(call, 2, names)
-        a.update(axis=1, relay_op="add")
-        op = "nn.bias_add"
+        dts = (call.args[0].dtype, call.args[1].dtype, call.dtype)
+        if dts == ("float32", "float32", "float32"):
+            pass
+        elif dts[0] in ("int8", "uint8") and dts[1] in ("int8", "uint8") and dts[2] == "int32":
+            a.update(input_zero_point=0, kernel_zero_point=0, input_scale=1.0, kernel_scale=1.0, relay_op=op)
+            op = "qnn." + op.split(".")[1]
+        else:
+            raise UnsupportedError(f"{op} with {dts}: float32 or int8 x int8 -> int32 only")
+        if "groups" not in a and op.endswith("conv2d"):
+            a["groups"] = 1
     elif op in ("tachikoma.qnn.conv2d", "tachikoma.qnn.dense"):
         # a tachikoma BYOC composite (relay/contrib/tachikoma.py): the contraction with zero
         # zero points, then the float32 post-ops whose folded constants ride in the attrs
@@ -292,6 +335,13 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
         consts["postops_o_scl"] = np.asarray(po["o_scl"], np.float32).reshape(-1)
         a.update(act_scl=float(po["act_scl"]), sum_scl=float(po["sum_scl"]), dst_zp=float(po["dst_zp"]),
                  clip_lo=float(po["clip"][0]), clip_hi=float(po["clip"][1]), has_sum=int(len(ins) > 2))
+    elif op in ("clip", "nn.relu") and call.dtype == "float32":
+        ins = _tensor_args(call, 1, names)
+        if op == "clip":
+            a.update(ew="clip", rhs_kind=0, lo=float(a["a_min"]), hi=float(a["a_max"]), relay_op=op)
+        else:
+            a.update(ew="relu", rhs_kind=0, relay_op=op)
+        op = "ewise"
     elif op == "clip":
         ins = _tensor_args(call, 1, names)
         a["lo"] = _clip_bound(a["a_min"], call.dtype)
@@ -300,10 +350,16 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
         ins = _tensor_args(call, 1, names)
         a["lo"] = 0
         a["hi"] = int(np.iinfo(np.dtype(call.dtype)).max)
-    elif op in ("cast", "nn.max_pool2d", "nn.avg_pool2d", "nn.global_avg_pool2d", "nn.batch_flatten", "reshape"):
+    elif op in ("cast", "nn.max_pool2d", "nn.avg_pool2d", "nn.global_avg_pool2d", "nn.batch_flatten", "reshape",
+                "annotation.stop_fusion", "annotation.cast_hint"):
         ins = _tensor_args(call, 1, names)
-        if op == "cast" and (call.args[0].dtype not in INT_DTYPES or call.dtype not in INT_DTYPES):
-            raise UnsupportedError("cast: integer types only")
+        ok = INT_DTYPES + ("float32",)
+        if op == "cast" and (call.args[0].dtype not in ok or call.dtype not in ok):
+            raise UnsupportedError("cast: integer and float32 types only")
+        if op == "nn.avg_pool2d" and call.dtype == "float32":
+            raise UnsupportedError("nn.avg_pool2d: float32 is not on the device path")
+        if op != "cast" and call.dtype not in ok:
+            raise UnsupportedError(f"{op} on {call.dtype}")
     else:
         raise UnsupportedError(f"operator {op} is not on the integer trace path")
     return PlanOp(index, name, op, ins, a, out, consts)
@@ -443,5 +499,38 @@ def build(mod, target: str = "mi355x", params=None, mod_name: str = "default", f
             "the reference's CPU llvm path is not part of it")
     params = {k: np.ascontiguousarray(np.asarray(v.numpy() if hasattr(v, "numpy") else v))
               for k, v in (params or {}).items()}
+    mod, params = lift_constants(mod, params)
     plan = lower(mod, params)
     return ExecutorFactory(plan, params, t, mod_name, fuse=fuse)
+
+
+def lift_constants(mod, params: Dict[str, np.ndarray]):
+    """Tensor-valued constants (the folded weights and biases of a ``relay.quantize`` result)
+    become params named ``_const<k>``, uploaded once like any weight; scalar constants stay in
+    the ops' attributes.  QNN ops' scale / zero-point arguments are left alone."""
+    func = mod["main"] if isinstance(mod, IRModule) else IRModule.from_expr(mod)["main"]
+    params = dict(params)
+    lifted: Dict[int, Var] = {}
+
+    def lift(c: Constant) -> Expr:
+        if id(c) not in lifted:
+            name = f"_const{len(lifted)}"
+            while name in params:
+                name += "_"
+            lifted[id(c)] = Var(name, c.data.shape, str(c.data.dtype))
+            params[name] = np.ascontiguousarray(c.data)
+        return lifted[id(c)]
+
+    new: Dict[int, Expr] = {}
+    for n in post_order(func.body):
+        if not isinstance(n, Call):
+            continue
+        k = 2 if n.op.startswith("qnn.") and n.op != "qnn.requantize" else (1 if n.op == "qnn.requantize" else len(n.args))
+        args = [new.get(id(x), x) for x in n.args]
+        args = [lift(x) if i < k and isinstance(x, Constant) and x.data.size > 1 else x for i, x in enumerate(args)]
+        if any(x is not y for x, y in zip(args, n.args)):
+            new[id(n)] = Call(n.op, args, n.attrs, n.checked_type)
+    if not lifted:
+        return mod, params
+    body = new.get(id(func.body), func.body)
+    return IRModule(Function(list(func.params) + [lifted[k] for k in lifted], body)), params

@@ -254,8 +254,28 @@ class DeviceModule:
                     pa.count_include_pad = int(a.get("count_include_pad", False))
                 elif kind == "nn.global_avg_pool2d":
                     n.kind = _lib.NODE_KINDS[kind]
-                elif kind in ("nn.batch_flatten", "reshape"):
+                elif kind in ("nn.batch_flatten", "reshape", "annotation.stop_fusion", "annotation.cast_hint"):
                     n.kind = _lib.NODE_KINDS["copy"]
+                elif kind == "ewise":
+                    n.kind = _lib.NODE_KINDS["ewise"]
+                    ew = n.attrs.ewise
+                    ew.op = _lib.TK_EW[a["ew"]]
+                    ew.rhs_kind = a["rhs_kind"]
+                    ew.scalar_f = a.get("scalar_f", 0.0)
+                    ew.scalar_i = a.get("scalar_i", 0)
+                    ew.lo = a.get("lo", 0.0)
+                    ew.hi = a.get("hi", 0.0)
+                    ew.multiplier = a.get("multiplier", 0)
+                    ew.shift = a.get("shift", 0)
+                elif kind == "nn.conv2d":  # float32 (int8 ones are lowered to qnn.conv2d)
+                    n.kind = _lib.NODE_KINDS["conv2d_f32"]
+                    ca = n.attrs.conv2d
+                    ca.strides[:] = list(a["strides"])
+                    ca.padding[:] = list(a["padding"])
+                    ca.dilation[:] = list(a["dilation"])
+                    ca.groups = a["groups"]
+                elif kind == "nn.dense":
+                    n.kind = _lib.NODE_KINDS["dense_f32"]
                 else:
                     raise _lib.TachikomaError(f"no device lowering for {kind}")
             n.n_inputs = len(ins)

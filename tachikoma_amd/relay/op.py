@@ -53,17 +53,95 @@ def bias_add(data: Expr, bias: Expr, axis: int = 1) -> Call:
     return Call("nn.bias_add", [data, bias], {"axis": axis}, data.checked_type)
 
 
-def add(lhs: Expr, rhs: Expr) -> Call:
-    """``relay.add`` (python/tvm/relay/op/tensor.py; topi broadcast_add): on the integer trace
-    path the broadcast operand is a per-channel vector along axis 1 (a bias given as [C, 1, 1]
-    or [C], the way frontends and the reference's tachikoma tests write it)."""
+def _broadcast(name: str, lhs: Expr, rhs: Expr) -> TensorType:
+    """Relay's BroadcastRel (src/relay/op/type_relations.cc): numpy broadcasting, equal dtypes."""
     if lhs.dtype != rhs.dtype:
-        raise TypeError("add: dtype mismatch")
-    nd, rs = len(lhs.shape), tuple(rhs.shape)
-    padded = (1,) * (nd - len(rs)) + rs if len(rs) <= nd else None
-    if nd < 2 or padded is None or padded[1] != lhs.shape[1] or any(d != 1 for i, d in enumerate(padded) if i != 1):
-        raise NotImplementedError(f"add: only a per-channel vector broadcast along axis 1 ({lhs.shape} + {rs})")
-    return Call("add", [lhs, rhs], {}, lhs.checked_type)
+        raise TypeError(f"{name}: dtype mismatch {lhs.dtype} vs {rhs.dtype}")
+    try:
+        shape = np.broadcast_shapes(tuple(lhs.shape), tuple(rhs.shape))
+    except ValueError as e:
+        raise TypeError(f"{name}: {lhs.shape} and {rhs.shape} do not broadcast") from e
+    return TensorType(tuple(int(d) for d in shape), lhs.dtype)
+
+
+def add(lhs: Expr, rhs: Expr) -> Call:
+    """``relay.add`` (python/tvm/relay/op/tensor.py; topi broadcast_add), numpy broadcasting.
+    The device runs same-shape, scalar and per-channel-vector (a bias given as [C, 1, 1] or
+    [C], the way frontends and the reference's tachikoma tests write it) operands."""
+    return Call("add", [lhs, rhs], {}, _broadcast("add", lhs, rhs))
+
+
+def multiply(lhs: Expr, rhs: Expr) -> Call:
+    """``relay.multiply`` (topi broadcast_mul)."""
+    return Call("multiply", [lhs, rhs], {}, _broadcast("multiply", lhs, rhs))
+
+
+def right_shift(lhs: Expr, rhs: Expr) -> Call:
+    """``relay.right_shift`` (arithmetic shift for signed types)."""
+    _check_int(lhs, "right_shift")
+    return Call("right_shift", [lhs, rhs], {}, _broadcast("right_shift", lhs, rhs))
+
+
+def left_shift(lhs: Expr, rhs: Expr) -> Call:
+    """``relay.left_shift`` (wraps in the operand type)."""
+    _check_int(lhs, "left_shift")
+    return Call("left_shift", [lhs, rhs], {}, _broadcast("left_shift", lhs, rhs))
+
+
+def round(data: Expr) -> Call:  # noqa: A001  (relay.round)
+    """``relay.round``: llvm.round, halves away from zero."""
+    if data.dtype in INT_DTYPES:
+        raise TypeError("round: float tensor expected")
+    return Call("round", [data], {}, data.checked_type)
+
+
+def fixed_point_multiply(data: Expr, multiplier: int, shift: int) -> Call:
+    """``relay.fixed_point_multiply`` (topi/math.py:644-673 → tir.q_multiply_shift(x, m, 31, s))."""
+    _check_int(data, "fixed_point_multiply")
+    return Call("fixed_point_multiply", [data], {"multiplier": int(multiplier), "shift": int(shift)},
+                data.checked_type)
+
+
+def stop_fusion(data: Expr) -> Call:
+    """``annotation.stop_fusion``: identity that ends a fusion group."""
+    return Call("annotation.stop_fusion", [data], {}, data.checked_type)
+
+
+def cast_hint(data: Expr, dtype: str) -> Call:
+    """``annotation.cast_hint``: identity carrying the dtype the quantizer will cast to."""
+    return Call("annotation.cast_hint", [data], {"dtype": str(np.dtype(dtype))}, data.checked_type)
+
+
+def conv2d(data: Expr, weight: Expr, strides=(1, 1), padding=(0, 0), dilation=(1, 1), groups=1, channels=None,
+           kernel_size=None, data_layout="NCHW", kernel_layout="OIHW", out_layout="", out_dtype="") -> Call:
+    """``relay.nn.conv2d`` (NCHW/OIHW): float32, or int8 x int8 -> out_dtype (the realized
+    quantized graph, realize.cc:147-174)."""
+    if data_layout != "NCHW" or kernel_layout != "OIHW":
+        raise NotImplementedError("nn.conv2d: only NCHW/OIHW layouts are supported")
+    n, c, h, w = data.shape
+    o, cg, kh, kw = weight.shape
+    sh, sw = _tuple2(strides)
+    dh, dw = _tuple2(dilation)
+    pt, pl, pb, pr = get_pad_tuple2d(padding)
+    if c != cg * int(groups) or o % int(groups):
+        raise TypeError(f"nn.conv2d: channels {c} / groups {groups} vs weight {weight.shape}")
+    oh = (h + pt + pb - dh * (kh - 1) - 1) // sh + 1
+    ow = (w + pl + pr - dw * (kw - 1) - 1) // sw + 1
+    odt = str(np.dtype(out_dtype)) if out_dtype else data.dtype
+    attrs = {"strides": (sh, sw), "padding": (pt, pl, pb, pr), "dilation": (dh, dw), "groups": int(groups),
+             "channels": o, "kernel_size": (kh, kw), "data_layout": "NCHW", "kernel_layout": "OIHW",
+             "out_dtype": odt}
+    return Call("nn.conv2d", [data, weight], attrs, TensorType((n, o, oh, ow), odt))
+
+
+def dense(data: Expr, weight: Expr, units=None, out_dtype="") -> Call:
+    """``relay.nn.dense``: data [M, K] x weight [N, K]^T."""
+    m, k = data.shape
+    nn_, k2 = weight.shape
+    if k != k2:
+        raise TypeError(f"nn.dense: {data.shape} x {weight.shape}")
+    odt = str(np.dtype(out_dtype)) if out_dtype else data.dtype
+    return Call("nn.dense", [data, weight], {"units": nn_, "out_dtype": odt}, TensorType((m, nn_), odt))
 
 
 def clip(a: Expr, a_min: float, a_max: float) -> Call:
@@ -94,7 +172,6 @@ def _pool(name, data, pool_size, strides, dilation, padding, layout, ceil_mode, 
         raise NotImplementedError(f"{name}: only NCHW layout is supported")
     if ceil_mode:
         raise NotImplementedError(f"{name}: ceil_mode is not supported")
-    _check_int(data, name)
     kh, kw = _tuple2(pool_size)
     sh, sw = _tuple2(strides)
     dh, dw = _tuple2(dilation)
@@ -111,7 +188,6 @@ def _pool(name, data, pool_size, strides, dilation, padding, layout, ceil_mode, 
 def global_avg_pool2d(data: Expr, layout="NCHW", out_layout="") -> Call:
     if layout != "NCHW":
         raise NotImplementedError("nn.global_avg_pool2d: only NCHW layout is supported")
-    _check_int(data, "nn.global_avg_pool2d")
     n, c, _, _ = data.shape
     return Call("nn.global_avg_pool2d", [data], {"layout": layout}, TensorType((n, c, 1, 1), data.dtype))
 

@@ -315,3 +315,71 @@ def trace_bytes_per_sample(model: Model) -> int:
     plan = lower(model.mod, model.params)
     b = model.input_shape[0]
     return sum(t.nbytes for t in plan.records) // b
+
+
+# ---------------------------------------------------------------- float32 models (relay.quantize input)
+
+@dataclass
+class FloatModel:
+    """A float32 graph for ``relay.quantize.quantize``: the reference's
+    quantizer consumes float Relay graphs with batch norm already folded (SimplifyInference /
+    FoldScaleAxis), i.e. conv -> bias_add -> relu chains."""
+    name: str
+    mod: relay.IRModule
+    params: Dict[str, np.ndarray]
+    input_name: str
+    input_shape: Tuple[int, ...]
+    seed: int
+
+    def random_input(self, seed: Optional[int] = None, batch: Optional[int] = None) -> np.ndarray:
+        rng = np.random.default_rng(self.seed + 1000 if seed is None else seed)
+        shape = list(self.input_shape)
+        if batch is not None:
+            shape[0] = batch
+        return rng.standard_normal(shape).astype(np.float32)
+
+
+def resnet_float(depth: int = 18, batch: int = 1, hw: int = 224, seed: int = 5, classes: int = 1000) -> FloatModel:
+    """torchvision ResNet-18 / ResNet-50 topology in float32 with He-normal weights and small
+    biases (BN folded), seeded; input N(0, 1)."""
+    from .relay import op as _op
+    rng = np.random.default_rng(seed)
+    params: Dict[str, np.ndarray] = {}
+
+    def conv(x, name, cin, cout, k, stride=1, pad=0, relu=True):
+        w = relay.var(name + ".weight", (cout, cin, k, k), "float32")
+        bvar = relay.var(name + ".bias", (cout,), "float32")
+        params[name + ".weight"] = (rng.standard_normal((cout, cin, k, k)) * math.sqrt(2.0 / (cin * k * k))
+                                    ).astype(np.float32)
+        params[name + ".bias"] = (rng.standard_normal(cout) * 0.05).astype(np.float32)
+        y = relay.nn.bias_add(_op.conv2d(x, w, strides=stride, padding=pad), bvar)
+        return relay.nn.relu(y) if relu else y
+
+    x = relay.var("data", (batch, 3, hw, hw), "float32")
+    y = conv(x, "conv1", 3, 64, 7, 2, 3)
+    y = relay.nn.max_pool2d(y, pool_size=(3, 3), strides=(2, 2), padding=(1, 1))
+    cin = 64
+    stages = ((64, 2, 1), (128, 2, 2), (256, 2, 2), (512, 2, 2)) if depth == 18 else \
+        ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
+    for li, (width, blocks, stride) in enumerate(stages):
+        cout = width if depth == 18 else width * 4
+        for bi in range(blocks):
+            s = stride if bi == 0 else 1
+            pre = f"layer{li + 1}.{bi}"
+            if depth == 18:
+                z = conv(y, f"{pre}.conv1", cin, cout, 3, s, 1)
+                z = conv(z, f"{pre}.conv2", cout, cout, 3, 1, 1, relu=False)
+            else:
+                z = conv(y, f"{pre}.conv1", cin, width, 1)
+                z = conv(z, f"{pre}.conv2", width, width, 3, s, 1)
+                z = conv(z, f"{pre}.conv3", width, cout, 1, relu=False)
+            sc = y if (s == 1 and cin == cout) else conv(y, f"{pre}.downsample", cin, cout, 1, s, relu=False)
+            y = relay.nn.relu(_op.add(z, sc))
+            cin = cout
+    y = relay.nn.batch_flatten(relay.nn.global_avg_pool2d(y))
+    wf = relay.var("fc.weight", (classes, cin), "float32")
+    bf = relay.var("fc.bias", (classes,), "float32")
+    params["fc.weight"] = (rng.standard_normal((classes, cin)) / math.sqrt(cin)).astype(np.float32)
+    params["fc.bias"] = (rng.standard_normal(classes) * 0.05).astype(np.float32)
+    y = relay.nn.bias_add(_op.dense(y, wf), bf)
+    return FloatModel(f"resnet{depth}_float", relay.IRModule.from_expr(y), params, "data", (batch, 3, hw, hw), seed)

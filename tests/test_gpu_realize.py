@@ -1,0 +1,82 @@
+"""relay.quantize-realized graphs on the MI355X: every record of the
+trace — integer shift/add/clip chains, int8 contractions, and the float32 ops the quantizer
+leaves (input quantize, the skipped first conv, dequantize, pool, classifier) — bit-exact
+against the oracle (oracle/realize_ref.py fixes the float summation order the kernels use)."""
+import numpy as np
+import pytest
+
+from oracle import graph_ref, realize_ref
+from tachikoma_amd import _lib, relay, zoo
+from tachikoma_amd.contrib import graph_executor
+from tachikoma_amd.relay.quantize import qconfig, quantize
+from tachikoma_amd.trace_format import read_trace
+
+from . import tk_gpu as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(records, expected):
+    for name, exp in expected.items():
+        got = records[name]
+        assert got.shape == exp.shape and got.dtype == exp.dtype, (name, got.shape, exp.shape, got.dtype, exp.dtype)
+        if not np.array_equal(got, exp):
+            idx = tuple(np.argwhere(got != exp)[0])
+            raise AssertionError(f"record {name}: first mismatch at {idx}: {got[idx]} vs {exp[idx]}")
+
+
+@pytest.mark.parametrize("depth,cfg", [(18, {}), (18, {"skip_conv_layers": []}), (18, {"weight_scale": "max"}),
+                                       (50, {})])
+def test_realized_resnet_trace_bit_exact(device, tmp_path, depth, cfg):
+    m = zoo.resnet_float(depth, batch=2, hw=64)
+    with qconfig(**cfg):
+        q = quantize(m.mod, m.params)
+    lib = relay.build(q, target="mi355x")
+    gm = graph_executor.GraphModule(lib["default"]())
+    x = m.random_input()
+    gm.set_input("data", x)
+    path = str(tmp_path / "q.tkt")
+    gm.dump_trace(path)
+    tr = read_trace(path)
+    exp = graph_ref.calibrate(q, {}, {"data": x})
+    assert set(exp) <= set(tr.records)
+    _compare(tr.records, exp)
+
+
+def _ew(x, op, rhs=None, scalar=None, **kw):
+    out = G.empty(x.shape, str(x.dtype))
+    a = _lib.tk_ewise_attrs()
+    a.op = _lib.TK_EW[op]
+    a.rhs_kind = 2 if rhs is not None else (1 if scalar is not None else 0)
+    if scalar is not None:
+        if x.dtype == np.float32:
+            a.scalar_f = float(scalar)
+        else:
+            a.scalar_i = int(scalar)
+    a.lo, a.hi = kw.get("lo", 0.0), kw.get("hi", 0.0)
+    a.multiplier, a.shift = kw.get("multiplier", 0), kw.get("shift", 0)
+    dx = G.dev(x)
+    dr = G.dev(rhs) if rhs is not None else None
+    rc = _lib.load().tk_ewise(G.ref(dx).ptr, G.ref(dr).ptr if dr is not None else None, G.ref(out).ptr,
+                              a, G.stream())
+    G._sync_check(rc, f"tk_ewise {op}")
+    return out.cpu().numpy()
+
+
+def test_ewise_ops_bit_exact(device):
+    rng = np.random.default_rng(11)
+    i32 = rng.integers(-2**31, 2**31, 4099).astype(np.int32)
+    i32[:4] = [2**31 - 1, -2**31, 0, -1]
+    other = rng.integers(-2**31, 2**31, 4099).astype(np.int32)
+    for op, s in (("add", 1 << 20), ("right_shift", 7), ("left_shift", 3), ("multiply", -3)):
+        assert np.array_equal(_ew(i32, op, scalar=s), realize_ref.binary(op, i32, np.int32(s), "int32")), op
+    assert np.array_equal(_ew(i32, "add", rhs=other), realize_ref.binary("add", i32, other, "int32"))
+    f = (rng.standard_normal(4099) * 100).astype(np.float32)
+    f[:6] = [2.5, -2.5, 0.5, -0.5, 1.5, -1.5]
+    assert np.array_equal(_ew(f, "round"), realize_ref.round_away(f))
+    assert np.array_equal(_ew(f, "multiply", scalar=np.float32(1 / 0.0625)), (f * np.float32(16.0)).astype(np.float32))
+    assert np.array_equal(_ew(f, "clip", lo=-127.0, hi=127.0), realize_ref.clip(f, -127.0, 127.0))
+    i64 = rng.integers(-2**31, 2**31, 4099).astype(np.int64)
+    for m_, s_ in ((1518500250, -3), (1395864371, 1), (2**30, -2)):
+        got = _ew(i64, "fixed_point_multiply", multiplier=m_, shift=s_)
+        assert np.array_equal(got, realize_ref.fixed_point_multiply(i64, m_, s_)), (m_, s_)
