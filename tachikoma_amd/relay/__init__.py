@@ -3,11 +3,12 @@
 from . import qnn  # noqa: F401
 from .expr import (Call, Constant, Expr, Function, IRModule, TensorType, Var, const, free_vars,  # noqa: F401
                    post_order, var)
-from .op import (add, avg_pool2d, batch_flatten, bias_add, cast, clip, global_avg_pool2d, max_pool2d,  # noqa: F401
-                 relu, reshape)
+from .op import (add, avg_pool2d, batch_flatten, bias_add, cast, cast_hint, clip, fixed_point_multiply,  # noqa: F401
+                 global_avg_pool2d, left_shift, max_pool2d, multiply, relu, reshape, right_shift, round, stop_fusion)
 from . import op as _op
 from .parser import ParseError, astext, fromtext, parse  # noqa: F401  (tvm.parser.parse / fromtext)
 from . import contrib  # noqa: F401,E402  (relay.op.contrib.tachikoma analogue: contrib.tachikoma)
+from . import quantize  # noqa: F401,E402  (relay.quantize: float32 graph -> integer graph)
 
 
 class _NN:
@@ -17,6 +18,8 @@ class _NN:
     avg_pool2d = staticmethod(_op.avg_pool2d)
     global_avg_pool2d = staticmethod(_op.global_avg_pool2d)
     batch_flatten = staticmethod(_op.batch_flatten)
+    conv2d = staticmethod(_op.conv2d)
+    dense = staticmethod(_op.dense)
 
 
 nn = _NN()
