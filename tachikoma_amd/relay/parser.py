@@ -185,9 +185,27 @@ def _call(op: str, args: List[Expr], attrs: Dict[str, Any]) -> Expr:
             return _op.batch_flatten(*args)
         if op == "reshape":
             return _op.reshape(*args, **a)
+        # float32 graphs and relay.quantize-realized graphs
+        if op == "nn.conv2d":
+            return _op.conv2d(*args, **a)
+        if op == "nn.dense":
+            return _op.dense(*args, **a)
+        if op in ("add", "multiply", "right_shift", "left_shift"):
+            return getattr(_op, op)(*args)
+        if op == "round":
+            return _op.round(*args)
+        if op == "fixed_point_multiply":
+            return _op.fixed_point_multiply(*args, **a)
+        if op == "annotation.stop_fusion":
+            return _op.stop_fusion(*args)
+        if op == "annotation.cast_hint":
+            return _op.cast_hint(*args, **a)
+        if op == "relay.op.annotation.simulated_quantize":
+            from .quantize.passes import simulated_quantize
+            return simulated_quantize(*args, **a)
     except TypeError as e:
         raise ParseError(f"{op}: {e}") from e
-    raise ParseError(f"operator {op} is not in the integer QNN subset")
+    raise ParseError(f"operator {op} is not in the supported subset (QNN, float32 CNN, realized quantized graphs)")
 
 
 class _Parser:

@@ -188,3 +188,21 @@ def test_fold_constant_matches_oracle_ops():
                   ("multiply", np.int32(-7))):
         call = getattr(O, op)(relay.const(a), relay.const(b))
         assert np.array_equal(eval_const_call(call, [a, b]), realize_ref.binary(op, a, b, "int32"))
+
+
+def test_realized_graph_text_round_trip():
+    """IRModule.astext -> relay.parse of a realized graph: same
+    ops, same oracle records."""
+    m = zoo.resnet_float(18, batch=1, hw=32)
+    with qconfig(weight_scale="max"):
+        q = quantize(m.mod, m.params)
+    q2 = relay.parse(q.astext())
+    assert [n.op for n in _calls(q2)] == [n.op for n in _calls(q)]
+    x = m.random_input()
+    r1 = graph_ref.calibrate(q, {}, {"data": x})
+    r2 = graph_ref.calibrate(q2, {}, {"data": x})
+    assert list(r1) == list(r2)
+    for k in r1:
+        assert np.array_equal(r1[k], r2[k]), k
+    f2 = relay.parse(m.mod.astext())  # the float input graph too
+    assert [n.op for n in _calls(f2)] == [n.op for n in _calls(m.mod)]
