@@ -309,6 +309,12 @@ int tk_ewise(const tk_tensor* x, const tk_tensor* rhs, tk_tensor* out, const tk_
 int tk_conv2d_f32(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, const tk_conv2d_attrs* attrs,
                   void* stream);
 int tk_dense_f32(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, void* stream);
+/* relay.quantize kl_divergence calibration, host only (src/relay/quantize/calibrate.cc:35-146
+ * MinimizeKL, called by kl_divergence.py:_find_scale_by_kl): hist = num_bins int32 counts over
+ * float32 edges[num_bins + 1] symmetric about 0; writes the threshold whose 8-bit quantisation
+ * (num_quantized_bins buckets) minimises the KL divergence. */
+int tk_find_scale_by_kl(const int32_t* hist, const float* edges, int num_bins, int num_quantized_bins,
+                        float* threshold);
 
 /* ---------------------------------------------------------------- executor
  * Native run loop replacing GraphExecutor::Run (graph_executor.cc:61-66) and

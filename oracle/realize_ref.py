@@ -174,3 +174,64 @@ def eval_call(call, args):
     if op == "cast":
         return cast(args[0], a["dtype"])
     return None
+
+
+def minimize_kl(hist, edges, num_bins: int, num_quantized_bins: int) -> float:
+    """MinimizeKL (src/relay/quantize/calibrate.cc:35-146) in float32 scalar arithmetic, same
+    operation order — small num_bins only (pure-Python loops)."""
+    F = np.float32
+    zero, half_q = num_bins // 2, num_quantized_bins // 2
+    thr, div = [], []
+
+    def smooth(p, eps=F(0.0001)):
+        zeros = sum(1 for v in p if v == 0)
+        nonz = len(p) - zeros
+        if nonz == 0:
+            return None
+        eps1 = F(eps * F(zeros) / F(nonz))
+        if eps1 >= 1:
+            return None
+        return [F(v + F(eps * F(v == 0)) - F(eps1 * F(v != 0))) for v in p]
+
+    for i in range(half_q, zero + 1):
+        lo, hi = zero - i, zero + i + 1
+        thr.append(F(edges[hi]))
+        ln = hi - lo
+        win = [0] * ln
+        p = [F(0)] * ln
+        for j in range(num_bins):
+            if j <= lo:
+                p[0] = F(p[0] + F(hist[j]))
+            elif j >= hi:
+                p[-1] = F(p[-1] + F(hist[j]))
+            else:
+                win[j - lo] = int(hist[j])
+                p[j - lo] = F(hist[j])
+        per = ln // num_quantized_bins
+        merged = [F(sum(win[j * per:(j + 1) * per])) for j in range(num_quantized_bins)]
+        merged[-1] = F(merged[-1] + F(sum(win[num_quantized_bins * per:])))
+        q = [F(0)] * ln
+        for j in range(num_quantized_bins):
+            a, b = j * per, (ln if j == num_quantized_bins - 1 else (j + 1) * per)
+            nz = sum(1 for k in range(a, b) if win[k] != 0)
+            if nz:
+                for k in range(a, b):
+                    if p[k] != 0:
+                        q[k] = F(merged[j] / F(nz))
+        p, q = smooth(p), smooth(q)
+        if q is None:
+            div.append(F(np.inf))
+            continue
+        p = p or []
+        ps, qs = F(0), F(0)
+        for v in p:
+            ps = F(ps + v)
+        for v in q:
+            qs = F(qs + v)
+        d = F(0)
+        for k in range(len(p)):
+            pk, qk = F(p[k] / ps), F(q[k] / qs)
+            if pk != 0 and qk != 0:
+                d = F(d + F(pk * F(np.log(F(pk / qk)))))
+        div.append(d)
+    return float(thr[int(np.argmin(div))])

@@ -251,6 +251,8 @@ SIGNATURES = {
     "tk_ewise": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_ewise_attrs), _VP]),
     "tk_conv2d_f32": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_conv2d_attrs), _VP]),
     "tk_dense_f32": (ctypes.c_int, [_PT, _PT, _PT, _VP]),
+    "tk_find_scale_by_kl": (ctypes.c_int, [ctypes.POINTER(_I32), ctypes.POINTER(_F32), ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(_F32)]),
     "tk_module_create": (ctypes.c_int, [ctypes.POINTER(tk_node), ctypes.c_int, ctypes.POINTER(_VP)]),
     "tk_module_destroy": (ctypes.c_int, [_VP]),
     "tk_module_num_nodes": (ctypes.c_int, [_VP]),

@@ -22,7 +22,7 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libtachikoma.so")
 ARCH = os.environ.get("TK_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["tk_host.cc", "tk_format.cc", "tk_runtime.cc", "tk_elementwise.hip", "tk_gemm.hip", "tk_residual.hip", "tk_realize.hip"]
+SOURCES = ["tk_host.cc", "tk_calibrate.cc", "tk_format.cc", "tk_runtime.cc", "tk_elementwise.hip", "tk_gemm.hip", "tk_residual.hip", "tk_realize.hip"]
 HEADERS = ["tk_common.h"]
 
 

@@ -391,16 +391,110 @@ def _max_scale(w: np.ndarray) -> float:
     return float(np.amax(np.abs(w)))
 
 
+def stats_profile(mod):
+    """CreateStatsCollector (src/relay/quantize/calibrate.cc:148-190): every simulated_quantize
+    becomes the identity of its input; the inputs of the non-weight ones, in post-order, are the
+    values to profile.  Returns (profile module, the profiled expressions)."""
+    func = mod["main"] if isinstance(mod, IRModule) else mod
+    targets: List[Expr] = []
+
+    def strip(call: Call, args):
+        if call.op == SQ:
+            if call.attrs["kind"] != QAnnotateKind.WEIGHT:
+                assert not isinstance(args[0], Constant)
+                targets.append(args[0])
+            return args[0]
+        return call if all(x is y for x, y in zip(args, call.args)) else _forward(call, args)
+
+    body = rebuild(func.body, strip)
+    return IRModule(Function(_params_of(body, func.params), body)), targets
+
+
+def collect_stats(mod, dataset, chunk_by: int = -1):
+    """_calibrate.py:collect_stats: run the profile graph over the dataset on the MI355X (the
+    engine records every op output, so each profiled value is read back by its record name) and
+    yield, per chunk of layers, the concatenated flattened values."""
+    from ..build_module import build
+    from ...contrib.graph_executor import GraphModule
+    prof, targets = stats_profile(mod)
+    body = prof["main"].body
+    names: Dict[int, str] = {}
+    counter = 0
+    for n in post_order(body):
+        if isinstance(n, Var):
+            names[id(n)] = n.name_hint
+        elif isinstance(n, Call):
+            names[id(n)] = f"%{counter}"
+            counter += 1
+    gm = GraphModule(build(prof, target="mi355x")["default"]())
+    tnames = [names[id(t)] for t in targets]
+    chunk = len(tnames) if chunk_by == -1 else chunk_by
+    for i in range(0, len(tnames), chunk):
+        outs: List[List[np.ndarray]] = [[] for _ in tnames[i:i + chunk]]
+        for batch in dataset:
+            gm.set_input(**batch)
+            gm.run()
+            for j, name in enumerate(tnames[i:i + chunk]):
+                outs[j].append(np.asarray(gm.get_node_output(name).numpy()))
+        yield [np.concatenate(o).reshape(-1) for o in outs]
+
+
+def find_scale_by_percentile(arr: np.ndarray, percentile: float = 0.99999) -> float:
+    """_calibrate.py:_find_scale_by_percentile."""
+    x = np.abs(arr)
+    max_k = int(x.size * percentile)
+    return float(np.partition(x, max_k)[max_k])
+
+
+def find_scale_by_kl(arr: np.ndarray, quantized_dtype: str = "int8", num_bins: int = 8001,
+                     num_quantized_bins: int = 255) -> float:
+    """kl_divergence.py:_find_scale_by_kl: a symmetric histogram of the values, then the native
+    MinimizeKL (tk_find_scale_by_kl, csrc/tk_calibrate.cc)."""
+    import ctypes
+    from ... import _lib
+    arr = np.asarray(arr)
+    min_val, max_val = np.min(arr), np.max(arr)
+    thres = max(abs(min_val), abs(max_val))
+    if min_val >= 0 and quantized_dtype in ["uint8"]:
+        num_quantized_bins = num_quantized_bins * 2 + 1
+    hist, edges = np.histogram(arr, bins=num_bins, range=(-thres, thres))
+    hist = np.ascontiguousarray(hist, np.int32)
+    edges = np.ascontiguousarray(edges, np.float32)
+    out = ctypes.c_float()
+    _lib.check(_lib.load().tk_find_scale_by_kl(hist.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                               edges.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                               num_bins, num_quantized_bins, ctypes.byref(out)),
+               "tk_find_scale_by_kl")
+    return float(out.value)
+
+
+def _dataset_scales(mod, dataset, finder) -> List[float]:
+    if dataset is None:
+        raise ValueError("calibrate: this calibrate_mode needs a dataset (list of {input name: array})")
+    cfg = current_qconfig()
+    scales: List[float] = []
+    for samples in collect_stats(mod, list(dataset), cfg.calibrate_chunk_by):
+        scales += [finder(s) for s in samples]
+    return scales
+
+
 def calibrate(mod, dataset=None) -> IRModule:
     """_calibrate.py:158-238 (``_set_params``): per simulated_quantize,
-    dom_scale = scale / 2^(nbit - sign), clip = +-(2^(nbit - sign) - 1), all float32."""
+    dom_scale = scale / 2^(nbit - sign), clip = +-(2^(nbit - sign) - 1), all float32; the scale
+    is ``global_scale``, or found on the dataset (``kl_divergence``, ``percentile``) for inputs and
+    activations, and ``power2`` / ``max`` of the constant for weights."""
     cfg = current_qconfig()
-    if cfg.calibrate_mode != "global_scale":
-        raise UnsupportedError(f"calibrate_mode={cfg.calibrate_mode}: only global_scale is implemented "
-                               "(kl_divergence/percentile need the float graph run on a dataset)")
     wfunc = {"power2": _power2_scale, "max": _max_scale}.get(cfg.weight_scale)
     if wfunc is None:
         raise ValueError(f"Unknown weight scale mode {cfg.weight_scale}")
+    if cfg.calibrate_mode == "global_scale":
+        dataset_scales = None
+    elif cfg.calibrate_mode == "kl_divergence":
+        dataset_scales = iter(_dataset_scales(mod, dataset, find_scale_by_kl))
+    elif cfg.calibrate_mode == "percentile":
+        dataset_scales = iter(_dataset_scales(mod, dataset, find_scale_by_percentile))
+    else:
+        raise ValueError(f"Unknown calibrate mode {cfg.calibrate_mode}")
     func = mod["main"] if isinstance(mod, IRModule) else mod
 
     def bind(call: Call, args):
@@ -413,7 +507,7 @@ def calibrate(mod, dataset=None) -> IRModule:
                 raise ValueError("calibrate: weight simulated_quantize over a non-constant")
             scale = wfunc(args[0].data)
         else:
-            scale = cfg.global_scale
+            scale = cfg.global_scale if dataset_scales is None else next(dataset_scales)
         consts = [_sconst(scale / valid_range, f32), _sconst(-(valid_range - 1), f32), _sconst(valid_range - 1, f32)]
         return Call(SQ, [args[0]] + consts, call.attrs, call.checked_type)
 
@@ -437,15 +531,13 @@ def _scalar(e: Expr) -> float:
 
 
 def _fixed_point_multiplier_shift(x: float):
-    """GetFixedPointMultiplierShift (src/relay/qnn/utils.cc:33-57) on a double."""
-    if x == 0:
-        return 0, 0
-    m, e = math.frexp(x)
-    q = int(math.floor(abs(m) * (1 << 31) + 0.5)) * (1 if m >= 0 else -1)  # std::round: halves away
-    if q == (1 << 31):
-        q //= 2
-        e += 1
-    return int(q), int(e)
+    """GetFixedPointMultiplierShift (src/relay/qnn/utils.cc:33-57), the library's host port."""
+    import ctypes
+    from ... import _lib
+    m, sh = ctypes.c_int32(), ctypes.c_int32()
+    _lib.check(_lib.load().tk_fixed_point_multiplier_shift(float(x), ctypes.byref(m), ctypes.byref(sh)),
+               "tk_fixed_point_multiplier_shift")
+    return int(m.value), int(sh.value)
 
 
 def _mul_and_div(data: Expr, s1, s2, dtype: str) -> Expr:

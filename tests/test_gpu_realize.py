@@ -80,3 +80,47 @@ def test_ewise_ops_bit_exact(device):
     for m_, s_ in ((1518500250, -3), (1395864371, 1), (2**30, -2)):
         got = _ew(i64, "fixed_point_multiply", multiplier=m_, shift=s_)
         assert np.array_equal(got, realize_ref.fixed_point_multiply(i64, m_, s_)), (m_, s_)
+
+
+@pytest.mark.parametrize("mode", ["kl_divergence", "percentile"])
+def test_dataset_calibration_on_device(device, tmp_path, mode, monkeypatch):
+    """collect_stats runs the profile graph on the MI355X; its statistics (float32 records,
+    bit-exact) give the same per-layer scales as the oracle's run of the same graph, and the
+    realized graph then traces bit-exact."""
+    from tachikoma_amd.relay.quantize import passes
+    m = zoo.resnet_float(18, batch=2, hw=64)
+    data = [{"data": m.random_input(seed=s)} for s in range(2)]
+    with qconfig(calibrate_mode=mode):
+        q = quantize(m.mod, m.params, dataset=data)
+    dev_consts = [n.data for n in relay.post_order(q["main"].body) if isinstance(n, relay.Constant)]
+
+    def oracle_collect(mod, dataset, chunk_by=-1):
+        prof, targets = passes.stats_profile(mod)
+        names, c = {}, 0
+        for n in relay.post_order(prof["main"].body):
+            if isinstance(n, relay.Call):
+                names[id(n)] = f"%{c}"
+                c += 1
+            elif isinstance(n, relay.Var):
+                names[id(n)] = n.name_hint
+        outs = [[] for _ in targets]
+        for batch in dataset:
+            rec = graph_ref.calibrate(prof, {}, batch)
+            for j, t in enumerate(targets):
+                outs[j].append(rec[names[id(t)]])
+        yield [np.concatenate(o).reshape(-1) for o in outs]
+
+    monkeypatch.setattr(passes, "collect_stats", oracle_collect)
+    with qconfig(calibrate_mode=mode):
+        q_ref = quantize(m.mod, m.params, dataset=data)
+    ref_consts = [n.data for n in relay.post_order(q_ref["main"].body) if isinstance(n, relay.Constant)]
+    assert len(dev_consts) == len(ref_consts)
+    for a, b in zip(dev_consts, ref_consts):
+        assert a.dtype == b.dtype and np.array_equal(a, b)
+    lib = relay.build(q, target="mi355x")
+    gm = graph_executor.GraphModule(lib["default"]())
+    x = m.random_input(seed=7)
+    gm.set_input("data", x)
+    path = str(tmp_path / "q.tkt")
+    gm.dump_trace(path)
+    _compare(read_trace(path).records, graph_ref.calibrate(q, {}, {"data": x}))

@@ -166,8 +166,11 @@ def test_unsupported_modes_fail_loudly():
     x = relay.var("data", (1, 4, 8, 8), "float32")
     params = {}
     y = _conv_chain(1, np.random.default_rng(6), params, x)
-    with pytest.raises(UnsupportedError):
+    with pytest.raises(ValueError):
         with qconfig(calibrate_mode="kl_divergence"):
+            quantize(relay.IRModule.from_expr(y), params)  # needs a dataset
+    with pytest.raises(UnsupportedError):
+        with qconfig(partition_conversions="enabled"):
             quantize(relay.IRModule.from_expr(y), params)
     with pytest.raises(AttributeError):
         qconfig(no_such_field=1)
@@ -206,3 +209,69 @@ def test_realized_graph_text_round_trip():
         assert np.array_equal(r1[k], r2[k]), k
     f2 = relay.parse(m.mod.astext())  # the float input graph too
     assert [n.op for n in _calls(f2)] == [n.op for n in _calls(m.mod)]
+
+
+def test_kl_threshold_matches_restatement():
+    """tk_find_scale_by_kl (native MinimizeKL) vs the oracle's scalar float32 restatement."""
+    import ctypes
+    from tachikoma_amd import _lib
+    from tachikoma_amd.relay.quantize.passes import find_scale_by_kl
+    rng = np.random.default_rng(8)
+    for dist in (rng.standard_normal(5000), np.abs(rng.standard_normal(5000)), rng.laplace(size=5000) * 3):
+        arr = dist.astype(np.float32)
+        thres = max(abs(arr.min()), abs(arr.max()))
+        hist, edges = np.histogram(arr, bins=101, range=(-thres, thres))
+        assert edges.dtype == np.float32  # numpy keeps the data's float32 (the C side reads float*)
+        h = np.ascontiguousarray(hist, np.int32)
+        out = ctypes.c_float()
+        _lib.check(_lib.load().tk_find_scale_by_kl(h.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                   edges.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 101, 11,
+                                                   ctypes.byref(out)), "kl")
+        assert np.float32(out.value) == np.float32(realize_ref.minimize_kl(hist, edges, 101, 11))
+        t = find_scale_by_kl(arr)  # full size: 8001 bins, 255 buckets
+        assert 0 < t <= thres * 1.0001
+
+
+def test_percentile_scale():
+    from tachikoma_amd.relay.quantize.passes import find_scale_by_percentile
+    arr = np.arange(-100000, 100000, dtype=np.float32)
+    assert find_scale_by_percentile(arr) == np.sort(np.abs(arr))[int(arr.size * 0.99999)]
+
+
+@pytest.mark.parametrize("mode", ["kl_divergence", "percentile"])
+def test_dataset_calibration_order(monkeypatch, mode):
+    """Dataset modes consume one scale per non-weight simulated_quantize, in post-order (the
+    order collect_stats profiles them); the stats here come from the oracle run of the profile
+    graph (the device run is tests/test_gpu_realize.py)."""
+    from tachikoma_amd.relay.quantize import passes
+    m = zoo.resnet_float(18, batch=1, hw=32)
+    data = [{"data": m.random_input(seed=s)} for s in range(2)]
+
+    def fake_collect(mod, dataset, chunk_by=-1):
+        prof, targets = passes.stats_profile(mod)
+        names, c = {}, 0
+        for n in relay.post_order(prof["main"].body):
+            if isinstance(n, relay.Call):
+                names[id(n)] = f"%{c}"
+                c += 1
+            elif isinstance(n, relay.Var):
+                names[id(n)] = n.name_hint
+        outs = [[] for _ in targets]
+        for batch in dataset:
+            rec = graph_ref.calibrate(prof, {}, batch)
+            for j, t in enumerate(targets):
+                outs[j].append(rec[names[id(t)]])
+        yield [np.concatenate(o).reshape(-1) for o in outs]
+
+    monkeypatch.setattr(passes, "collect_stats", fake_collect)
+    with qconfig(calibrate_mode=mode, skip_conv_layers=[]):
+        q = quantize(m.mod, m.params, dataset=data)
+    with qconfig(calibrate_mode=mode, skip_conv_layers=[], do_simulation=True):
+        s = quantize(m.mod, m.params, dataset=data)
+    sq = [n for n in _calls(s) if n.op == passes.SQ]
+    kinds = [n.attrs["kind"] for n in sq]
+    scales = [float(n.args[1].data) for n in sq]
+    assert len(set(scales)) > 3  # per-layer scales, not one global scale
+    assert any(k != 2 for k in kinds)
+    out = list(graph_ref.calibrate(q, {}, {"data": data[0]["data"]}).values())[-1]
+    assert out.dtype == np.float32 and np.isfinite(out).all()
