@@ -292,6 +292,10 @@ __device__ __forceinline__ void tile_of(const GemmArgs& g, int& mt, int& nt) {
   }
   const int local = L >> 3;
   mt = local % g.mtiles;
+  if (g.xcd_order == 2) {  // contiguous N-tile chunks per XCD (A/B: adjacent tiles share an L2)
+    nt = (L & 7) * (g.ntiles8 >> 3) + local / g.mtiles;
+    return;
+  }
   nt = (local / g.mtiles) * 8 + (L & 7);
 }
 
@@ -1524,9 +1528,14 @@ static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out
   return TK_OK;
 }
 
-static int xcd_order() {
+// Tile order (tile_of): on planes of up to 28x28 outputs, each XCD takes a contiguous run of N
+// tiles, so the int32 record lines two neighbouring tiles share (rows of 784 B or less) are
+// completed in one L2; on larger planes N tiles are striped over the XCDs (the 56x56 stage
+// measured 5-7 % faster striped, the 28/14/7 stages 5-11 % faster chunked,
+// profiles/r01e_ab_xcd_order.txt).  TK_XCD overrides (0 = plain order).
+static int xcd_order(int64_t out_hw) {
   const char* e = getenv("TK_XCD");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : (out_hw <= 784 ? 2 : 1);
 }
 
 static int nt_stores() {
@@ -1653,7 +1662,7 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   ga.ch_is_row = 1;
   ga.ablate = ablate_flags();
   ga.nt = nt_stores();
-  ga.xcd_order = xcd_order();
+  ga.xcd_order = xcd_order((int64_t)g.OH * g.OW);
   int rc = setup_block(ga, blk, out, g.O, 1);
   if (rc) return rc;
   if (!use_mfma_conv(g, a->groups)) {
