@@ -246,27 +246,29 @@ struct ConvF32Geom {
 
 __global__ __launch_bounds__(kEwBlock) void conv2d_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                               float* __restrict__ y, ConvF32Geom g) {
-  const int plane = blockIdx.y;  // n * O + o
-  const int o = plane % g.O, n = plane / g.O;
-  const int og = g.O / g.groups, grp = o / og;
   const int ohw = g.OH * g.OW;
-  for (int p = blockIdx.x * kEwBlock + threadIdx.x; p < ohw; p += gridDim.x * kEwBlock) {
-    const int oh = p / g.OW, ow = p - (p / g.OW) * g.OW;
-    float acc = 0.0f;
-    for (int ci = 0; ci < g.Cg; ++ci) {
-      const float* xp = x + ((int64_t)n * g.C + grp * g.Cg + ci) * g.H * g.W;
-      const float* wp = w + ((int64_t)o * g.Cg + ci) * g.KH * g.KW;
-      for (int r = 0; r < g.KH; ++r) {
-        const int ih = oh * g.sh - g.pt + r * g.dh;
-        for (int s = 0; s < g.KW; ++s) {
-          const int iw = ow * g.sw - g.pl + s * g.dw;
-          const float v = (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) ? xp[ih * g.W + iw] : 0.0f;
-          const float prod = v * wp[r * g.KW + s];
-          acc = acc + prod;
+  const int og = g.O / g.groups;
+  for (int plane = blockIdx.y; plane < g.N * g.O; plane += gridDim.y) {  // n * O + o
+    const int o = plane % g.O, n = plane / g.O;
+    const int grp = o / og;
+    for (int p = blockIdx.x * kEwBlock + threadIdx.x; p < ohw; p += gridDim.x * kEwBlock) {
+      const int oh = p / g.OW, ow = p - (p / g.OW) * g.OW;
+      float acc = 0.0f;
+      for (int ci = 0; ci < g.Cg; ++ci) {
+        const float* xp = x + ((int64_t)n * g.C + grp * g.Cg + ci) * g.H * g.W;
+        const float* wp = w + ((int64_t)o * g.Cg + ci) * g.KH * g.KW;
+        for (int r = 0; r < g.KH; ++r) {
+          const int ih = oh * g.sh - g.pt + r * g.dh;
+          for (int s = 0; s < g.KW; ++s) {
+            const int iw = ow * g.sw - g.pl + s * g.dw;
+            const float v = (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) ? xp[ih * g.W + iw] : 0.0f;
+            const float prod = v * wp[r * g.KW + s];
+            acc = acc + prod;
+          }
         }
       }
+      y[(int64_t)plane * ohw + p] = acc;
     }
-    y[(int64_t)plane * ohw + p] = acc;
   }
 }
 
@@ -285,13 +287,9 @@ int conv2d_f32_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, const 
   TK_CHECK_ARG(g.C == g.Cg * g.groups && g.O % g.groups == 0, "channels / groups mismatch");
   TK_CHECK_ARG(y->shape[0] == g.N && y->shape[1] == g.O && y->shape[2] == g.OH && y->shape[3] == g.OW,
                "output shape mismatch");
-  TK_CHECK_ARG((int64_t)g.N * g.O <= 65535 * 1024, "too many planes");
+  TK_CHECK_ARG((int64_t)g.N * g.O < INT32_MAX && (int64_t)g.OH * g.OW < INT32_MAX, "tensor too large");
   const int ohw = g.OH * g.OW;
-  dim3 grid((unsigned)std::min(ew_grid(ohw), 64), (unsigned)(g.N * g.O));
-  if (grid.y > 65535) {
-    set_error("tk_conv2d_f32: N*O exceeds the grid's y dimension");
-    return TK_ERR_SHAPE;
-  }
+  dim3 grid((unsigned)std::min(ew_grid(ohw), 64), (unsigned)std::min(g.N * g.O, 65535));
   hipLaunchKernelGGL(conv2d_f32_kernel, grid, dim3(kEwBlock), 0, s, (const float*)ptr(x), (const float*)ptr(w),
                      (float*)ptr(y), g);
   TK_LAUNCH_CHECK();

@@ -489,10 +489,13 @@ def calibrate(mod, dataset=None) -> IRModule:
         raise ValueError(f"Unknown weight scale mode {cfg.weight_scale}")
     if cfg.calibrate_mode == "global_scale":
         dataset_scales = None
-    elif cfg.calibrate_mode == "kl_divergence":
-        dataset_scales = iter(_dataset_scales(mod, dataset, find_scale_by_kl))
-    elif cfg.calibrate_mode == "percentile":
-        dataset_scales = iter(_dataset_scales(mod, dataset, find_scale_by_percentile))
+    elif cfg.calibrate_mode in ("kl_divergence", "percentile"):
+        finder = find_scale_by_kl if cfg.calibrate_mode == "kl_divergence" else find_scale_by_percentile
+        found = _dataset_scales(mod, dataset, finder)
+        n_act = len(stats_profile(mod)[1])
+        if len(found) != n_act:
+            raise RuntimeError(f"calibrate: {len(found)} profiled scales for {n_act} activation quantizers")
+        dataset_scales = iter(found)
     else:
         raise ValueError(f"Unknown calibrate mode {cfg.calibrate_mode}")
     func = mod["main"] if isinstance(mod, IRModule) else mod

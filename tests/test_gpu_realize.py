@@ -124,3 +124,27 @@ def test_dataset_calibration_on_device(device, tmp_path, mode, monkeypatch):
     path = str(tmp_path / "q.tkt")
     gm.dump_trace(path)
     _compare(read_trace(path).records, graph_ref.calibrate(q, {}, {"data": x}))
+
+
+@pytest.mark.parametrize("shape", [(64, 3, 2, 2, 1100, 3, 1, 1), (2, 6, 9, 9, 8, 3, 2, 2), (1, 4, 7, 5, 6, 1, 1, 0)])
+def test_conv2d_f32_bit_exact(device, shape):
+    """tk_conv2d_f32 vs the oracle's fixed-order restatement, incl. more (n, o) planes than the
+    grid's y dimension holds (64 x 1100) and a grouped, strided case."""
+    n, c, h, w, o, k, s, p = shape
+    groups = 2 if c % 2 == 0 and o % 2 == 0 and c == 6 else 1
+    rng = np.random.default_rng(12)
+    x = rng.standard_normal((n, c, h, w)).astype(np.float32)
+    wt = rng.standard_normal((o, c // groups, k, k)).astype(np.float32)
+    oh = (h + 2 * p - k) // s + 1
+    ow = (w + 2 * p - k) // s + 1
+    out = G.empty((n, o, oh, ow), "float32")
+    a = _lib.tk_conv2d_attrs()
+    a.strides[:] = [s, s]
+    a.padding[:] = [p, p, p, p]
+    a.dilation[:] = [1, 1]
+    a.groups = groups
+    dx, dw = G.dev(x), G.dev(wt)
+    G._sync_check(_lib.load().tk_conv2d_f32(G.ref(dx).ptr, G.ref(dw).ptr, G.ref(out).ptr, a, G.stream()),
+                  "tk_conv2d_f32")
+    exp = realize_ref.conv2d_f32(x, wt, (s, s), (p, p, p, p), (1, 1), groups)
+    assert np.array_equal(out.cpu().numpy(), exp)
