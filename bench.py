@@ -9,13 +9,22 @@ the complete per-op trace of one sample; value = samples traced by all ranks ÷
 max-over-ranks wall time.  Inputs are resident in HBM before timing starts.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]
-        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+  * N > 1 without torch.distributed.run: this process starts N rank processes (before any
+    GPU call) and exits with their status; with torch.distributed.run (WORLD_SIZE set),
+    WORLD_SIZE must equal --gpus.
+  * --dist-backend gloo rehearses N ranks on one GPU (all ranks share cuda:0).
+
+After the timed region, the trace image is checked record for record against the CPU
+oracle (every record of the CPU baseline's samples at N = 1; the first and last sample of
+every shard at N > 1); any mismatch makes the run exit non-zero.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,13 +36,14 @@ import numpy as np  # noqa: E402
 
 INT8_MFMA_PEAK_OPS = 5.0e15  # gfx950 dense int8 (2x the 2.5 PF dense bf16 peak), MI355X_MICROARCH.md
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (6.3 TB/s measured streaming copy), MI355X_MICROARCH.md
+METRIC = "ResNet-50 int8 op-traces/sec at 1/2/4/8 GPU; bit-exact vs CPU"
 
 
 def _log(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
@@ -43,33 +53,164 @@ def parse():
     p.add_argument("--cpu-budget-s", type=float, default=15.0, help="CPU baseline time budget")
     p.add_argument("--skip-cpu", action="store_true")
     p.add_argument("--sink", choices=["memory", "file"], default="memory",
-                   help="memory: trace image complete in pinned host RAM; file: also write each step to disk")
+                   help="memory: trace image complete in pinned host RAM; file: also write every step's image "
+                        "to trace.rank<r>.tkt, overlapped with the next step (two pinned images, writer thread)")
     p.add_argument("--out-dir", default="/tmp")
     p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse N>1 on one GPU")
-    return p.parse_args()
+    p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
+    return p.parse_args(argv)
 
 
-def cpu_baseline(model_fn, batch_hint: int, budget_s: float):
+# ---------------------------------------------------------------- N-rank launcher
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, cmd) -> int:
+    """`python bench.py --gpus N`: one process per GPU running `cmd`, started before this
+    process touches the GPU (the parent never initialises HIP); rank r gets RANK = LOCAL_RANK
+    = r and a torch.distributed rendezvous on 127.0.0.1.  Rank 0 prints the JSON line; the
+    exit status is the first non-zero rank status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(list(cmd), env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            time.sleep(0.2)
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code and not rc:
+                    rc = code
+                    for q in live:  # one rank failed: the others would block in a collective
+                        q.terminate()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+# ---------------------------------------------------------------- host facts
+
+def cpu_quota() -> float | None:
+    """CPUs granted by the cgroup (cpu.max quota / period), None when unlimited/unknown."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()
+            if q != "max":
+                return int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def d2h_probe(device, nbytes: int = 1 << 30, reps: int = 4) -> float:
+    """Pinned device→host bandwidth (GB/s) of one large hipMemcpyAsync, measured with HIP
+    events on a side stream: the PCIe ceiling the traced steps are compared with."""
+    import torch
+    src = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    src.fill_(1)
+    dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    s = torch.cuda.Stream(device=device)
+    best = 0.0
+    with torch.cuda.stream(s):
+        dst.copy_(src, non_blocking=True)  # warm (page tables, SDMA queue)
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            dst.copy_(src, non_blocking=True)
+            e1.record(s)
+            e1.synchronize()
+            best = max(best, nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    del src, dst
+    return best
+
+
+# ---------------------------------------------------------------- CPU baseline + parity
+
+class Parity:
+    """Record-by-record comparison of the GPU trace image with the CPU oracle's records."""
+
+    def __init__(self, records):
+        self.records = records          # {name: [B_shard, ...]} views into the trace image
+        self.samples = 0
+        self.n_records = 0
+        self.mismatches = 0
+        self.first = None
+
+    def check(self, local_index: int, global_index: int, expected) -> None:
+        self.samples += 1
+        for name, exp in expected.items():
+            self.n_records += 1
+            got = self.records[name][local_index:local_index + 1]
+            if got.shape != exp.shape or got.dtype != exp.dtype or not np.array_equal(got, exp):
+                self.mismatches += 1
+                if self.first is None:
+                    where = None
+                    if got.shape == exp.shape:
+                        bad = np.argwhere(got != exp)[0]
+                        where = {"index": [int(v) for v in bad[1:]], "gpu": int(got[tuple(bad)]),
+                                 "cpu": int(exp[tuple(bad)])}
+                    self.first = {"sample": global_index, "record": name, **(where or {"shape": list(got.shape)})}
+
+    def summary(self) -> dict:
+        return {"samples": self.samples, "records": self.n_records, "mismatches": self.mismatches,
+                "first_mismatch": self.first}
+
+
+def cpu_baseline(model_fn, offset: int, batch: int, budget_s: float, threads: int, parity: Parity):
     """Time the oracle's C restatement (OpenMP port of the reference's int16 conv / int64
-    requantize semantics) doing the same per-op record-and-run on the host cores."""
+    requantize semantics) doing the same per-op record-and-run, one sample at a time, on
+    `threads` host cores; every sample it traces is also checked against the GPU trace."""
     from oracle import graph_ref
-    threads = min(16, len(os.sched_getaffinity(0)))
     model = model_fn(batch=1)
-    x_all = model.sample_inputs(0, batch_hint)
-    # warm (page in weights, OpenMP pool) on one sample, then as many samples as fit the budget
+    one = model.sample_inputs(offset, 1)
     t0 = time.perf_counter()
-    graph_ref.calibrate(model.mod, model.params, {"data": x_all[:1]}, backend="c", threads=threads)
-    one = time.perf_counter() - t0
-    n = max(1, min(batch_hint, int(budget_s / max(one, 1e-3))))
-    t0 = time.perf_counter()
-    for i in range(n):
-        graph_ref.calibrate(model.mod, model.params, {"data": x_all[i:i + 1]}, backend="c", threads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "op-traces/s", "cores": threads, "kind": "port",
-            "sample": f"{n} samples of {model.name} int8 224x224 traced one by one (batch-1 record-and-run, "
-                      f"every op output kept), C/OpenMP oracle, {dt:.1f}s"}
+    rec = graph_ref.calibrate(model.mod, model.params, {"data": one}, backend="c", threads=threads)
+    first = time.perf_counter() - t0  # includes paging in the weights / OpenMP pool start
+    parity.check(0, offset, rec)
+    del rec
+    n = max(1, min(batch - 1, int(budget_s / max(first, 1e-3))))
+    picks = sorted(set(int(round(v)) for v in np.linspace(1, batch - 1, n))) if batch > 1 else []
+    dt = 0.0
+    for i in picks:
+        x = model.sample_inputs(offset + i, 1)
+        t0 = time.perf_counter()
+        rec = graph_ref.calibrate(model.mod, model.params, {"data": x}, backend="c", threads=threads)
+        dt += time.perf_counter() - t0
+        parity.check(i, offset + i, rec)
+        del rec
+    timed = len(picks) or 1
+    if not picks:
+        dt = first
+    return {"value": round(timed / dt, 3), "unit": "op-traces/s", "cores": threads, "kind": "port",
+            "sample": f"{timed} samples of {model.name} int8 224x224 spread over the shard, traced one by one "
+                      f"(batch-1 record-and-run, every op output kept), C/OpenMP oracle on {threads} threads, "
+                      f"{dt:.1f}s timed (first sample excluded as warm-up)"}
 
 
 def pmc_traffic(model: str, batch: int, launches: int):
@@ -85,14 +226,23 @@ def pmc_traffic(model: str, batch: int, launches: int):
     return None, None
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+# ---------------------------------------------------------------- one rank
 
+def main(argv=None) -> int:
+    args = parse(argv)
+    if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
+        return launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] +
+                            (sys.argv[1:] if argv is None else list(argv)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    home_cpus = os.sched_getaffinity(0)
+
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
         if args.dist_backend == "nccl":
             torch.cuda.set_device(local_rank)
@@ -103,13 +253,20 @@ def main():
     device = torch.device("cuda", torch.cuda.current_device())
     coll_dev = device if args.dist_backend == "nccl" else torch.device("cpu")
 
-    from tachikoma_amd import relay, shard, zoo
+    from tachikoma_amd import _lib, relay, shard, zoo
     from tachikoma_amd.contrib import graph_executor
+    from tachikoma_amd.trace_format import read_trace
+
+    # NUMA: this rank's CPUs (and so its pinned trace image) on its GPU's socket
+    placement = {"pci": None, "numa_node": None, "cpus": len(home_cpus), "bound": False}
+    if not args.no_numa_bind:
+        placement = shard.bind_to_gpu_node(device.index)
 
     B = args.batch
     model_fn = zoo.MODELS[args.model]
     model = model_fn(batch=B)
-    _log(f"rank {rank}/{world}: building {args.model} batch {B} on {device}")
+    _log(f"rank {rank}/{world}: building {args.model} batch {B} on {device} "
+         f"(numa node {placement['numa_node']}, {placement['cpus']} cpus)")
     lib = relay.build(model.mod, target="mi355x", params=model.params)
     m = graph_executor.GraphModule(lib["default"](device.index))
     # weak scaling: B samples per GPU; this rank traces samples [offset, offset + B) of the global batch
@@ -117,29 +274,55 @@ def main():
     x = model.sample_inputs(offset, count)
     m.set_input("data", x)
     m.set_trace_meta(model=model.name, sample_offset=offset, rank=rank, world=world, n_samples=count)
-    cap = m.trace_capture()
-    if args.sink == "file":
+    caps = [m.trace_capture()]
+    if args.sink == "file" and not args.no_trace:
+        caps.append(graph_executor.TraceCapture(m.module, m._meta))  # second image: write i while i+1 runs
         os.makedirs(args.out_dir, exist_ok=True)
-    _log(f"trace image {cap.layout.total / 1e9:.2f} GB pinned, {len(m.plan.ops)} ops")
+    image_pages = shard.numa_pages(caps[0].ptr, caps[0].layout.total)
+    _log(f"trace image {caps[0].layout.total / 1e9:.2f} GB pinned x{len(caps)} "
+         f"(pages per node {image_pages}), {len(m.plan.ops)} ops")
     stream = torch.cuda.current_stream(device)
+    path = shard.shard_file(args.out_dir, rank)
+
+    import concurrent.futures
+    writer = concurrent.futures.ThreadPoolExecutor(max_workers=1) if len(caps) > 1 else None
+    pending = [None] * len(caps)
+
+    def write_image(cap):
+        cap.synchronize()
+        cap.write(path)
+
+    def step(i):
+        if args.no_trace:
+            m.run(trace=False)
+            return
+        k = i % len(caps)
+        cap = caps[k]
+        if writer is not None:
+            if pending[k] is not None:
+                pending[k].result()  # the writer is done with this image: it may be overwritten
+            cap.capture_inputs(stream)
+            m.module.run(stream, cap.capture_stream, cap.host_dst)
+            pending[k] = writer.submit(write_image, cap)
+        else:
+            # memory sink: the next run's kernels wait for this run's copies on the device
+            # (tk_module_run's capture event), the host does not block between steps
+            m.run(trace=True)
+
+    def drain():
+        for k, f in enumerate(pending):
+            if f is not None:
+                f.result()
+                pending[k] = None
+        torch.cuda.synchronize(device)  # every stream, the capture streams included
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    def step(i):
-        if args.no_trace:
-            m.run(trace=False)
-            torch.cuda.synchronize(device)
-            return
-        m.run(trace=True)
-        cap.synchronize()
-        if args.sink == "file":
-            cap.write(shard.shard_file(args.out_dir, rank))
-
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize(device)
+    drain()
 
     # ---- timed region: K traced steps
     barrier()
@@ -147,7 +330,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
-    torch.cuda.synchronize(device)
+    drain()
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -157,16 +340,18 @@ def main():
         dist.all_reduce(tc, op=dist.ReduceOp.MAX)
         t = tc
     elapsed_max = float(t.item())
+    if writer is not None:
+        writer.shutdown()
 
     # ---- compute-only steps (no capture): the kernels alone, each node bracketed by HIP
     # events recorded on the stream the node's kernel runs on (tk_module_set_profiling);
     # the roofline below is taken from these, where no D2H copy shares the device
     torch.cuda.synchronize(device)
-    tc = time.perf_counter()
+    tc0 = time.perf_counter()
     for _ in range(args.steps):
         m.run(trace=False)
     torch.cuda.synchronize(device)
-    compute_ms = (time.perf_counter() - tc) / max(args.steps, 1) * 1e3
+    compute_ms = (time.perf_counter() - tc0) / max(args.steps, 1) * 1e3
     m.module.set_profiling(True)
     node_ms = np.zeros(m.module.n_nodes)
     for _ in range(args.steps):
@@ -186,9 +371,8 @@ def main():
         if not recs or m.module.node_kinds[i] not in ("conv_block", "dense_block", "qnn.conv2d", "qnn.dense"):
             continue
         op = ops_by_name[recs[0]]
-        x = m.plan.tensor(op.inputs[0])
+        xin = m.plan.tensor(op.inputs[0])
         w = m.plan.tensor(op.inputs[1])
-        out_elems = int(np.prod(op.out.shape))
         if op.op == "qnn.conv2d":
             o, cg, kh, kw = w.shape
             nb, _, oh, ow = op.out.shape
@@ -198,7 +382,7 @@ def main():
         rec_bytes = sum(ops_by_name[r].out.nbytes for r in recs)
         # a fused residual join also reads the other qnn.add operand
         res_bytes = sum(ops_by_name[r].out.nbytes for r in recs if ops_by_name[r].op == "qnn.add")
-        blk_bytes += x.nbytes + w.nbytes + (4 * op.out.shape[1] if len(recs) > 1 else 0) + rec_bytes + res_bytes
+        blk_bytes += xin.nbytes + w.nbytes + (4 * op.out.shape[1] if len(recs) > 1 else 0) + rec_bytes + res_bytes
         blk_ops += 2.0 * macs
         blk_ms += node_ms[i]
         n_launch += 1
@@ -208,30 +392,68 @@ def main():
     traffic, traffic_src = pmc_traffic(args.model, B, n_launch)
 
     # ---- trace-digest all-gather (RCCL over xGMI): one u64 record digest per rank, computed
-    # on the device over the records of the last traced step (outside the timed region)
+    # on the device over the records of one more traced step (outside the timed region); the
+    # image it leaves is the one checked below
     m.run(trace=not args.no_trace)
-    if not args.no_trace:
-        cap.synchronize()
+    torch.cuda.synchronize(device)
     digests = shard.gather_digests(m.module.records_digest(stream).to(coll_dev))
     if args.sink == "file" and not args.no_trace:
-        path = shard.shard_file(args.out_dir, rank)
-        cap.write(path)
+        caps[0].write(path)
         entries = [shard.ShardEntry(r, *shard.shard_range(B * world, world, r), shard.hex64(d),
                                     shard.shard_file(args.out_dir, r)) for r, d in enumerate(digests)]
         if rank == 0:
             shard.write_manifest(os.path.join(args.out_dir, "trace.manifest.json"), model.name, B * world, entries)
 
+    # ---- PCIe ceiling of this rank, measured in this run
+    d2h_peak = d2h_probe(device)
+    trace_bytes = caps[0].layout.total
+    d2h_achieved = trace_bytes / (elapsed_max / args.steps) / 1e9 if not args.no_trace else 0.0
+
+    # ---- parity: the trace image vs the CPU oracle, record for record
+    parity = Parity(read_trace(caps[0].bytes()).records) if not args.no_trace else None
+    cpu = None
+    quota = cpu_quota()
+    if parity is not None:
+        if world == 1 and not args.skip_cpu:
+            # the CPU baseline runs on every core this process may use (its original affinity,
+            # capped by the cgroup's CPU quota), and checks each sample it traces
+            os.sched_setaffinity(0, home_cpus)
+            threads = len(home_cpus) if quota is None else max(1, min(len(home_cpus), int(quota)))
+            _log(f"cpu baseline (oracle port, {threads} threads) + parity ...")
+            cpu = cpu_baseline(model_fn, offset, count, args.cpu_budget_s, threads, parity)
+        else:
+            from oracle import graph_ref
+            one = model_fn(batch=1)
+            for i in sorted({0, count - 1}):
+                rec = graph_ref.calibrate(one.mod, one.params, {"data": x[i:i + 1]}, backend="c")
+                parity.check(i, offset + i, rec)
+    rank_info = {"rank": rank, "pci": placement["pci"], "numa_node": placement["numa_node"],
+                 "cpus": placement["cpus"], "image_pages_per_node": image_pages,
+                 "d2h": {"achieved_GBps": round(trace_bytes / (elapsed / args.steps) / 1e9, 2),
+                         "measured_peak_GBps": round(d2h_peak, 2),
+                         "frac": round(trace_bytes / (elapsed / args.steps) / 1e9 / d2h_peak, 4)},
+                 "parity": parity.summary() if parity is not None else None}
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank_info)
+    else:
+        ranks = [rank_info]
+
+    rc = 0
     if rank == 0:
         traces = B * world * args.steps
         value = traces / elapsed_max
-        cpu = None
-        if not args.skip_cpu and world == 1:  # reported on rank 0 at N = 1 only
-            _log("cpu baseline (oracle port) ...")
-            cpu = cpu_baseline(model_fn, B, args.cpu_budget_s)
         macs_per_sample = zoo.macs_per_sample(model_fn(batch=1))
-        trace_bytes = cap.layout.total
+        par = None
+        if parity is not None:
+            ps = [r["parity"] for r in ranks]
+            par = {"samples": sum(p["samples"] for p in ps), "records": sum(p["records"] for p in ps),
+                   "mismatches": sum(p["mismatches"] for p in ps),
+                   "first_mismatch": next((p["first_mismatch"] for p in ps if p["first_mismatch"]), None),
+                   "oracle": "oracle/graph_ref.py C backend (reference int16 conv / int64 requantize semantics)"}
+            rc = 1 if par["mismatches"] else 0
         line = {
-            "metric": "ResNet-50 int8 op-traces/sec at 1/2/4/8 GPU; bit-exact vs CPU",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "op-traces/s",
             "n_gpus": world,
@@ -246,7 +468,8 @@ def main():
             "config": {"workload": f"{args.model} int8 224x224, {B} samples per GPU (BASELINE config 4 shard), "
                                    f"full per-op trace to pinned host memory",
                        "model": args.model, "global_batch": B * world, "samples_per_gpu": B, "seq_len": None,
-                       "parallelism": f"batch-shard x{world}", "sink": args.sink},
+                       "parallelism": f"batch-shard x{world}", "sink": args.sink,
+                       "dist_backend": args.dist_backend if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved_bw / 1e9, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved_bw / 1e9 / HBM_PEAK_GBPS, 4),
                          "traffic": None if traffic is None else int(traffic),
@@ -257,8 +480,14 @@ def main():
                          "nodes_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
                          "algorithmic_bytes_per_step": int(blk_bytes),
                          "mfma_tops": round(achieved_ops / 1e12, 1),
-                         "mfma_frac": round(achieved_ops / INT8_MFMA_PEAK_OPS, 4)},
+                         "mfma_frac": round(achieved_ops / INT8_MFMA_PEAK_OPS, 4),
+                         "d2h": {"achieved_GBps": round(d2h_achieved, 2), "measured_peak_GBps": round(d2h_peak, 2),
+                                 "frac": round(d2h_achieved / d2h_peak, 4) if d2h_peak else None,
+                                 "note": "trace image bytes per step / max-over-ranks step time vs a 1 GiB pinned "
+                                         "D2H copy measured on rank 0 in this run"}},
             "cpu_baseline": cpu,
+            "parity": par,
+            "ranks": ranks,
             "extra": {
                 "compute_only_ms_per_step": round(compute_ms, 3),
                 "compute_only_traces_per_s": round(B * world / (compute_ms * 1e-3), 1),
@@ -268,12 +497,20 @@ def main():
                 "macs_per_sample": macs_per_sample,
                 "ops_per_sample": 2 * macs_per_sample,
                 "record_digests": [shard.hex64(d) for d in digests],
+                "library": _lib.build_info(),
+                "host_cpus": {"affinity": len(home_cpus), "cgroup_quota": quota, "os_cpu_count": os.cpu_count()},
             },
         }
         print(json.dumps(line), flush=True)
+        if rc:
+            _log(f"PARITY FAILURE: {par['mismatches']} mismatching records, first {par['first_mismatch']}")
     if world > 1:
+        flag = torch.tensor([rc], dtype=torch.int32, device=coll_dev)
+        dist.broadcast(flag, 0)
+        rc = int(flag.item())
         dist.destroy_process_group()
+    return rc
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -55,6 +55,10 @@ const char* tk_last_error(void);
 /* Library/ABI version (TK_ABI_VERSION) and the offload arch it was built for. */
 int tk_abi_version(void);
 const char* tk_build_arch(void);
+/* Hex digest of the sources the library was compiled from (tachikoma_amd/build.py hashes
+ * csrc/ and include/ and passes it as -DTK_SOURCE_HASH); the Python loader refuses a
+ * library whose digest differs from the tree it is imported from. */
+const char* tk_build_info(void);
 
 /* ---------------------------------------------------------------- tensors */
 /* Layout-identical to DLPack DLDevice / DLDataType / DLTensor. */
@@ -378,8 +382,16 @@ int tk_module_num_nodes(const tk_module* mod);
  * are non-NULL, output k of node i is copied device→host into
  * host_dst[i * TK_MAX_NODE_OUTPUTS + k] (NULL entries are skipped) on
  * capture_stream, the copies gated by an event recorded after node i, so they
- * overlap the following nodes. */
+ * overlap the following nodes.  After the last copy an event is recorded on
+ * capture_stream; every later tk_module_run* call first makes its stream wait on
+ * it, so a run never overwrites buffers the previous traced run is still copying
+ * (the call returns as soon as the work is enqueued, like GraphExecutor::Run on an
+ * asynchronous device). */
 int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst);
+/* Makes `stream` wait for the copies of the last traced run: call before writing any
+ * tensor the module reads (GraphModule.set_input / load_params,
+ * graph_executor.cc:158-166 SetInput) on a stream of your own. */
+int tk_module_wait_capture(tk_module* mod, void* stream);
 /* Runs nodes [begin, end) only (per-op record-and-run, Trace.calibrate analogue). */
 int tk_module_run_range(tk_module* mod, int begin, int end, void* stream);
 /* Runs once with a timing event after every node and returns per-node device time in
@@ -431,7 +443,8 @@ int64_t tk_trace_layout(const char* json, const tk_array_meta* params, int n_par
                         int64_t* record_offsets);
 int tk_trace_write_headers(const char* json, const tk_array_meta* params, int n_params,
                            const tk_array_meta* records, int n_records, void* image, int64_t image_size);
-/* Writes `size` bytes of `image` to `path` (O_TRUNC); large sequential writes. */
+/* Writes `size` bytes of `image` to `path` (O_TRUNC): the file is sized once and up to 8
+ * threads pwrite disjoint ranges of 256 MB or more. */
 int tk_write_file(const char* path, const void* image, int64_t size);
 
 /* ---------------------------------------------------------------- digest

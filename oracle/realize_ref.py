@@ -63,6 +63,21 @@ def clip(x: np.ndarray, a_min: float, a_max: float) -> np.ndarray:
 
 
 def fixed_point_multiply(x: np.ndarray, multiplier: int, shift: int) -> np.ndarray:
+    """relay.fixed_point_multiply → topi fixed_point_multiply (topi/math.py:644-673) →
+    tir.q_multiply_shift legalization (intrin_rule.cc:197-250) in x's dtype: the power-of-two
+    case (m == 1<<30, :223-237) shifts and rounds in x's own dtype (int64 wraps at 64 bits), the
+    general case (QMultiplyShift, :166-195) casts x to int64 (no narrowing) and the result to
+    int32."""
+    if x.dtype == np.int64:
+        u = x.astype(np.uint64)
+        if multiplier == (1 << 30):
+            e = shift - 1
+            if e > 0:
+                return (u << np.uint64(e)).astype(np.int64)
+            k = -e
+            return (u + np.uint64(1 << (k - 1))).astype(np.int64) >> np.int64(k)
+        ls, rs = max(shift, 0), max(-shift, 0)
+        return ref._q_multiply_shift_general(x, np.int64(multiplier), ls, rs, ls != 0).astype(np.int64)
     return ref.q_multiply_shift(x.astype(np.int64), multiplier, shift).astype(x.dtype)
 
 

@@ -29,4 +29,5 @@ def cpu(dev_id: int = 0) -> Device:
 from . import relay  # noqa: E402,F401
 from . import contrib  # noqa: E402,F401
 from . import trace_format  # noqa: E402,F401
+from . import runtime  # noqa: E402,F401  (save_param_dict / load_param_dict / load_module)
 from ._lib import TachikomaError  # noqa: E402,F401

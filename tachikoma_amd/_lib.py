@@ -217,6 +217,7 @@ SIGNATURES = {
     "tk_last_error": (ctypes.c_char_p, []),
     "tk_abi_version": (ctypes.c_int, []),
     "tk_build_arch": (ctypes.c_char_p, []),
+    "tk_build_info": (ctypes.c_char_p, []),
     "tk_fixed_point_multiplier_shift": (ctypes.c_int, [_F64, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     "tk_requantize_prepare": (ctypes.c_int, [ctypes.POINTER(_F32), ctypes.c_int, _F32, ctypes.c_int,
                                              ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(ctypes.c_int)]),
@@ -257,6 +258,7 @@ SIGNATURES = {
     "tk_module_destroy": (ctypes.c_int, [_VP]),
     "tk_module_num_nodes": (ctypes.c_int, [_VP]),
     "tk_module_run": (ctypes.c_int, [_VP, _VP, _VP, ctypes.POINTER(_VP)]),
+    "tk_module_wait_capture": (ctypes.c_int, [_VP, _VP]),
     "tk_module_run_range": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _VP]),
     "tk_module_run_profiled": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_F32)]),
     "tk_module_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
@@ -280,12 +282,16 @@ _LIB: Optional[ctypes.CDLL] = None
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
     """Load the HIP library (fails loudly: there is no fallback path).
 
-    ``TK_LIB_PATH`` substitutes another build of the same library (A/B kernel timing in
-    tools/, one process per build on the same box)."""
+    The library must have been built from the sources of this tree: its ``tk_build_info()``
+    (the source digest compiled in by build.py) is compared with the digest of the in-tree
+    sources, and a stale library is refused.  ``TK_LIB_PATH`` substitutes the ablation build
+    of the same sources (A/B kernel timing in tools/, one process per build on one box); it
+    is announced on stderr and reported by ``build_info()``."""
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = os.environ.get("TK_LIB_PATH", path)
+    override = os.environ.get("TK_LIB_PATH")
+    path = override or path
     if not os.path.exists(path):
         raise TachikomaError(
             f"{path} not found: build it with `python tachikoma_amd/build.py` "
@@ -295,8 +301,23 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    from .build import source_hash
+    built = lib.tk_build_info().decode()
+    want = source_hash()
+    if built.split("+")[0] != want:
+        raise TachikomaError(
+            f"{path} was built from other sources (library {built}, tree {want}): rebuild it with "
+            "`python tachikoma_amd/build.py`")
+    if override:
+        import sys
+        sys.stderr.write(f"[tachikoma] TK_LIB_PATH: using {path} ({built})\n")
     _LIB = lib
     return lib
+
+
+def build_info() -> str:
+    """Source digest (and build flavour) of the loaded library."""
+    return load().tk_build_info().decode()
 
 
 def check(rc: int, what: str = "") -> None:

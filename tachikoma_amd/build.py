@@ -4,10 +4,17 @@ Plain hipcc, no cmake: each translation unit is compiled to an object in
 ``tachikoma_amd/_build/`` (in parallel) and linked into one shared library whose
 exported symbols are exactly the ``extern "C"`` entry points of
 ``include/tachikoma.h``.
+
+Rebuilds are decided by content, not by file times: ``source_hash()`` digests every
+source, header and the compile flags; each object carries a stamp of the digest it was
+built from, and the digest is compiled into the library (``tk_build_info()``), so
+``_lib.load()`` can refuse a library that does not match the tree it is imported from
+(a stale binary pushed to a GPU box).
 """
 from __future__ import annotations
 
 import concurrent.futures
+import hashlib
 import json
 import os
 import re
@@ -20,10 +27,13 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libtachikoma.so")
-ARCH = os.environ.get("TK_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"
 
-SOURCES = ["tk_host.cc", "tk_calibrate.cc", "tk_format.cc", "tk_runtime.cc", "tk_elementwise.hip", "tk_gemm.hip", "tk_residual.hip", "tk_realize.hip"]
+SOURCES = ["tk_host.cc", "tk_calibrate.cc", "tk_format.cc", "tk_runtime.cc", "tk_elementwise.hip", "tk_gemm.hip",
+           "tk_residual.hip", "tk_realize.hip"]
 HEADERS = ["tk_common.h"]
+BASE_FLAGS = ["-std=c++17", "-O3", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-Wall",
+              "-Wno-unused-function"]
 
 
 def _hipcc() -> str:
@@ -33,11 +43,21 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the tachikoma HIP library cannot be built")
 
 
-def _newer(target: str, deps) -> bool:
-    if not os.path.exists(target):
-        return False
-    t = os.path.getmtime(target)
-    return all(os.path.getmtime(d) <= t for d in deps)
+def _hash_inputs():
+    return ([os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS] +
+            [os.path.join(ROOT, "include", "tachikoma.h")])
+
+
+def source_hash() -> str:
+    """Digest of everything the library is compiled from (sources, headers, flags)."""
+    h = hashlib.sha256()
+    h.update(" ".join(BASE_FLAGS).encode())
+    for path in _hash_inputs():
+        h.update(os.path.basename(path).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
 
 
 RESOURCES = os.path.join(BUILD, "kernel_resources.json")
@@ -57,9 +77,7 @@ def _resources(stderr: str):
 
 
 def _compile(src: str, obj: str, extra):
-    hipcc = _hipcc()
-    cmd = [hipcc, "-std=c++17", "-O3", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}",
-           "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function", "-c", src, "-o", obj] + extra
+    cmd = [_hipcc()] + BASE_FLAGS + ["-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj] + extra
     if src.endswith(".cc"):
         cmd[1:1] = ["-x", "hip"]
     else:
@@ -73,37 +91,37 @@ def _compile(src: str, obj: str, extra):
     return _resources(r.stderr)
 
 
-def build_ablation(verbose: bool = True) -> str:
-    """Profiling variant with the main-loop ablation switches compiled in (TK_ABLATE env, see
-    GemmArgs::ablate): tachikoma_amd/_ab/libtachikoma_ablate.so, loaded by the tools through
-    TK_LIB_PATH.  The product library has them compiled out."""
-    out_dir = os.path.join(HERE, "_ab")
-    obj_dir = os.path.join(BUILD, "ablate")
-    os.makedirs(out_dir, exist_ok=True)
+def _stamp(obj: str) -> str:
+    return obj + ".stamp"
+
+
+def _read(path: str) -> str:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return ""
+
+
+def _write(path: str, text: str) -> None:
+    with open(path, "w") as f:
+        f.write(text)
+
+
+def _build_into(obj_dir: str, lib: str, defines, tag: str, force: bool, verbose: bool) -> str:
     os.makedirs(obj_dir, exist_ok=True)
-    objs = []
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    digest = source_hash()
+    build_id = digest + tag
+    if not force and os.path.exists(lib) and _read(_stamp(lib)) == build_id:
+        return lib  # up to date (objects are only consulted when something must be rebuilt)
+    extra = list(defines) + [f'-DTK_SOURCE_HASH="{build_id}"']
+    jobs, objs = [], []
     for s in SOURCES:
         obj = os.path.join(obj_dir, s + ".o")
-        _compile(os.path.join(CSRC, s), obj, ["-DTK_ABLATION_BUILD"])
         objs.append(obj)
-    lib = os.path.join(out_dir, "libtachikoma_ablate.so")
-    subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib] + objs, check=True)
-    if verbose:
-        print(f"[tachikoma] built {lib}")
-    return lib
-
-
-def build(force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(BUILD, exist_ok=True)
-    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "tachikoma.h")]
-    jobs = []
-    objs = []
-    for s in SOURCES:
-        src = os.path.join(CSRC, s)
-        obj = os.path.join(BUILD, s + ".o")
-        objs.append(obj)
-        if force or not _newer(obj, [src] + hdrs + [__file__]):
-            jobs.append((src, obj))
+        if force or not os.path.exists(obj) or _read(_stamp(obj)) != build_id:
+            jobs.append((os.path.join(CSRC, s), obj))
     if jobs:
         workers = min(len(jobs), int(os.environ.get("MAX_JOBS", "8")))
         res = {}
@@ -111,25 +129,42 @@ def build(force: bool = False, verbose: bool = True) -> str:
             with open(RESOURCES) as f:
                 res = json.load(f)
         with concurrent.futures.ThreadPoolExecutor(max_workers=workers) as ex:
-            futs = [(os.path.basename(s), ex.submit(_compile, s, o, [])) for s, o in jobs]
-            for name, f in futs:
+            futs = [(os.path.basename(s), o, ex.submit(_compile, s, o, extra)) for s, o in jobs]
+            for name, o, f in futs:
                 r = f.result()
-                if name.endswith(".hip"):
+                _write(_stamp(o), build_id)
+                if name.endswith(".hip") and not tag:
                     res[name] = r
-        with open(RESOURCES, "w") as f:
-            json.dump(res, f, indent=1, sort_keys=True)
-        # a kernel that spills to scratch (or copies its arguments there) runs several times
-        # slower: fail the build instead of shipping it
-        bad = [k for unit in res.values() for k, v in unit.items() if v.get("ScratchSize", 0)]
-        if bad:
-            raise RuntimeError(f"kernels using scratch memory: {bad[:5]} (see {RESOURCES})")
-    if force or jobs or not _newer(LIB, objs):
-        tmp = LIB + ".tmp"
-        subprocess.run([_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs, check=True)
-        os.replace(tmp, LIB)
+        if not tag:
+            with open(RESOURCES, "w") as f:
+                json.dump(res, f, indent=1, sort_keys=True)
+            # a kernel that spills to scratch (or copies its arguments there) runs several times
+            # slower: fail the build instead of shipping it
+            bad = [k for unit in res.values() for k, v in unit.items() if v.get("ScratchSize", 0)]
+            if bad:
+                raise RuntimeError(f"kernels using scratch memory: {bad[:5]} (see {RESOURCES})")
+    if force or jobs or not os.path.exists(lib) or _read(_stamp(lib)) != build_id:
+        tmp = lib + ".tmp"
+        subprocess.run([_hipcc(), "-shared", "-fPIC", "-pthread", f"--offload-arch={ARCH}", "-o", tmp] + objs,
+                       check=True)
+        os.replace(tmp, lib)
+        _write(_stamp(lib), build_id)
         if verbose:
-            print(f"[tachikoma] built {LIB}")
-    return LIB
+            print(f"[tachikoma] built {lib} ({build_id})")
+    return lib
+
+
+def build_ablation(verbose: bool = True) -> str:
+    """Profiling variant with the kernel-selection and main-loop ablation switches read from
+    the environment (TK_ABLATE, TK_XCD, TK_RING, ...; see tune_env in csrc/tk_gemm.hip):
+    tachikoma_amd/_ab/libtachikoma_ablate.so, loaded by the tools through TK_LIB_PATH.  The
+    product library has them compiled out."""
+    return _build_into(os.path.join(BUILD, "ablate"), os.path.join(HERE, "_ab", "libtachikoma_ablate.so"),
+                       ["-DTK_ABLATION_BUILD"], "+ablation", False, verbose)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    return _build_into(BUILD, LIB, [], "", force, verbose)
 
 
 if __name__ == "__main__":

@@ -61,12 +61,18 @@ class TraceCapture:
         self.image = torch.empty(self.layout.total, dtype=torch.uint8, pin_memory=True)
         self.ptr = self.image.data_ptr()
         self.layout.write_headers(self.ptr, self.layout.total)
-        # params once, from the device copies
-        for (name, shape, dtype), off in zip(params, self.layout.param_offsets):
-            self._host_bytes(off, shape, dtype).copy_(_as_bytes(module.buffers[name]))
+        # params once, from the device copies (again after load_params: refresh_params)
+        self.param_offsets = {p[0]: (off, p[1], p[2]) for p, off in zip(params, self.layout.param_offsets)}
+        self.refresh_params(list(self.param_offsets))
         self.record_offsets = dict(zip([r[0] for r in records], self.layout.record_offsets))
         self.host_dst = module.host_dst_array({n: self.ptr + off for n, off in self.record_offsets.items()})
         self.capture_stream = torch.cuda.Stream(device=module.device)
+
+    def refresh_params(self, names) -> None:
+        """Copy the named params' device buffers into the params section (synchronous)."""
+        for name in names:
+            off, shape, dtype = self.param_offsets[name]
+            self._host_bytes(off, shape, dtype).copy_(_as_bytes(self.module.buffers[name]))
 
     def _host_bytes(self, off: int, shape, dtype: str):
         """Byte view of a payload (NDArray-list payloads are not element-aligned)."""
@@ -121,10 +127,14 @@ class GraphModule:
 
     # -- reference surface -------------------------------------------------
     def set_input(self, key=None, value=None, **params):
+        """graph_executor.py:166-197: ``key`` (name or input index) = ``value`` plus keyword
+        params; every shape is checked before the first write, and the writes wait for the
+        last traced run's copies (tk_module_wait_capture)."""
+        vals = {}
         if key is not None:
-            self.module.set_input(key, value)
-        for k, v in params.items():
-            self.module.set_input(k, v)
+            vals[self.plan.inputs[key].name if isinstance(key, int) else key] = value
+        vals.update(params)
+        self.module.set_inputs(vals)
 
     def run(self, trace: bool = False, **inputs):
         import torch
@@ -157,14 +167,26 @@ class GraphModule:
         return NDArrayView(t)
 
     def load_params(self, params_bytes: bytes) -> None:
-        """``GraphModule.load_params``: an NDArray-list blob (file_utils.cc:184-206)."""
-        for name, arr in tf.parse_ndarray_list(params_bytes).items():
-            if name in self.module.buffers:
-                self.module.set_input(name, arr)
-        raise_if_packed = [o.name for o in self.plan.ops if o.op == "qnn.conv2d"]
-        if raise_if_packed:
-            # packed conv weights were prepared at build time; rebuild to use new weights
-            raise _lib.TachikomaError("load_params after build: rebuild the module (conv weights are pre-packed)")
+        """``GraphModule.load_params`` (python/tvm/contrib/graph_executor.py:318-327 →
+        GraphExecutor::LoadParams, graph_executor.cc:283-291): an NDArray-list blob
+        (file_utils.cc:184-206).  Names that are not graph inputs or params are skipped, like
+        the reference; every other entry must match its buffer's shape and dtype, and all of
+        them are checked before the first buffer is written.  The build-time buffers derived
+        from a param (packed MFMA weights and weight sums) are re-derived on the device, and the
+        params section of the trace image is refreshed."""
+        known = {t.name: t for t in list(self.plan.inputs) + list(self.plan.params)}
+        sel = {}
+        for name, arr in tf.parse_ndarray_list(params_bytes, copy=True).items():
+            t = known.get(name)
+            if t is None:
+                continue
+            if tuple(arr.shape) != tuple(t.shape) or str(arr.dtype) != t.dtype:
+                raise _lib.TachikomaError(f"load_params: {name} is {arr.dtype}{list(arr.shape)}, "
+                                          f"the graph expects {t.dtype}{list(t.shape)}")
+            sel[name] = arr
+        self.module.set_inputs(sel)
+        if self._capture is not None:
+            self._capture.refresh_params([n for n in sel if n in self._capture.param_offsets])
 
     # -- trace / debug surface ---------------------------------------------
     def get_node_output(self, name: str) -> NDArrayView:
@@ -212,9 +234,9 @@ class GraphModule:
         timings = self.profile()
         events, t = [], 0.0
         for name, ms in timings.items():
-            us = ms * 1e3
-            events.append({"name": name, "cat": "Op", "ph": "B", "ts": t * 1e3, "pid": 1, "tid": 1})
-            events.append({"name": name, "cat": "Op", "ph": "E", "ts": (t + us) * 1e3, "pid": 1, "tid": 1})
+            us = ms * 1e3  # Chrome trace "ts" is in microseconds (debug_result.py:151-189)
+            events.append({"name": name, "cat": "Op", "ph": "B", "ts": t, "pid": 1, "tid": 1})
+            events.append({"name": name, "cat": "Op", "ph": "E", "ts": t + us, "pid": 1, "tid": 1})
             t += us
         with open(path, "w") as f:
             json.dump({"traceEvents": events, "displayTimeUnit": "ns"}, f)

@@ -1533,29 +1533,39 @@ static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out
 // completed in one L2; on larger planes N tiles are striped over the XCDs (the 56x56 stage
 // measured 5-7 % faster striped, the 28/14/7 stages 5-11 % faster chunked,
 // profiles/r01e_ab_xcd_order.txt).  TK_XCD overrides (0 = plain order).
+// Kernel-selection switches (TK_XCD, TK_RING, TK_FASTEPI, ...) exist for A/B measurements
+// only: they are read from the environment in the ablation build (build.py --ablation,
+// -DTK_ABLATION_BUILD, loaded by the tools through TK_LIB_PATH).  The product library
+// compiles them to their defaults, so no variable on a box changes what it runs.
+#ifdef TK_ABLATION_BUILD
+static const char* tune_env(const char* name) { return getenv(name); }
+#else
+static const char* tune_env(const char*) { return nullptr; }
+#endif
+
 static int xcd_order(int64_t out_hw) {
-  const char* e = getenv("TK_XCD");
+  const char* e = tune_env("TK_XCD");
   return e ? atoi(e) : (out_hw <= 784 ? 2 : 1);
 }
 
 static int nt_stores() {
-  const char* e = getenv("TK_NT");
+  const char* e = tune_env("TK_NT");
   return e ? atoi(e) : 1;
 }
 
 static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
+  const char* e = tune_env(name);
   return e ? atoi(e) : dflt;
 }
 
 static int ring_depth() {
-  const char* e = getenv("TK_RING");
+  const char* e = tune_env("TK_RING");
   const int r = e ? atoi(e) : 3;
   return r >= 3 && r <= 5 ? r : 3;
 }
 
 static int ablate_flags() {
-  const char* e = getenv("TK_ABLATE");
+  const char* e = tune_env("TK_ABLATE");
   return e ? atoi(e) : 0;
 }
 
@@ -1571,7 +1581,7 @@ struct SplitPlan {
 // operand is staged once for both M halves); plain convs use MT = 2 above 64 channels.
 static bool conv_mt1(const ConvGeom& g, bool block) {
   if (g.O <= 64) return true;
-  if (!block || getenv("TK_MT2")) return false;
+  if (!block || tune_env("TK_MT2")) return false;
   return !(g.O == 128 && g.k_eff >= 512 && env_int("TK_MT2_128", 1));
 }
 
@@ -1599,7 +1609,7 @@ static int64_t conv_ntiles(const ConvGeom& g, int ipt) {
 // 2 workgroups per CU the wide ring's LDS allows hold the whole grid (TK_WIDE_MAX_TILES).
 static bool conv_wide(const ConvGeom& g, bool block, int ipt) {
   if (!block || g.KH * g.KW > 64 || g.cin_pad % 128 != 0 || g.k_pad / kBK < 8 || ring_depth() != 3 ||
-      !env_int("TK_WIDE", 1) || !env_int("TK_UNITAP", 1) || getenv("TK_MT2"))
+      !env_int("TK_WIDE", 1) || !env_int("TK_UNITAP", 1) || tune_env("TK_MT2"))
     return false;
   const int64_t tiles = conv_ntiles(g, ipt) * ((g.O + 63) / 64);
   return tiles <= env_int("TK_WIDE_MAX_TILES", 512);

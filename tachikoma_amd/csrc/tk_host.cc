@@ -16,6 +16,10 @@ extern "C" {
 const char* tk_last_error(void) { return tk::g_last_error.c_str(); }
 int tk_abi_version(void) { return TK_ABI_VERSION; }
 const char* tk_build_arch(void) { return "gfx950"; }
+#ifndef TK_SOURCE_HASH
+#define TK_SOURCE_HASH "unknown"
+#endif
+const char* tk_build_info(void) { return TK_SOURCE_HASH; }
 
 // GetFixedPointMultiplierShift (src/relay/qnn/utils.cc:33-57).
 int tk_fixed_point_multiplier_shift(double multiplier, int32_t* significand, int32_t* shift) {

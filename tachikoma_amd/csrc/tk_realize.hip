@@ -52,15 +52,17 @@ __device__ __forceinline__ T ew_apply(T x, T r, const tk_ewise_attrs& a) {
     if constexpr (OP == TK_EW_RIGHT_SHIFT) return (T)(x >> (r & (sizeof(T) * 8 - 1)));  // arithmetic
     if constexpr (OP == TK_EW_RELU) return x > 0 ? x : (T)0;
     if constexpr (OP == TK_EW_FIXED_POINT_MULTIPLY) {
-      // tir.q_multiply_shift(x, m, 31, s), intrin_rule.cc:166-250 (general form; the power-of-two
-      // special case m == 1<<30 cannot come out of the quantizer's non-power-of-two branch)
+      // tir.q_multiply_shift(x, m, 31, s), intrin_rule.cc:166-250.  The power-of-two special
+      // case m == 1<<30 (:223-237) shifts and rounds in x's own dtype (x << e, or
+      // (x + (1 << (k-1))) >> k, int64 for an int64 x); the general form computes in int64 and
+      // casts the result to int32 (QMultiplyShift, :166-195)
       int64_t v = (int64_t)x;
       const int s = a.shift;
       if (a.multiplier == (1 << 30)) {
         const int e = s - 1;
-        if (e > 0) return (T)(int32_t)((uint32_t)(int32_t)v << e);
+        if (e > 0) return (T)((U)x << e);
         const int k = -e;
-        return (T)(int32_t)((int32_t)((uint32_t)(int32_t)v + (1u << (k - 1))) >> k);
+        return (T)((T)((U)x + ((U)1 << (k - 1))) >> k);
       }
       const int ls = s > 0 ? s : 0, rs = s > 0 ? 0 : -s;
       if (ls) v = (int64_t)((uint64_t)v << ls);

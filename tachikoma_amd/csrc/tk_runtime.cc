@@ -143,13 +143,26 @@ struct tk_module {
   std::vector<tk::Node> nodes;
   std::vector<hipEvent_t> done;  // one per node, recorded after it on the compute stream
   std::vector<hipEvent_t> prof;  // n+1 timing events for run_profiled / profiling mode
+  // Recorded on the capture stream after the last D2H copy of a traced run.  Every later
+  // run (and, through tk_module_wait_capture, every input write) first makes its stream wait
+  // on it: the copies read the module's buffers, so overwriting them before the copies land
+  // would mix two runs in one trace image (write-after-read across streams).
+  hipEvent_t capture_done = nullptr;
+  bool capture_recorded = false;
   bool profiling = false;
   bool have_times = false;
   ~tk_module() {
     for (auto e : done) (void)hipEventDestroy(e);
     for (auto e : prof) (void)hipEventDestroy(e);
+    if (capture_done) (void)hipEventDestroy(capture_done);
   }
 };
+
+// The stream about to write the module's buffers waits for the last traced run's copies.
+static int wait_capture(tk_module* mod, hipStream_t s) {
+  if (mod->capture_recorded) TK_HIP(hipStreamWaitEvent(s, mod->capture_done, 0));
+  return TK_OK;
+}
 
 extern "C" {
 
@@ -304,6 +317,14 @@ int tk_module_create(const tk_node* nodes, int n_nodes, tk_module** out) {
       return TK_ERR_HIP;
     }
   }
+  {
+    hipError_t e = hipEventCreateWithFlags(&mod->capture_done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      mod->capture_done = nullptr;
+      tk::set_error(std::string("tk_module_create: hipEventCreate failed: ") + hipGetErrorString(e));
+      return TK_ERR_HIP;
+    }
+  }
   *out = mod.release();
   return TK_OK;
 }
@@ -353,6 +374,8 @@ int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* cons
   hipStream_t s = tk::as_stream(stream);
   hipStream_t cs = tk::as_stream(capture_stream);
   bool capture = capture_stream && host_dst;
+  int rc0 = wait_capture(mod, s);
+  if (rc0) return rc0;
   if (mod->profiling) TK_HIP(hipEventRecord(mod->prof[0], s));
   for (size_t i = 0; i < mod->nodes.size(); ++i) {
     tk::Node& n = mod->nodes[i];
@@ -375,8 +398,21 @@ int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* cons
       }
     }
   }
+  if (capture) {
+    // the next run / input write waits for these copies (wait_capture)
+    TK_HIP(hipEventRecord(mod->capture_done, cs));
+    mod->capture_recorded = true;
+  }
   mod->have_times = mod->profiling;
   return TK_OK;
+}
+
+int tk_module_wait_capture(tk_module* mod, void* stream) {
+  if (!mod) {
+    tk::set_error("tk_module_wait_capture: null module");
+    return TK_ERR_INVALID_ARG;
+  }
+  return wait_capture(mod, tk::as_stream(stream));
 }
 
 int tk_module_run_range(tk_module* mod, int begin, int end, void* stream) {
@@ -385,6 +421,8 @@ int tk_module_run_range(tk_module* mod, int begin, int end, void* stream) {
     return TK_ERR_INVALID_ARG;
   }
   hipStream_t s = tk::as_stream(stream);
+  int rc0 = wait_capture(mod, s);
+  if (rc0) return rc0;
   for (int i = begin; i < end; ++i) {
     int rc = tk::run_node(mod->nodes[i], s);
     if (rc) return rc;
@@ -401,6 +439,8 @@ int tk_module_run_profiled(tk_module* mod, void* stream, float* node_ms) {
   int rc0 = ensure_prof_events(mod);
   if (rc0) return rc0;
   hipStream_t s = tk::as_stream(stream);
+  rc0 = wait_capture(mod, s);
+  if (rc0) return rc0;
   TK_HIP(hipEventRecord(mod->prof[0], s));
   for (size_t i = 0; i < n; ++i) {
     int rc = tk::run_node(mod->nodes[i], s);

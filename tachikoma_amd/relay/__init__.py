@@ -30,6 +30,17 @@ class analysis:  # noqa: N801  (mirrors relay.analysis)
     post_order = staticmethod(post_order)
 
 
+def save_param_dict(params):
+    """relay.save_param_dict (python/tvm/relay/param_dict.py) → runtime.save_param_dict."""
+    from ..runtime import save_param_dict as _s
+    return _s(params)
+
+
+def load_param_dict(param_bytes):
+    from ..runtime import load_param_dict as _l
+    return _l(param_bytes)
+
+
 def build(mod, target: str = "mi355x", params=None, mod_name: str = "default", fuse: bool = True):
     """``relay.build``: lower a QNN module to the MI355X engine (see build_module.py).
 

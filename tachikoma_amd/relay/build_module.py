@@ -486,6 +486,27 @@ class ExecutorFactory:
     def get_params(self) -> Dict[str, np.ndarray]:
         return dict(self.params)
 
+    def get_graph_json(self) -> str:
+        """The lowered plan as JSON (the graph-JSON role of executor_factory.py:get_graph_json)."""
+        import json
+        from ..runtime import plan_to_json
+        return json.dumps(plan_to_json(self.plan))
+
+    def get_executor_config(self) -> str:
+        return self.get_graph_json()
+
+    def save(self) -> bytes:
+        """SaveToBinary analogue (json_runtime.h:105-135): plan + params + op constants."""
+        from ..runtime import serialize_module
+        return serialize_module(self)
+
+    def export_library(self, path: str) -> str:
+        """executor_factory.py:144-211 analogue: one file that ``runtime.load_module`` reloads
+        without re-lowering (the kernels are the in-tree library)."""
+        with open(path, "wb") as f:
+            f.write(self.save())
+        return path
+
     def _create(self, dev=None):
         from .device_module import DeviceModule
         return DeviceModule(self.plan, self.params, dev, fuse=self.fuse)
@@ -497,6 +518,10 @@ def build(mod, target: str = "mi355x", params=None, mod_name: str = "default", f
         raise UnsupportedError(
             f"target {target!r}: this engine builds for MI355X only ({', '.join(TARGETS)}); "
             "the reference's CPU llvm path is not part of it")
+    if isinstance(params, (bytes, bytearray, memoryview)):
+        # a params blob as written by save_param_dict / SaveParams (file_utils.cc:184-206)
+        from ..runtime import load_param_dict
+        params = load_param_dict(bytes(params))
     params = {k: np.ascontiguousarray(np.asarray(v.numpy() if hasattr(v, "numpy") else v))
               for k, v in (params or {}).items()}
     mod, params = lift_constants(mod, params)

@@ -18,7 +18,7 @@ separate trace record) from one kernel.
 from __future__ import annotations
 
 import ctypes
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 import numpy as np
 
@@ -49,6 +49,9 @@ class DeviceModule:
         self._keep: List[object] = []
         self.node_records: List[List[str]] = []  # tk node index -> record names of its outputs
         self.node_kinds: List[str] = []
+        # param name -> re-derivations of the build-time buffers computed from it (packed MFMA
+        # weights + weight sums), re-run whenever the param's device copy is rewritten
+        self._derived: Dict[str, List[Callable[[int], None]]] = {}
         self.groups = exec_groups(plan, fuse=fuse)
         with torch.cuda.device(self.device):
             self._alloc(params)
@@ -303,9 +306,6 @@ class DeviceModule:
         the conv path's weight packing happens once here instead of padding both operands on
         every run (the dense path's per-call pad_rows kernels).  Records are unchanged (same
         buffers).  Returns False (plain dense block) when the conv would not take MFMA."""
-        import os
-        if os.environ.get("TK_DENSE_CONV", "1") == "0":
-            return False
         m, k = head.out.shape[0], self.plan.tensor(head.inputs[0]).shape[1]
         u = head.out.shape[1]
         x4 = self._view_ref(head.inputs[0], (m, k, 1, 1))
@@ -333,9 +333,7 @@ class DeviceModule:
         emit(sn, "shadow", [])
         packed = self._scratch(self.lib.tk_conv2d_packed_weight_bytes(w4.ptr, 1))
         sums = self._scratch(((u + 127) // 128 * 128) * 4)
-        _lib.check(self.lib.tk_conv2d_pack_weight(w4.ptr, 1, ctypes.c_void_p(packed.data_ptr()),
-                                                  ctypes.c_void_p(sums.data_ptr()), ctypes.c_void_p(stream)),
-                   f"{head.name} pack weight")
+        self._pack(head.inputs[1], head.name, w4, packed, sums, stream)
         n.kind = _lib.NODE_KINDS["conv_block"]
         n.ext[0], n.ext[1], n.ext[2] = shadow.data_ptr(), packed.data_ptr(), sums.data_ptr()
         nbytes = self.lib.tk_conv2d_scratch_bytes(x4.ptr, w4.ptr, ctypes.byref(ca), 1)
@@ -393,6 +391,16 @@ class DeviceModule:
         p.outputs[0] = self._ref(op.name).ptr
         emit(p, op.op, [op.name])
 
+    def _pack(self, param: str, what: str, weight: _lib.TensorRef, packed, sums, stream) -> None:
+        """Pack an MFMA conv weight (and its per-channel sums) now, and register the packing
+        so that rewriting ``param`` (set_input / load_params) re-derives both."""
+        def pack(s: int) -> None:
+            _lib.check(self.lib.tk_conv2d_pack_weight(weight.ptr, 1, ctypes.c_void_p(packed.data_ptr()),
+                                                      ctypes.c_void_p(sums.data_ptr()), ctypes.c_void_p(s)),
+                       f"{what} pack weight")
+        pack(stream)
+        self._derived.setdefault(param, []).append(pack)
+
     def _prep_conv(self, n, op: PlanOp, ins, is_mfma: bool, shadow_bufs, ensure_shadow, stream):
         """MFMA path: shadow of the input + packed weight + weight sums (+ scratch: patch sums,
         split-K partial tiles)."""
@@ -402,9 +410,7 @@ class DeviceModule:
         packed = self._scratch(self.lib.tk_conv2d_packed_weight_bytes(ins[1].ptr, 1))
         o = op.out.shape[1]
         sums = self._scratch(((o + 127) // 128 * 128) * 4)
-        _lib.check(self.lib.tk_conv2d_pack_weight(ins[1].ptr, 1, ctypes.c_void_p(packed.data_ptr()),
-                                                  ctypes.c_void_p(sums.data_ptr()), ctypes.c_void_p(stream)),
-                   f"{op.name} pack weight")
+        self._pack(op.inputs[1], op.name, ins[1], packed, sums, stream)
         n.ext[0] = shadow_bufs[op.inputs[0]].data_ptr()
         n.ext[1] = packed.data_ptr()
         n.ext[2] = sums.data_ptr()
@@ -426,16 +432,56 @@ class DeviceModule:
             self.handle = None
 
     # ------------------------------------------------------------ execution
-    def set_input(self, name: str, value) -> None:
+    def _check_value(self, name: str, value):
+        """(host array or device tensor) of ``value`` for buffer ``name``; raises on a shape
+        mismatch before anything is written."""
         torch = _torch()
+        if name not in self.buffers:
+            raise KeyError(f"set_input: {name} is not an input or param of the graph")
         buf = self.buffers[name]
         if isinstance(value, torch.Tensor):
-            buf.copy_(value.to(buf.dtype).reshape(buf.shape), non_blocking=True)
+            if value.numel() != buf.numel():
+                raise ValueError(f"set_input {name}: {tuple(value.shape)} vs {tuple(buf.shape)}")
+            return value
+        v = np.asarray(value.numpy() if hasattr(value, "numpy") else value)
+        if tuple(v.shape) != tuple(buf.shape):
+            raise ValueError(f"set_input {name}: shape {v.shape} vs {tuple(buf.shape)}")
+        return v
+
+    def set_input(self, name: str, value) -> None:
+        """GraphExecutor::SetInput (graph_executor.cc:158-166): copy into the module's buffer on
+        the current stream, after the last traced run's copies have read it; a param feeding a
+        packed MFMA weight is re-packed."""
+        self._write(name, self._check_value(name, value))
+        self._rederive([name])
+
+    def set_inputs(self, values: Dict[str, object]) -> None:
+        """Several buffers at once, every shape checked before the first write."""
+        checked = {k: self._check_value(k, v) for k, v in values.items()}
+        for k, v in checked.items():
+            self._write(k, v)
+        self._rederive(list(checked))
+
+    def _write(self, name: str, v) -> None:
+        torch = _torch()
+        buf = self.buffers[name]
+        s = torch.cuda.current_stream(self.device)
+        self.wait_capture(s)
+        if isinstance(v, torch.Tensor):
+            buf.copy_(v.to(buf.dtype).reshape(buf.shape), non_blocking=True)
         else:
-            v = np.asarray(value.numpy() if hasattr(value, "numpy") else value)
-            if tuple(v.shape) != tuple(buf.shape):
-                raise ValueError(f"set_input {name}: shape {v.shape} vs {tuple(buf.shape)}")
             buf.copy_(torch.from_numpy(np.ascontiguousarray(v.astype(np.dtype(str(buf.dtype).replace("torch.", ""))))))
+
+    def _rederive(self, names: List[str]) -> None:
+        s = _lib.stream_handle(_torch().cuda.current_stream(self.device))
+        for name in names:
+            for fn in self._derived.get(name, []):
+                fn(s)
+
+    def wait_capture(self, stream=None) -> None:
+        """Make ``stream`` wait for the last traced run's D2H copies (tk_module_wait_capture)."""
+        _lib.check(self.lib.tk_module_wait_capture(self.handle, ctypes.c_void_p(_lib.stream_handle(stream))),
+                   "tk_module_wait_capture")
 
     def host_dst_array(self, record_ptrs: Dict[str, int]):
         """Per node × output slot host pointers for tk_module_run (NULL = not captured)."""

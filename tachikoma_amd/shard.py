@@ -99,3 +99,93 @@ def read_manifest(path: str) -> dict:
 
 def hex64(v: int) -> str:
     return f"{v & 0xFFFFFFFFFFFFFFFF:016x}"
+
+
+# ---------------------------------------------------------------- host placement
+# Each rank pins a whole shard image (7.45 GB for ResNet-50 at 64 samples) that its GPU
+# writes at PCIe rate; at 8 GPUs that is ~450 GB/s of host writes, so every image must sit
+# in the DRAM of its GPU's own socket.  The rank binds itself to the CPUs of the GPU's NUMA
+# node before allocating (pinned pages are placed by the allocating thread's node under the
+# default local policy) and reports where the pages landed.
+
+def gpu_pci_address(device_index: int) -> Optional[str]:
+    """PCI address (domain:bus:device.function) of a visible GPU, from the HIP runtime."""
+    import torch
+    p = torch.cuda.get_device_properties(device_index)
+    try:
+        return f"{int(p.pci_domain_id):04x}:{int(p.pci_bus_id):02x}:{int(p.pci_device_id):02x}.0"
+    except AttributeError:
+        return None
+
+
+def pci_numa_node(pci: Optional[str]) -> Optional[int]:
+    if not pci:
+        return None
+    try:
+        with open(f"/sys/bus/pci/devices/{pci}/numa_node") as f:
+            node = int(f.read().strip())
+    except (OSError, ValueError):
+        return None
+    return node if node >= 0 else None
+
+
+def _parse_cpulist(text: str) -> List[int]:
+    cpus: List[int] = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.extend(range(int(a), int(b) + 1))
+        else:
+            cpus.append(int(part))
+    return cpus
+
+
+def node_cpus(node: int) -> List[int]:
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            return _parse_cpulist(f.read())
+    except OSError:
+        return []
+
+
+def bind_to_gpu_node(device_index: int) -> dict:
+    """Restrict this process to the CPUs of the GPU's NUMA node (intersected with the current
+    affinity).  Returns {"pci", "numa_node", "cpus", "bound"}; nothing changes when the node
+    or its CPU list cannot be read."""
+    pci = gpu_pci_address(device_index)
+    node = pci_numa_node(pci)
+    info = {"pci": pci, "numa_node": node, "cpus": len(os.sched_getaffinity(0)), "bound": False}
+    if node is None:
+        return info
+    cpus = set(node_cpus(node)) & set(os.sched_getaffinity(0))
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+        info.update(cpus=len(cpus), bound=True)
+    return info
+
+
+def numa_pages(ptr: int, nbytes: int) -> Optional[dict]:
+    """{node: pages} of the mappings overlapping [ptr, ptr + nbytes) from /proc/self/numa_maps
+    (None where the kernel does not expose it)."""
+    try:
+        with open("/proc/self/maps") as f:
+            ranges = {}
+            for line in f:
+                lo, hi = (int(x, 16) for x in line.split()[0].split("-"))
+                if lo < ptr + nbytes and hi > ptr:
+                    ranges[lo] = hi
+        out: dict = {}
+        with open("/proc/self/numa_maps") as f:
+            for line in f:
+                fields = line.split()
+                if int(fields[0], 16) not in ranges:
+                    continue
+                for fld in fields[1:]:
+                    if fld.startswith("N") and "=" in fld:
+                        k, v = fld[1:].split("=")
+                        out[int(k)] = out.get(int(k), 0) + int(v)
+        return out or None
+    except (OSError, ValueError):
+        return None

@@ -1,0 +1,70 @@
+"""Host logic of bench.py that needs no GPU: the N-rank self-launcher (`python bench.py --gpus
+N` must start N ranks, not one), the record-by-record parity checker, host placement helpers,
+and a 2-rank gloo rendezvous through the launcher's environment."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import bench
+from tachikoma_amd import shard
+
+
+def test_launcher_starts_n_ranks(tmp_path):
+    out = tmp_path / "ranks"
+    out.mkdir()
+    code = ("import json, os, sys; d = {k: os.environ[k] for k in "
+            "('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')}; "
+            f"open(os.path.join({str(out)!r}, 'r' + d['RANK']), 'w').write(json.dumps(d))")
+    assert bench.launch_ranks(3, [sys.executable, "-c", code]) == 0
+    docs = [json.loads((out / f"r{r}").read_text()) for r in range(3)]
+    assert [d["RANK"] for d in docs] == ["0", "1", "2"]
+    assert all(d["WORLD_SIZE"] == "3" and d["MASTER_ADDR"] == "127.0.0.1" for d in docs)
+    assert len({d["MASTER_PORT"] for d in docs}) == 1
+
+
+def test_launcher_propagates_failure():
+    code = "import os, sys, time; r = int(os.environ['RANK']); sys.exit(7) if r == 1 else time.sleep(60)"
+    assert bench.launch_ranks(2, [sys.executable, "-c", code]) == 7  # rank 0 is terminated, not waited for
+
+
+def test_launcher_gloo_rendezvous(tmp_path):
+    """The launched ranks form a torch.distributed group (gloo on CPU, world 2)."""
+    out = tmp_path / "sum"
+    code = ("import os, torch, torch.distributed as dist; dist.init_process_group('gloo'); "
+            "t = torch.tensor([dist.get_rank() + 1]); dist.all_reduce(t); "
+            f"open({str(out)!r} + os.environ['RANK'], 'w').write(str(int(t)))")
+    assert bench.launch_ranks(2, [sys.executable, "-c", code]) == 0
+    assert [open(f"{out}{r}").read() for r in range(2)] == ["3", "3"]
+
+
+def test_world_size_must_match_gpus(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit, match="WORLD_SIZE=2 but --gpus 4"):
+        bench.main(["--gpus", "4"])
+
+
+def test_parity_checker():
+    rec = {"data": np.arange(12, dtype=np.int8).reshape(3, 4), "%0": np.arange(6, dtype=np.int32).reshape(3, 2)}
+    p = bench.Parity(rec)
+    p.check(1, 101, {"data": rec["data"][1:2].copy(), "%0": rec["%0"][1:2].copy()})
+    assert p.summary() == {"samples": 1, "records": 2, "mismatches": 0, "first_mismatch": None}
+    bad = rec["%0"][2:3].copy()
+    bad[0, 1] += 1
+    p.check(2, 102, {"%0": bad})
+    s = p.summary()
+    assert s["mismatches"] == 1 and s["first_mismatch"] == {"sample": 102, "record": "%0", "index": [1],
+                                                            "gpu": 5, "cpu": 6}
+
+
+def test_host_placement_helpers():
+    assert shard._parse_cpulist("0-2,5,7-8\n") == [0, 1, 2, 5, 7, 8]
+    assert shard.pci_numa_node(None) is None
+    assert shard.pci_numa_node("ffff:ff:1f.7") is None
+    a = np.ones(1 << 24, np.uint8)
+    pages = shard.numa_pages(a.ctypes.data, a.nbytes)
+    assert pages is None or sum(pages.values()) >= (1 << 24) // 4096
+    q = bench.cpu_quota()
+    assert q is None or q > 0

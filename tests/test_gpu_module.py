@@ -1,0 +1,144 @@
+"""GraphModule boundary on the MI355X: traced runs never race with later writes, load_params
+re-derives every build-time buffer, and a saved module reloads in a fresh process.
+
+References: python/tvm/contrib/graph_executor.py:166-327 (set_input / run / load_params),
+src/runtime/graph_executor/graph_executor.cc:283-291 (LoadParams), src/runtime/contrib/json/
+json_runtime.h:105-135 (SaveToBinary / LoadFromBinary)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import graph_ref
+from tachikoma_amd import _lib, relay, runtime, zoo
+from tachikoma_amd.contrib import graph_executor
+from tachikoma_amd.relay.build_module import lift_constants
+from tachikoma_amd.trace_format import read_trace
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _compare(records, expected):
+    assert set(expected) <= set(records)
+    for name, exp in expected.items():
+        got = records[name]
+        assert got.shape == exp.shape and got.dtype == exp.dtype, (name, got.shape, exp.shape)
+        if not np.array_equal(got, exp):
+            idx = tuple(np.argwhere(got != exp)[0])
+            raise AssertionError(f"record {name}: first mismatch at {idx}: {got[idx]} vs {exp[idx]}")
+
+
+def _image_records(m):
+    return read_trace(m.trace_capture().bytes()).records
+
+
+def test_traced_run_then_immediate_rewrite(device):
+    """run(trace=True) returns while the D2H copies are in flight; an immediate set_input(B)
+    and untraced run() must wait for them, so the image holds run A record for record."""
+    import torch
+    model = zoo.resnet18(batch=16)
+    xa = model.sample_inputs(0, 16)
+    xb = model.sample_inputs(16, 16)
+    lib = relay.build(model.mod, target="mi355x", params=model.params)
+    m = graph_executor.GraphModule(lib["default"]())
+    m.set_input("data", xa)
+    m.run(trace=True)
+    m.set_input("data", xb)   # no synchronisation in between
+    m.run()
+    m.trace_capture().synchronize()
+    torch.cuda.synchronize()
+    recs = _image_records(m)
+    exp = graph_ref.calibrate(model.mod, model.params, {"data": xa[[0, 15]]}, backend="c")
+    _compare({k: v[[0, 15]] for k, v in recs.items()}, exp)
+    # and the untraced run computed B
+    out = m.get_output(0).numpy()
+    exp_b = graph_ref.calibrate(model.mod, model.params, {"data": xb[[3]]}, backend="c")
+    np.testing.assert_array_equal(out[[3]], exp_b[m.plan.outputs[0]])
+
+
+def _reversed(params):
+    """Same shapes, dtypes and value ranges, different values: each array reversed along axis 0."""
+    return {k: np.ascontiguousarray(np.asarray(v)[::-1]) for k, v in params.items()}
+
+
+@pytest.mark.parametrize("name,batch", [("resnet18", 2), ("qnn_dense_128", None), ("mobilenet_v2", 1)])
+def test_load_params_repacks(device, tmp_path, name, batch):
+    model = zoo.MODELS[name]() if batch is None else zoo.MODELS[name](batch=batch)
+    x = model.fixed_input if batch is None else model.random_input()
+    p2 = _reversed(model.params)
+    lib = relay.build(model.mod, target="mi355x", params=model.params)
+    m = graph_executor.GraphModule(lib["default"]())
+    m.set_input(model.input_name, x)
+    m.run(trace=True)                      # capture exists: its params section must refresh too
+    m.load_params(relay.save_param_dict(p2))
+    path = str(tmp_path / "p2.tkt")
+    m.dump_trace(path)
+    tr = read_trace(path)
+    exp = graph_ref.calibrate(model.mod, p2, {model.input_name: x}, backend="c")
+    _compare(tr.records, exp)
+    for k, v in p2.items():
+        np.testing.assert_array_equal(tr.params[k], v)
+
+
+def test_load_params_realized_graph(device, tmp_path):
+    """relay.quantize output: its folded weights are lifted to params (_const<k>) and the int8
+    convolutions pack them; load_params re-packs."""
+    from tachikoma_amd.relay.quantize import quantize
+    fm = zoo.resnet_float(18, batch=2, hw=64)
+    q = quantize(fm.mod, fm.params)
+    mod_l, p1 = lift_constants(q, {})
+    p2 = _reversed(p1)
+    lib = relay.build(mod_l, target="mi355x", params=p1)
+    m = graph_executor.GraphModule(lib["default"]())
+    x = fm.random_input()
+    m.set_input("data", x)
+    m.load_params(relay.save_param_dict(p2))
+    path = str(tmp_path / "q2.tkt")
+    m.dump_trace(path)
+    exp = graph_ref.calibrate(mod_l, p2, {"data": x})
+    _compare(read_trace(path).records, exp)
+
+
+def test_load_params_rejects_before_writing(device, tmp_path):
+    model = zoo.resnet18(batch=1)
+    x = model.random_input()
+    lib = relay.build(model.mod, target="mi355x", params=model.params)
+    m = graph_executor.GraphModule(lib["default"]())
+    m.set_input("data", x)
+    bad = _reversed(model.params)
+    first = next(iter(bad))
+    bad[next(reversed(list(bad)))] = np.zeros((3, 3), np.int8)   # last entry has the wrong shape
+    bad["not_in_graph"] = np.zeros(4, np.int32)                    # skipped like LoadParams
+    with pytest.raises(_lib.TachikomaError):
+        m.load_params(relay.save_param_dict(bad))
+    # nothing was written: still the build-time params
+    np.testing.assert_array_equal(m.get_input(first).numpy(), model.params[first])
+    path = str(tmp_path / "p1.tkt")
+    m.dump_trace(path)
+    exp = graph_ref.calibrate(model.mod, model.params, {"data": x}, backend="c")
+    _compare(read_trace(path).records, exp)
+
+
+def test_export_library_reload_in_fresh_process(device, tmp_path):
+    model = zoo.resnet18(batch=2)
+    x = model.random_input()
+    lib = relay.build(model.mod, target="mi355x", params=model.params)
+    mod_path = str(tmp_path / "resnet18.tkm")
+    lib.export_library(mod_path)
+    x_path = str(tmp_path / "x.npy")
+    np.save(x_path, x)
+    out = str(tmp_path / "reloaded.tkt")
+    code = ("import sys, numpy as np; sys.path.insert(0, %r)\n"
+            "from tachikoma_amd import runtime\n"
+            "from tachikoma_amd.contrib import graph_executor\n"
+            "lib = runtime.load_module(%r)\n"
+            "m = graph_executor.GraphModule(lib['default']())\n"
+            "m.set_input('data', np.load(%r))\n"
+            "m.dump_trace(%r)\n") % (ROOT, mod_path, x_path, out)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    exp = graph_ref.calibrate(model.mod, model.params, {"data": x}, backend="c")
+    _compare(read_trace(out).records, exp)

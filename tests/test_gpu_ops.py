@@ -5,6 +5,8 @@ sweeps over the edge cases the reference tests: zero points (scalar / per-channe
 uint8 operands, strides, padding, dilation, groups/depthwise, ragged K and M,
 saturation, per-axis requantize, both rounding modes.
 """
+import zlib
+
 import numpy as np
 import pytest
 
@@ -99,7 +101,7 @@ CONV_CASES = [
 @pytest.mark.parametrize("case", CONV_CASES, ids=[f"conv{i}" for i in range(len(CONV_CASES))])
 def test_conv2d_random(tk, case):
     n, c, h, w, o, k, s, p, d, g, dx, dw_, za, zw = case
-    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()))  # PYTHONHASHSEED-independent
     x = _rand(rng, (n, c, h, w), dx)
     wt = _rand(rng, (o, c // g, k, k), dw_)
     pad = (p, p, p, p) if isinstance(p, int) else p

@@ -80,6 +80,12 @@ def test_ewise_ops_bit_exact(device):
     for m_, s_ in ((1518500250, -3), (1395864371, 1), (2**30, -2)):
         got = _ew(i64, "fixed_point_multiply", multiplier=m_, shift=s_)
         assert np.array_equal(got, realize_ref.fixed_point_multiply(i64, m_, s_)), (m_, s_)
+    # int64 data beyond the int32 range: the power-of-two branch works in int64 (no wrap at 32
+    # bits), the general branch multiplies the full int64 value (intrin_rule.cc:166-237)
+    wide = rng.integers(-2**40, 2**40, 4099).astype(np.int64)
+    for m_, s_ in ((2**30, 4), (2**30, -3), (1518500250, -3)):
+        got = _ew(wide, "fixed_point_multiply", multiplier=m_, shift=s_)
+        assert np.array_equal(got, realize_ref.fixed_point_multiply(wide, m_, s_)), (m_, s_)
 
 
 @pytest.mark.parametrize("mode", ["kl_divergence", "percentile"])

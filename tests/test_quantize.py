@@ -275,3 +275,32 @@ def test_dataset_calibration_order(monkeypatch, mode):
     assert any(k != 2 for k in kinds)
     out = list(graph_ref.calibrate(q, {}, {"data": data[0]["data"]}).values())[-1]
     assert out.dtype == np.float32 and np.isfinite(out).all()
+
+
+def test_fixed_point_multiply_int64_power_of_two_kat():
+    """relay.fixed_point_multiply on int64 data: the power-of-two branch of the
+    q_multiply_shift legalization (intrin_rule.cc:223-237) shifts and rounds in x's dtype, so
+    int64 values beyond the int32 range do not wrap; the general branch (:166-195) casts the
+    int64 product's result to int32."""
+    from oracle import realize_ref
+    x = np.array([2**35 + 3, -(2**35) - 9, 5, -5], np.int64)
+    assert realize_ref.fixed_point_multiply(x, 1 << 30, 4).tolist() == [2**38 + 24, -(2**38) - 72, 40, -40]
+    assert realize_ref.fixed_point_multiply(x, 1 << 30, -3).tolist() == [2**31, -(2**31) - 1, 0, 0]
+    # general branch: (x * m + 2^(30+rs)) >> (31+rs) in int64 (wrapping at 64 bits), then int32
+    m, s = 1518500250, -3
+
+    def wrap(v, bits):
+        return ((v + 2**(bits - 1)) % 2**bits) - 2**(bits - 1)
+    exp = [wrap(wrap(wrap(int(v) * m, 64) + (1 << 33), 64) >> 34, 32) for v in x]
+    assert realize_ref.fixed_point_multiply(x, m, s).tolist() == exp
+
+
+def test_kl_histogram_edges_are_float32():
+    """kl_divergence.py:46-48 hands np.histogram's edges to MinimizeKL as c_float*: for the
+    float32 statistics the profile graph produces, numpy builds float32 edges (result_type of
+    the float32 range and data), so the reference's cast reads real float32 edges and
+    find_scale_by_kl's explicit float32 conversion is the identity."""
+    arr = np.random.default_rng(0).standard_normal(10000).astype(np.float32)
+    thres = max(abs(np.min(arr)), abs(np.max(arr)))
+    _, edges = np.histogram(arr, bins=8001, range=(-thres, thres))
+    assert edges.dtype == np.float32
