@@ -18,9 +18,15 @@ Files, as the reference writes them:
   * ``_tvmdbg_execution_trace.json`` — Chrome trace, B/E events per node, pid = tid = 1,
     ``displayTimeUnit`` "ns" (debug_result.py:151-189).
 
-Granularity: one graph node per Relay op (MRT names ``%N``), i.e. finer than the
-reference's FuseOps-fused nodes; a fused device block's ops each get their own node,
-with the block's device time attributed to its first op and 0 to the rest.
+Granularity (``create(..., granularity=)``):
+  * ``"fused"`` (default, the reference's): one graph node per FuseOps-fused primitive
+    function (relay/fuse.py: fuse_ops.cc partitioning, te_compiler_cache.cc naming, e.g.
+    ``tvmgen_default_fused_qnn_conv2d_nn_bias_add_qnn_requantize_clip_3``); its output is the
+    value of the group's last op, and params appear as ``null`` nodes before their first
+    consumer, as the graph codegen emits bound constants;
+  * ``"op"``: one graph node per Relay op (MRT names ``%N``), finer than the reference.
+Device time of a node is the time of the device kernels that write its records (a device
+block's time goes to the node holding its first op).
 """
 from __future__ import annotations
 
@@ -42,29 +48,55 @@ CHROME_TRACE_FILE_NAME = "_tvmdbg_execution_trace.json"
 OUTPUT_TENSORS_FILE_NAME = "output_tensors.params"
 
 
-def executor_graph_json(plan) -> dict:
-    """The plan as a graph-executor JSON graph (graph_executor.h:226-340 layout): null nodes
-    for graph inputs and params, one tvm_op node per op, in topological order."""
+def executor_graph_json(plan, granularity: str = "op", mod_name: str = "default") -> dict:
+    """The plan as a graph-executor JSON graph (graph_executor.h:226-340 layout).
+
+    ``"op"``: null nodes for graph inputs and params, one tvm_op node per op, topological.
+    ``"fused"``: null nodes for graph inputs, then the fused calls in the graph codegen's post
+    order, each preceded by null nodes for the params it uses first
+    (graph_executor_codegen.cc:408-472).  ``"outputs"`` maps every node to the plan tensor
+    holding its value (the fused group's last op for a fused node)."""
     nodes: List[dict] = []
     index: Dict[str, int] = {}
     dltype: List[str] = []
     shapes: List[List[int]] = []
-    for t in list(plan.inputs) + list(plan.params):
+    outputs: List[str] = []
+    arg_nodes: List[int] = []
+
+    def null(t):
         index[t.name] = len(nodes)
+        arg_nodes.append(len(nodes))
         nodes.append({"op": "null", "name": t.name, "inputs": []})
         dltype.append(t.dtype)
         shapes.append([int(d) for d in t.shape])
-    arg_nodes = list(range(len(nodes)))
-    for op in plan.ops:
-        index[op.name] = len(nodes)
-        nodes.append({
-            "op": "tvm_op", "name": op.name,
-            "inputs": [[index[x], 0, 0] for x in op.inputs],
-            "attrs": {"func_name": "tachikoma_" + op.op.replace(".", "_"), "num_inputs": str(len(op.inputs)),
-                      "num_outputs": "1", "flatten_data": "0"},
-        })
-        dltype.append(op.out.dtype)
-        shapes.append([int(d) for d in op.out.shape])
+        outputs.append(t.name)
+
+    def call(name, func_name, inputs, out):
+        index[out.name] = len(nodes)
+        nodes.append({"op": "tvm_op", "name": name, "inputs": [[index[x], 0, 0] for x in inputs],
+                      "attrs": {"func_name": func_name, "num_inputs": str(len(inputs)), "num_outputs": "1",
+                                "flatten_data": "0"}})
+        dltype.append(out.dtype)
+        shapes.append([int(d) for d in out.shape])
+        outputs.append(out.name)
+
+    if granularity == "op":
+        for t in list(plan.inputs) + list(plan.params):
+            null(t)
+        for op in plan.ops:
+            call(op.name, "tachikoma_" + op.op.replace(".", "_"), op.inputs, op.out)
+    elif granularity == "fused":
+        from ...relay.fuse import fused_nodes
+        params = {t.name: t for t in plan.params}
+        for t in plan.inputs:
+            null(t)
+        for fn in fused_nodes(plan, mod_name):
+            for x in fn.inputs:
+                if x in params and x not in index:
+                    null(params[x])
+            call(fn.node_name, fn.func_name, fn.inputs, fn.ops[-1].out)
+    else:
+        raise ValueError(f"granularity must be 'fused' or 'op', not {granularity!r}")
     return {
         "nodes": nodes,
         "arg_nodes": arg_nodes,
@@ -72,6 +104,7 @@ def executor_graph_json(plan) -> dict:
         "heads": [[index[o], 0, 0] for o in plan.outputs],
         "attrs": {"dltype": ["list_str", dltype], "shape": ["list_shape", shapes],
                   "storage_id": ["list_int", list(range(len(nodes)))]},
+        "outputs": outputs,
     }
 
 
@@ -95,55 +128,74 @@ def _debug_nodes(graph: dict) -> List[dict]:
 class GraphModuleDebug(GraphModule):
     """GraphModule + the debug executor's dump (debug_executor.py:89-347)."""
 
-    def __init__(self, module, device_name: str, dump_root: Optional[str] = None):
+    def __init__(self, module, device_name: str, dump_root: Optional[str] = None, granularity: str = "fused",
+                 mod_name: str = "default"):
         super().__init__(module)
         self._dump_root = dump_root or tempfile.mkdtemp(prefix=DUMP_ROOT_PREFIX)
         folder = DUMP_PATH_PREFIX + "device_" + device_name.upper().replace("(", ":").replace(")", "").replace(":", "_")
         self._dump_path = os.path.join(self._dump_root, folder)
         os.makedirs(self._dump_path, 0o700, exist_ok=True)
-        self._graph = executor_graph_json(self.plan)
+        self.granularity = granularity
+        graph = executor_graph_json(self.plan, granularity, mod_name)
+        self._node_outputs: List[str] = graph.pop("outputs")
+        self._graph = graph
         self._nodes = _debug_nodes(self._graph)
         with open(os.path.join(self._dump_path, GRAPH_DUMP_FILE_NAME), "w") as f:
             json.dump({**self._graph, "nodes": self._nodes}, f, indent=4, sort_keys=False)
         self._times_s: List[List[float]] = []
-        self._outputs: Dict[str, np.ndarray] = {}
+        self._outputs: Dict[int, np.ndarray] = {}
 
     @property
     def dump_path(self) -> str:
         return self._dump_path
 
-    def _node_times(self, repeat: int) -> Dict[str, List[float]]:
-        """Device seconds per plan op: each device node's time goes to its first op."""
-        per_op: Dict[str, List[float]] = {n["name"]: [] for n in self._nodes}
+    def _node_times(self, repeat: int) -> List[List[float]]:
+        """Device seconds per graph node: each device node's time goes to the graph node that
+        holds its first record's op (a shadow node's to the next device node's)."""
+        node_of: Dict[str, int] = {}
+        if self.granularity == "fused":
+            from ...relay.fuse import fused_nodes
+            op_nodes = [i for i, n in enumerate(self._nodes) if n["op"] != "param"]
+            for gi, fn in zip(op_nodes, fused_nodes(self.plan)):
+                for op in fn.ops:
+                    node_of[op.name] = gi
+        else:
+            for i, n in enumerate(self._nodes):
+                node_of[n["name"]] = i
+        per_node: List[List[float]] = [[] for _ in self._nodes]
         for _ in range(max(1, repeat)):
             times = self.module.run_profiled()  # ms per device node, keyed by "+".join(records)
-            seen = set()
+            acc = [0.0] * len(self._nodes)
+            carry = 0.0
             for key, ms in times.items():
                 if key.startswith("<"):
-                    continue  # shadow nodes carry no op
-                recs = key.split("+")
-                for k, name in enumerate(recs):
-                    per_op[name].append(ms * 1e-3 if k == 0 else 0.0)
-                    seen.add(name)
-            for name in per_op:
-                if name not in seen:
-                    per_op[name].append(0.0)
-        return per_op
+                    carry += ms  # shadow nodes carry no op: charged to the consumer
+                    continue
+                acc[node_of[key.split("+")[0]]] += (ms + carry) * 1e-3
+                carry = 0.0
+            for i, t in enumerate(acc):
+                per_node[i].append(t)
+        return per_node
 
     def run(self, repeat: int = 1, sort_by_time: bool = True, **inputs):  # noqa: D401  (debug_executor.run)
         """Execute, time every node, dump the output tensors and the Chrome trace, print the table."""
         if inputs:
             self.set_input(**inputs)
-        per_op = self._node_times(repeat)
-        self._times_s = [per_op[n["name"]] for n in self._nodes]
-        self._outputs = {n["name"]: self.module.buffers[n["name"]].detach().cpu().numpy() for n in self._nodes}
+        self._times_s = self._node_times(repeat)
+        self._outputs = {i: self.module.buffers[name].detach().cpu().numpy()
+                         for i, name in enumerate(self._node_outputs)}
         self.dump_output_tensor()
         self.dump_chrome_trace()
         self.display_debug_result(sort_by_time)
 
     def get_output_tensors(self) -> Dict[str, np.ndarray]:
-        return {f"{n['name']}____topo-index:{i}____output-num:0": self._outputs[n["name"]]
+        """debug_result.py:114-127: keyed ``{name}____topo-index:{i}____output-num:{j}``."""
+        return {f"{n['name']}____topo-index:{i}____output-num:0": self._outputs[i]
                 for i, n in enumerate(self._nodes)}
+
+    def node_outputs(self) -> List[str]:
+        """Plan tensor holding each graph node's value (a fused node: its group's last op)."""
+        return list(self._node_outputs)
 
     def dump_output_tensor(self) -> None:
         with open(os.path.join(self._dump_path, OUTPUT_TENSORS_FILE_NAME), "wb") as f:
@@ -190,8 +242,8 @@ class GraphModuleDebug(GraphModule):
             shutil.rmtree(self._dump_root)
 
 
-def create(lib_factory, dev=None, dump_root: Optional[str] = None) -> GraphModuleDebug:
+def create(lib_factory, dev=None, dump_root: Optional[str] = None, granularity: str = "fused") -> GraphModuleDebug:
     """``debug_executor.create`` analogue taking what ``relay.build`` returns."""
-    module = lib_factory["default"](dev)
+    module = lib_factory[lib_factory.mod_name](dev)
     dev_id = int(module.device.index or 0)
-    return GraphModuleDebug(module, f"rocm({dev_id})", dump_root)
+    return GraphModuleDebug(module, f"rocm({dev_id})", dump_root, granularity, lib_factory.mod_name)

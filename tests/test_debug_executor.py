@@ -33,6 +33,61 @@ def test_executor_graph_json_layout():
     assert nodes[-1]["attrs"]["T"].startswith("type: ")
 
 
+def test_fused_graph_json_layout():
+    """granularity="fused": one tvm_op node per FuseOps group, named like the reference's
+    fused functions, params as null nodes before their first consumer."""
+    m = zoo.resnet18(batch=1)
+    plan = lower(m.mod, m.params)
+    g = executor_graph_json(plan, "fused")
+    outputs = g.pop("outputs")
+    ops = [n for n in g["nodes"] if n["op"] == "tvm_op"]
+    from tachikoma_amd.relay.fuse import fused_nodes
+    fns = fused_nodes(plan)
+    assert [n["name"] for n in ops] == [f.node_name for f in fns]
+    assert all(n["attrs"]["func_name"].startswith("tvmgen_default_fused_qnn_") or
+               n["attrs"]["func_name"].startswith("tvmgen_default_fused_nn_") for n in ops)
+    assert len(g["nodes"]) == len(plan.inputs) + len(plan.params) + len(fns)
+    for i, n in enumerate(g["nodes"]):
+        assert all(src[0] < i for src in n["inputs"])
+    assert g["nodes"][g["heads"][0][0]]["op"] == "tvm_op"
+    assert outputs[g["heads"][0][0]] == plan.outputs[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,batch", [("resnet18", 2), ("mobilenet_v2", 1)])
+def test_fused_debug_dump_matches_oracle(device, tmp_path, name, batch):
+    """Every fused node's dumped tensor equals the oracle's value of its group's last op."""
+    import tachikoma_amd
+    from oracle import graph_ref
+    from tachikoma_amd import relay, trace_format as tf
+    from tachikoma_amd.contrib.debugger import debug_executor
+
+    model = zoo.MODELS[name](batch=batch)
+    x = model.random_input()
+    lib = relay.build(model.mod, target="mi355x", params=model.params)
+    mod = debug_executor.create(lib, tachikoma_amd.rocm(0), dump_root=str(tmp_path / "dbg"))
+    mod.set_input("data", x)
+    mod.run()
+    with open(os.path.join(mod.dump_path, "output_tensors.params"), "rb") as f:
+        tensors = tf.parse_ndarray_list(f.read(), copy=True)
+    exp = graph_ref.calibrate(model.mod, model.params, {"data": x}, backend="c")
+    pattern = re.compile(r"^(.+)____topo-index:(\d+)____output-num:0$")
+    outs = mod.node_outputs()
+    n_fused = 0
+    for i, (key, arr) in enumerate(tensors.items()):
+        mt = pattern.match(key)
+        assert mt and int(mt.group(2)) == i
+        src = outs[i]
+        want = exp[src] if src in exp else model.params[src]
+        np.testing.assert_array_equal(arr, want)
+        n_fused += mt.group(1).startswith("tvmgen_default_fused_")
+    from tachikoma_amd.relay.fuse import fused_nodes
+    assert n_fused == len(fused_nodes(mod.plan))
+    lines = mod.get_debug_result().split("\n")
+    assert lines[-1].startswith("Total_time")
+    mod.exit()
+
+
 @pytest.mark.gpu
 def test_debug_dump_matches_oracle(device, tmp_path):
     import tachikoma_amd
@@ -43,7 +98,7 @@ def test_debug_dump_matches_oracle(device, tmp_path):
     model = zoo.lenet5(batch=2)
     x = model.sample_inputs(0, 2)
     lib = relay.build(model.mod, target="mi355x", params=model.params)
-    mod = debug_executor.create(lib, tachikoma_amd.rocm(0), dump_root=str(tmp_path / "dbg"))
+    mod = debug_executor.create(lib, tachikoma_amd.rocm(0), dump_root=str(tmp_path / "dbg"), granularity="op")
     mod.set_input("data", x)
     directory = mod.dump_path
     assert os.path.basename(directory) == "_tvmdbg_device_ROCM_0"
