@@ -397,8 +397,14 @@ def main(argv=None) -> int:
     m.run(trace=not args.no_trace)
     torch.cuda.synchronize(device)
     digests = shard.gather_digests(m.module.records_digest(stream).to(coll_dev))
+    file_check = None
     if args.sink == "file" and not args.no_trace:
         caps[0].write(path)
+        # the file on disk must carry exactly the records the device digested
+        from tachikoma_amd.trace_format import trace_file_digest
+        fd = trace_file_digest(path)
+        file_check = {"path": path, "file_digest": shard.hex64(fd), "device_digest": shard.hex64(digests[rank]),
+                      "equal": fd == (digests[rank] & 0xFFFFFFFFFFFFFFFF)}
         entries = [shard.ShardEntry(r, *shard.shard_range(B * world, world, r), shard.hex64(d),
                                     shard.shard_file(args.out_dir, r)) for r, d in enumerate(digests)]
         if rank == 0:
@@ -432,7 +438,8 @@ def main(argv=None) -> int:
                  "d2h": {"achieved_GBps": round(trace_bytes / (elapsed / args.steps) / 1e9, 2),
                          "measured_peak_GBps": round(d2h_peak, 2),
                          "frac": round(trace_bytes / (elapsed / args.steps) / 1e9 / d2h_peak, 4)},
-                 "parity": parity.summary() if parity is not None else None}
+                 "parity": parity.summary() if parity is not None else None,
+                 "file_sink": file_check}
     if world > 1:
         ranks = [None] * world
         dist.all_gather_object(ranks, rank_info)
@@ -452,6 +459,9 @@ def main(argv=None) -> int:
                    "first_mismatch": next((p["first_mismatch"] for p in ps if p["first_mismatch"]), None),
                    "oracle": "oracle/graph_ref.py C backend (reference int16 conv / int64 requantize semantics)"}
             rc = 1 if par["mismatches"] else 0
+        if any(r.get("file_sink") and not r["file_sink"]["equal"] for r in ranks):
+            _log("FILE SINK FAILURE: a written trace file's digest differs from its device digest")
+            rc = 1
         line = {
             "metric": METRIC,
             "value": round(value, 3),

@@ -93,6 +93,7 @@ struct GemmArgs {
   // tile's 64 channels x OH*OW pixels are one contiguous NCHW run: see the flat epilogue
   int32_t ipt, tcols;
   int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
+                       // 8192 residual join without the LUTs, 16384 skip the add record,
                        // 8/16/32/64 skip the conv / bias_add / requantize / clip record,
                        // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs, 1024 main-loop
                        // barrier without the lgkmcnt(0) drain, 2048 skip the fragment reads, 4096 skip
@@ -262,6 +263,14 @@ struct FillRows {
 __device__ FillRows tk_fill_rows{};
 __device__ int32_t tk_zero_words[4] = {0, 0, 0, 0};
 
+// Ablation switches of the profiling build (g.ablate, see GemmArgs::ablate); compiled out of
+// the product library.  Needs a local `abl` copy of g.ablate (lambdas must not touch g).
+#ifdef TK_ABLATION_BUILD
+#define TK_ABL(flag) (abl & (flag))
+#else
+#define TK_ABL(flag) 0
+#endif
+
 // Workgroup barrier that only drains this wave's LDS traffic.  __syncthreads() also waits
 // vmcnt(0), i.e. for every outstanding global store of the epilogue to complete, which
 // serialises the store latency once per barrier; the epilogue's barriers only order LDS.
@@ -380,6 +389,7 @@ gemm_i8_kernel(GemmArgs g) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  [[maybe_unused]] const int abl = g.ablate;
   if (kBlock && tid == 0) s_fast = 1;  // visible after the first barrier; only cleared later
   int mtile, ntile;
   tile_of(g, mtile, ntile);
@@ -887,9 +897,12 @@ gemm_i8_kernel(GemmArgs g) {
           if (has_add) {
             // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((resid_pre[k] >> (8 * e)) & 0xFFu)] - add_zp, qmin, qmax);
-            __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t rb = (resid_pre[k] >> (8 * e)) & 0xFFu;
+              q[e] = clamp_i32(TK_ABL(8192) ? q[e] + (int32_t)rb - add_zp : lut[q[e] & 0xFF] + lut[256 + rb] - add_zp,
+                               qmin, qmax);
+            }
+            if (!TK_ABL(16384)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
           }
           if (has_clip) {
 #pragma unroll
@@ -954,9 +967,12 @@ gemm_i8_kernel(GemmArgs g) {
           if constexpr (ADD) {
             // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((resid_pre[k] >> (8 * e)) & 0xFFu)] - add_zp, qmin, qmax);
-            __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, AUX);
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t rb = (resid_pre[k] >> (8 * e)) & 0xFFu;
+              q[e] = clamp_i32(TK_ABL(8192) ? q[e] + (int32_t)rb - add_zp : lut[q[e] & 0xFF] + lut[256 + rb] - add_zp,
+                               qmin, qmax);
+            }
+            if (!TK_ABL(16384)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, AUX);
           }
           if constexpr (CLIP) {
 #pragma unroll

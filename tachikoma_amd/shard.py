@@ -72,7 +72,10 @@ class ShardEntry:
     file: Optional[str] = None
 
 
-def write_manifest(path: str, model: str, global_batch: int, shards: List[ShardEntry]) -> None:
+def write_manifest(path: str, model: str, global_batch: int, shards: List[ShardEntry],
+                   world: Optional[int] = None) -> None:
+    """Run manifest: every shard (or chunk of a shard, see trace_job) with its sample range,
+    u64 record digest and file; the entries must tile [0, global_batch) exactly."""
     covered = sorted((s.sample_offset, s.n_samples) for s in shards)
     pos = 0
     for off, n in covered:
@@ -82,7 +85,8 @@ def write_manifest(path: str, model: str, global_batch: int, shards: List[ShardE
     if pos != global_batch:
         raise ValueError(f"shards cover {pos} of {global_batch} samples")
     doc = {"format": MANIFEST_FORMAT, "version": 1, "model": model, "global_batch": global_batch,
-           "world": len(shards), "shards": [asdict(s) for s in sorted(shards, key=lambda s: s.rank)]}
+           "world": len(shards) if world is None else int(world),
+           "shards": [asdict(s) for s in sorted(shards, key=lambda s: (s.rank, s.sample_offset))]}
     tmp = path + ".tmp"
     with open(tmp, "w") as f:
         json.dump(doc, f, indent=1)

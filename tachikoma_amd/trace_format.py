@@ -231,3 +231,20 @@ def records_digest(records: "Dict[str, np.ndarray] | Sequence[np.ndarray]") -> i
 
 def trace_file_digest(path_or_bytes) -> int:
     return records_digest(read_trace(path_or_bytes).records)
+
+
+def trace_bytes(meta: Dict[str, Any], params: Dict[str, np.ndarray], records: Dict[str, np.ndarray]) -> bytes:
+    """A complete trace file from host arrays (the same layout the device capture fills:
+    tk_trace_layout / tk_trace_write_headers), e.g. for traces produced on the CPU."""
+    p_items = [(k, tuple(np.asarray(v).shape), str(np.asarray(v).dtype)) for k, v in params.items()]
+    r_items = [(k, tuple(np.asarray(v).shape), str(np.asarray(v).dtype)) for k, v in records.items()]
+    layout = TraceLayout.compute(header_json(meta), p_items, r_items)
+    blob = bytearray(layout.total)
+    buf = (ctypes.c_char * len(blob)).from_buffer(blob)
+    layout.write_headers(ctypes.addressof(buf), len(blob))
+    del buf
+    for offs, arrays in ((layout.param_offsets, params.values()), (layout.record_offsets, records.values())):
+        for off, v in zip(offs, arrays):
+            raw = np.ascontiguousarray(v).reshape(-1).view(np.uint8)
+            blob[off:off + raw.size] = raw.tobytes()
+    return bytes(blob)

@@ -22,6 +22,11 @@ SHAPES = [  # name, C, H, O, K, stride, pad
     ("3x3 512->512 7", 512, 7, 512, 3, 1, 1),
     ("1x1 512->2048 7", 512, 7, 2048, 1, 1, 0),
     ("1x1 2048->512 7", 2048, 7, 512, 1, 1, 0),
+    # expand layers with the fused residual join (qnn.add -> clip), as in every bottleneck
+    ("res 1x1 64->256 56", 64, 56, 256, 1, 1, 0),
+    ("res 1x1 128->512 28", 128, 28, 512, 1, 1, 0),
+    ("res 1x1 256->1024 14", 256, 14, 1024, 1, 1, 0),
+    ("res 1x1 512->2048 7", 512, 7, 2048, 1, 1, 0),
 ]
 
 
@@ -41,8 +46,9 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None):
         x = torch.from_numpy(rng.integers(-128, 128, size=(batch, C, H, H)).astype(np.int8)).to(dev)
         w = torch.from_numpy(rng.integers(-128, 128, size=(O, C, K, K)).astype(np.int8)).to(dev)
         b = torch.from_numpy(rng.integers(-2**14, 2**14, size=O).astype(np.int32)).to(dev)
-        outs = [torch.empty((batch, O, OH, OH), dtype=t, device=dev) for t in (torch.int32, torch.int32, torch.int8,
-                                                                             torch.int8)]
+        res = name.startswith("res ")
+        outs = [torch.empty((batch, O, OH, OH), dtype=t, device=dev)
+                for t in (torch.int32, torch.int32, torch.int8) + ((torch.int8,) if res else ()) + (torch.int8,)]
         a = _lib.tk_block_attrs()
         a.conv.strides[:] = [S, S]
         a.conv.padding[:] = [P] * 4
@@ -55,9 +61,21 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None):
         a.requantize.multipliers, a.requantize.shifts = md.data_ptr(), sd.data_ptr()
         a.requantize.output_zero_point = 2
         a.has_clip, a.clip_min, a.clip_max = 1, 2, 127
+        keep = []
+        if res:
+            resid = torch.from_numpy(rng.integers(-128, 128, size=(batch, O, OH, OH)).astype(np.int8)).to(dev)
+            rr = _lib.TensorRef.from_torch(resid)
+            keep += [resid, rr]
+            a.has_add, a.block_is_rhs, a.residual = 1, 0, rr.ptr
+            for side, ratio in ((a.add.lhs, 0.71), (a.add.rhs, 1.37)):
+                m_, ms_, ss_ = requantize_plan(np.float32(ratio * 0.05), np.float32(0.05), "UPWARD")
+                side.mode, side.axis = m_, -1
+                side.multiplier, side.shift = int(ms_[0]), int(ss_[0])
+                side.input_zero_point, side.output_zero_point = 1, 3
+            a.add.output_zero_point = 3
         rx, rw, rb = [_lib.TensorRef.from_torch(t) for t in (x, w, b)]
         refs = [_lib.TensorRef.from_torch(t) for t in outs]
-        arr = (ctypes.POINTER(_lib.tk_tensor) * 4)(*[r.ptr for r in refs])
+        arr = (ctypes.POINTER(_lib.tk_tensor) * len(refs))(*[r.ptr for r in refs])
         st = ctypes.c_void_p(_lib.stream_handle())
         shadow = torch.empty(lib.tk_conv2d_shadow_bytes(rx.ptr), dtype=torch.uint8, device=dev)
         packed = torch.empty(lib.tk_conv2d_packed_weight_bytes(rw.ptr, 1), dtype=torch.uint8, device=dev)
@@ -72,7 +90,7 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None):
         def call():
             _lib.check(lib.tk_qnn_conv2d_block(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), rw.ptr,
                                                ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(sums.data_ptr()),
-                                               rb.ptr, arr, 4, ctypes.byref(a), ctypes.c_void_p(scratch.data_ptr()),
+                                               rb.ptr, arr, len(refs), ctypes.byref(a), ctypes.c_void_p(scratch.data_ptr()),
                                                ctypes.c_void_p(sh_out.data_ptr()), st))
         best = [float("inf")] * len(configs)
         for _ in range(reps):
@@ -93,7 +111,7 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None):
                     else:
                         os.environ[k] = v
         out_el = batch * O * OH * OH
-        by = x.numel() + w.numel() + 4 * O + out_el * 10
+        by = x.numel() + w.numel() + 4 * O + out_el * (12 if res else 10)
         macs = out_el * C * K * K
         cols = "  ".join(f"{us:8.1f} us {by / us / 1e3:6.0f} GB/s" for us in best)
         print(f"{name:22s} {cols}   ({2 * macs / best[0] / 1e6:.0f} TOPS)", flush=True)
