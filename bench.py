@@ -37,6 +37,7 @@ import numpy as np  # noqa: E402
 INT8_MFMA_PEAK_OPS = 5.0e15  # gfx950 dense int8 (2x the 2.5 PF dense bf16 peak), MI355X_MICROARCH.md
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (6.3 TB/s measured streaming copy), MI355X_MICROARCH.md
 METRIC = "ResNet-50 int8 op-traces/sec at 1/2/4/8 GPU; bit-exact vs CPU"
+BLOCK_KINDS = ("conv_block", "dense_block", "qnn.conv2d", "qnn.dense")
 
 
 def _log(msg: str) -> None:
@@ -343,32 +344,58 @@ def main(argv=None) -> int:
     if writer is not None:
         writer.shutdown()
 
-    # ---- compute-only steps (no capture): the kernels alone, each node bracketed by HIP
-    # events recorded on the stream the node's kernel runs on (tk_module_set_profiling);
-    # the roofline below is taken from these, where no D2H copy shares the device
+    # ---- compute-only steps (no capture): the kernels alone, timed with HIP events recorded
+    # on the stream they run on (torch's current stream, handed to the module); the roofline
+    # below is taken from these, where no D2H copy shares the device
     torch.cuda.synchronize(device)
     tc0 = time.perf_counter()
     for _ in range(args.steps):
         m.run(trace=False)
     torch.cuda.synchronize(device)
     compute_ms = (time.perf_counter() - tc0) / max(args.steps, 1) * 1e3
-    m.module.set_profiling(True)
-    node_ms = np.zeros(m.module.n_nodes)
+    # Block time from HIP events bracketing each maximal run of consecutive block nodes (52 of
+    # ResNet-50's 54 blocks are one run): a timing event between every two nodes would add the
+    # command processor's ~5.6 us per event to every node (rocprof: kernels back to back have
+    # no gap, event-separated ones 5.4-5.9 us, profiles/r02d_network_kernels.txt).
+    kinds = m.module.node_kinds
+    is_blk = [bool(recs) and kinds[i] in BLOCK_KINDS for i, recs in enumerate(m.module.node_records)]
+    segs = []
+    for i, f in enumerate(is_blk):
+        if segs and segs[-1][2] == f:
+            segs[-1][1] = i + 1
+        else:
+            segs.append([i, i + 1, f])
+    blk_segs = [sg for sg in segs if sg[2]]
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in blk_segs]
+    step_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    blk_ms, step_ms = 0.0, 0.0
     for _ in range(args.steps):
-        m.run(trace=False)
-        node_ms += np.array(m.module.node_times())
-    m.module.set_profiling(False)
-    node_ms /= max(args.steps, 1)
+        step_ev[0].record(stream)
+        k = 0
+        for b, e, f in segs:
+            if f:
+                evs[k][0].record(stream)
+                m.module.run_range(b, e, stream)
+                evs[k][1].record(stream)
+                k += 1
+            else:
+                m.module.run_range(b, e, stream)
+        step_ev[1].record(stream)
+        step_ev[1].synchronize()
+        blk_ms += sum(a.elapsed_time(z) for a, z in evs)
+        step_ms += step_ev[0].elapsed_time(step_ev[1])
+    blk_ms /= max(args.steps, 1)
+    step_ms /= max(args.steps, 1)
 
     # ---- roofline of the dominant kernel: the fused MFMA conv/dense layer block
     # (qnn.conv2d|dense -> bias_add -> requantize [-> qnn.add(residual)] [-> clip] in one
     # kernel).  It is bound by HBM: every op output of the block is a trace record that must
     # be written (int32 conv + int32 bias_add + int8 requantize [+ int8 add] + int8 clip per
     # output element); algorithmic bytes = input + weights + bias [+ residual] + records.
-    blk_ops, blk_bytes, blk_ms, n_launch = 0.0, 0.0, 0.0, 0
+    blk_ops, blk_bytes, n_launch = 0.0, 0.0, 0
     ops_by_name = {o.name: o for o in m.plan.ops}
     for i, recs in enumerate(m.module.node_records):
-        if not recs or m.module.node_kinds[i] not in ("conv_block", "dense_block", "qnn.conv2d", "qnn.dense"):
+        if not is_blk[i]:
             continue
         op = ops_by_name[recs[0]]
         xin = m.plan.tensor(op.inputs[0])
@@ -384,11 +411,10 @@ def main(argv=None) -> int:
         res_bytes = sum(ops_by_name[r].out.nbytes for r in recs if ops_by_name[r].op == "qnn.add")
         blk_bytes += xin.nbytes + w.nbytes + (4 * op.out.shape[1] if len(recs) > 1 else 0) + rec_bytes + res_bytes
         blk_ops += 2.0 * macs
-        blk_ms += node_ms[i]
         n_launch += 1
     achieved_bw = blk_bytes / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
     achieved_ops = blk_ops / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
-    total_ms = float(node_ms.sum())
+    total_ms = step_ms
     traffic, traffic_src = pmc_traffic(args.model, B, n_launch)
 
     # ---- trace-digest all-gather (RCCL over xGMI): one u64 record digest per rank, computed
@@ -501,7 +527,8 @@ def main(argv=None) -> int:
             "extra": {
                 "compute_only_ms_per_step": round(compute_ms, 3),
                 "compute_only_traces_per_s": round(B * world / (compute_ms * 1e-3), 1),
-                "all_node_ms_per_step": round(total_ms, 3),
+                "compute_step_device_ms": round(total_ms, 3),
+                "block_segments": len(blk_segs),
                 "trace_bytes_per_step": trace_bytes,
                 "trace_GBps_per_gpu": round(trace_bytes / (elapsed_max / args.steps) / 1e9, 2),
                 "macs_per_sample": macs_per_sample,

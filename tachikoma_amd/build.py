@@ -32,7 +32,7 @@ ARCH = "gfx950"
 SOURCES = ["tk_host.cc", "tk_calibrate.cc", "tk_format.cc", "tk_runtime.cc", "tk_elementwise.hip", "tk_gemm.hip",
            "tk_residual.hip", "tk_realize.hip"]
 HEADERS = ["tk_common.h"]
-BASE_FLAGS = ["-std=c++17", "-O3", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-Wall",
+BASE_FLAGS = ["-std=c++20", "-O3", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-Wall",
               "-Wno-unused-function"]
 
 

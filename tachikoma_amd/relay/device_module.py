@@ -502,6 +502,11 @@ class DeviceModule:
         else:
             _lib.check(self.lib.tk_module_run(self.handle, ctypes.c_void_p(s), None, None), "tk_module_run")
 
+    def run_range(self, begin: int, end: int, stream=None) -> None:
+        """Nodes [begin, end) only, on ``stream`` (tk_module_run_range; no capture)."""
+        _lib.check(self.lib.tk_module_run_range(self.handle, int(begin), int(end),
+                                                ctypes.c_void_p(_lib.stream_handle(stream))), "tk_module_run_range")
+
     def run_profiled(self, stream=None) -> Dict[str, float]:
         ms = (ctypes.c_float * self.n_nodes)()
         _lib.check(self.lib.tk_module_run_profiled(self.handle, ctypes.c_void_p(_lib.stream_handle(stream)), ms),

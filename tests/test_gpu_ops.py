@@ -261,6 +261,62 @@ BLOCK_CASES = [
 ]
 
 
+# stride-1 3x3 blocks with 64-channel multiples take the halo-tile kernel (conv3x3_halo_kernel):
+# whole-image tiles (several images per tile on small planes, last tile partial) and row-band
+# tiles (28x28: 7-row bands, 56x56: 4-row bands), both 4-column fragment counts
+HALO_CASES = [
+    # N, C, H, O, dx, za, out_dtype, clip
+    (3, 64, 28, 128, "int8", -3, "int8", (0, 127)),
+    (2, 64, 56, 64, "int8", 4, "int8", (2, 127)),
+    (5, 256, 14, 256, "int8", 1, "int8", (0, 127)),
+    (3, 512, 7, 512, "int8", -2, "int8", (0, 127)),
+    (40, 64, 6, 64, "uint8", 131, "uint8", (128, 255)),
+    (1, 128, 14, 192, "uint8", 125, "uint8", None),
+    (2, 192, 20, 64, "int8", 0, "int8", (-7, 99)),
+]
+
+
+@pytest.mark.parametrize("case", HALO_CASES, ids=[f"halo{i}" for i in range(len(HALO_CASES))])
+def test_conv3x3_halo_block(tk, case):
+    n, c, h, o, dx, za, odt, clip = case
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
+    x = _rand(rng, (n, c, h, h), dx)
+    wt = _rand(rng, (o, c, 3, 3), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_in = rng.uniform(1e-5, 1e-3, size=o).astype(np.float32)
+    s_out = np.float32(0.01)
+    pad = (1, 1, 1, 1)
+    outs = tk.conv2d_block(x, wt, bias, za, 0, s_in, s_out, 3, clip=clip, padding=pad, out_dtype=odt,
+                           want_shadow=True)
+    conv = ref.qnn_conv2d(x, wt, za, 0, padding=pad)
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(3), axis=1, out_dtype=odt)
+    exp = [conv, badd, rq] + ([ref.clip(rq, *clip)] if clip is not None else [])
+    for got, e in zip(outs, exp):
+        np.testing.assert_array_equal(got, e)
+    np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
+
+
+@pytest.mark.parametrize("rounding", ["UPWARD", "TONEAREST"])
+def test_conv3x3_halo_shift_regimes(tk, rounding):
+    """The halo kernel's general requantize path (right shifts 0..8, left shifts) and the
+    TONEAREST rounding, against the oracle."""
+    rng = np.random.default_rng(78)
+    n, c, h, o = 2, 64, 14, 64
+    x = _rand(rng, (n, c, h, h), "int8")
+    wt = _rand(rng, (o, c, 3, 3), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_out = np.float32(0.5)
+    s_in = (np.geomspace(2.0 ** -8, 3.5, o) * s_out).astype(np.float32)
+    outs = tk.conv2d_block(x, wt, bias, 3, 0, s_in, s_out, -4, clip=(-128, 127), padding=(1, 1, 1, 1),
+                           rounding=rounding, want_shadow=True)
+    conv = ref.qnn_conv2d(x, wt, 3, 0, padding=(1, 1, 1, 1))
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(-4), axis=1, out_dtype="int8", rounding=rounding)
+    for got, e in zip(outs, [conv, badd, rq, rq]):
+        np.testing.assert_array_equal(got, e)
+
+
 def test_conv_block_requantize_shift_regimes(tk):
     """Per-channel multipliers spanning right shifts 0..8 and left shifts 1..2, so the block
     epilogue's mul_hi fast path (right shift >= 2) and the general int64 path both run,

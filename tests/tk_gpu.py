@@ -251,7 +251,7 @@ def _rq_attrs(r, keep, input_scale, output_scale, output_zero_point, rounding="U
 
 def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1, 1), padding=(0, 0, 0, 0),
                  dilation=(1, 1), groups=1, out_dtype="int8", want_shadow=False, residual=None, add_params=None,
-                 block_is_rhs=False):
+                 block_is_rhs=False, rounding="UPWARD"):
     """Fused conv -> bias_add -> requantize(axis 1) [-> qnn.add(., residual)] [-> clip] through
     tk_qnn_conv2d_block.  add_params = (ls, lz, rs, rz, os, oz) of the qnn.add (lhs = the block's
     requantize output unless block_is_rhs)."""
@@ -276,7 +276,7 @@ def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1,
     a.conv.input_zero_point = int(za)
     a.conv.kernel_zero_point = int(zw)
     keep = []
-    _rq_attrs(a.requantize, keep, s_in, s_out, zp_out)
+    _rq_attrs(a.requantize, keep, s_in, s_out, zp_out, rounding=rounding)
     if clip is not None:
         a.has_clip = 1
         a.clip_min, a.clip_max = clip

@@ -30,7 +30,7 @@ SHAPES = [  # name, C, H, O, K, stride, pad
 ]
 
 
-def main(batch=64, iters=20, configs=None, reps=3, only=None):
+def main(batch=64, iters=20, configs=None, reps=3, only=None, rotate=1):
     """configs: list of env-var dicts (TK_ABLATE / TK_NT are read per launch); each layer is
     timed for every config, interleaved `reps` times, and the minimum is reported."""
     import os
@@ -47,8 +47,12 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None):
         w = torch.from_numpy(rng.integers(-128, 128, size=(O, C, K, K)).astype(np.int8)).to(dev)
         b = torch.from_numpy(rng.integers(-2**14, 2**14, size=O).astype(np.int32)).to(dev)
         res = name.startswith("res ")
-        outs = [torch.empty((batch, O, OH, OH), dtype=t, device=dev)
-                for t in (torch.int32, torch.int32, torch.int8) + ((torch.int8,) if res else ()) + (torch.int8,)]
+        # rotate > 1: that many output sets, used in turn (fresh pages / cold caches per call,
+        # like the network, where every record has its own buffer)
+        out_sets = [[torch.empty((batch, O, OH, OH), dtype=t, device=dev)
+                     for t in (torch.int32, torch.int32, torch.int8) + ((torch.int8,) if res else ()) + (torch.int8,)]
+                    for _ in range(rotate)]
+        outs = out_sets[0]
         a = _lib.tk_block_attrs()
         a.conv.strides[:] = [S, S]
         a.conv.padding[:] = [P] * 4
@@ -74,8 +78,10 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None):
                 side.input_zero_point, side.output_zero_point = 1, 3
             a.add.output_zero_point = 3
         rx, rw, rb = [_lib.TensorRef.from_torch(t) for t in (x, w, b)]
-        refs = [_lib.TensorRef.from_torch(t) for t in outs]
-        arr = (ctypes.POINTER(_lib.tk_tensor) * len(refs))(*[r.ptr for r in refs])
+        ref_sets = [[_lib.TensorRef.from_torch(t) for t in o] for o in out_sets]
+        arrs = [(ctypes.POINTER(_lib.tk_tensor) * len(r))(*[x.ptr for x in r]) for r in ref_sets]
+        refs = ref_sets[0]
+        turn = [0]
         st = ctypes.c_void_p(_lib.stream_handle())
         shadow = torch.empty(lib.tk_conv2d_shadow_bytes(rx.ptr), dtype=torch.uint8, device=dev)
         packed = torch.empty(lib.tk_conv2d_packed_weight_bytes(rw.ptr, 1), dtype=torch.uint8, device=dev)
@@ -88,6 +94,8 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None):
                                              ctypes.c_void_p(sums.data_ptr()), st))
 
         def call():
+            arr = arrs[turn[0] % rotate]
+            turn[0] += 1
             _lib.check(lib.tk_qnn_conv2d_block(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), rw.ptr,
                                                ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(sums.data_ptr()),
                                                rb.ptr, arr, len(refs), ctypes.byref(a), ctypes.c_void_p(scratch.data_ptr()),
@@ -123,4 +131,5 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None):
 if __name__ == "__main__":
     import json
     cfgs = json.loads(sys.argv[1]) if len(sys.argv) > 1 else None
-    main(configs=cfgs, only=sys.argv[2] if len(sys.argv) > 2 else None)
+    main(configs=cfgs, only=sys.argv[2] if len(sys.argv) > 2 else None,
+         rotate=int(sys.argv[3]) if len(sys.argv) > 3 else 1)

@@ -1,9 +1,27 @@
 """Per-kernel durations from a rocprofv3 rocpd database (kernels view): consecutive runs of
 the same kernel/grid are grouped, with their average duration and the gap between launches.
-usage: python tools/rocpd_kernels.py <run_results.db> [name-regex]"""
+usage: python tools/rocpd_kernels.py <run_results.db> [name-regex] [--seq N]
+  --seq N: instead, list the last N matching launches one by one (duration and the idle gap
+  before each), e.g. one compute-only step of the network."""
 import re
 import sqlite3
 import sys
+
+
+def seq(db, pat, n):
+    cur = sqlite3.connect(db).cursor()
+    rows = cur.execute("select name, start, end, grid_x from kernels order by start").fetchall()
+    prev = None
+    out = []
+    for name, s, e, gx in rows:
+        if not pat or re.search(pat, name):
+            out.append((re.sub(r"\(.*", "", name)[:60], gx // 256, (e - s) / 1e3, (s - prev) / 1e3 if prev else 0.0))
+        prev = e
+    tot = 0.0
+    for i, (nm, g, d, gap) in enumerate(out[-n:]):
+        tot += d
+        print(f"{i:3d} {nm:60s} wg {g:6d} {d:8.2f} us  gap {gap:6.2f}")
+    print(f"sum {tot:.1f} us")
 
 
 def main(db, pat=None):
@@ -35,4 +53,8 @@ def main(db, pat=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    if "--seq" in sys.argv:
+        i = sys.argv.index("--seq")
+        seq(sys.argv[1], sys.argv[2] if i > 2 else None, int(sys.argv[i + 1]))
+    else:
+        main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
