@@ -1107,69 +1107,77 @@ gemm_i8_kernel(GemmArgs g) {
   }
 }
 
-// ---------------------------------------------------------------- 3x3 halo-tile conv block
-// Stride-1 3x3 convolutions (pad 1) of the small-plane stages read each input pixel 9 times
-// through the im2col gather above, and the LDS-DMA fill rate per CU (not HBM) bounds their
-// main loop (profiles/r02b_block_ablations.txt: 10 of the 14x14 layer's 30 us are loads).  This
-// kernel stages the tile's input patch plus its one-pixel halo in LDS ONCE, for all input
-// channels, and forms every tap's B fragment from it by address arithmetic:
-//   * tile = 64 output channels x a spatial patch: ipt whole images (planes <= 112 pixels) or a
-//     band of th output rows of one image; P <= 224 output pixels = up to 14 MFMA columns of 16;
-//   * LDS halo [cin_pad/16][ipt][hr][hc][16 B] (the shadow's channel-blocked chunks; taps
-//     outside the image hold the input zero point, so they contribute 0 after the fold);
-//   * 4 waves = 2 (32 rows each, two 16-row fragments) x 2 (column halves); the weight
-//     fragments come straight from the packed weights into registers (D steps in flight), so
-//     the K loop has no workgroup barrier at all; v_mfma_i32_16x16x64_i8;
-//   * epilogue: the 64 x P accumulator tile is staged in LDS (over the halo) and every record
-//     is written in runs that are contiguous in NCHW memory (a whole image's 64 channels, or one
-//     channel's band), 4 elements per lane, then the next conv's shadow.
-// Same arithmetic as gemm_i8_kernel's conv blocks (zero-point fold, bias_add, requantize, clip).
-struct HaloArgs {
-  int32_t nimg;            // images in the batch
-  int32_t ipt, th, bands;  // images per tile, output rows per tile, row bands per image
-  int32_t hr, hc, plane;   // halo rows / cols per image; LDS pixels per channel group (padded to 16)
-  int32_t pimg, p;         // output pixels per image-band and per tile
-  int32_t nf, nf0;         // 16-column fragments of the tile; of them, those of the wn = 0 waves
-  int32_t stride;          // int32 pitch of the LDS staging rows
-  int32_t tiles, tiles8;   // (ceil(nimg / ipt) * bands) * mtiles; rounded up to 8
-  int32_t steps, spt;      // 64-byte K steps; steps per tap (cin_pad / 64)
-  int32_t chunks;          // LDS-DMA chunks of the halo (cin_pad/16 * plane, rounded up to 64)
+// ---------------------------------------------------------------- patch-tile conv blocks
+// 1x1 and 3x3 conv blocks whose input channels come in 64-channel steps (every ResNet layer but
+// the stem).  The im2col kernel above ends every tile with one burst of record stores, in step
+// across the whole grid (each layer's workgroups run in one round), so the stores of a small-grid
+// layer do not overlap any loads or MFMAs, and a 3x3 layer re-reads each input pixel 9 times
+// through the per-CU LDS-DMA fill path (profiles/r02b_block_ablations.txt, r02f_*).  Here:
+//   * a workgroup owns one spatial patch (ipt whole images of <= 224 pixels, or a band of th
+//     output rows) and a range of output channels, walked as nsub sub-tiles of R = 32 MF rows;
+//   * the patch's input (plus the one-pixel halo of a 3x3, strided pixels of a strided 1x1) is
+//     staged in LDS ONCE for all input channels as the shadow's 16-byte chunks; every tap's B
+//     fragment is an address into it (taps outside the image hold the input zero point);
+//   * 4 waves = 2 (MF 16-row fragments each) x 2 (column halves); weight fragments go straight
+//     from the packed weights into registers, D steps ahead, so the K loop has no barrier;
+//     v_mfma_i32_16x16x64_i8;
+//   * each sub-tile's epilogue stages its accumulators in LDS and writes every record in runs
+//     that are contiguous NCHW memory (an image's R channels, or one channel's band), 4 elements
+//     per lane, then the next conv's shadow; the stores are asynchronous, so they drain while the
+//     waves run the next sub-tile's K loop;
+//   * qnn.add residual joins read the residual bytes into registers during the K loop.
+// Same arithmetic as gemm_i8_kernel's conv blocks (zero-point fold, bias_add, requantize, add, clip).
+struct PatchArgs {
+  int32_t nimg;               // images in the batch
+  int32_t ipt, th, bands;     // images per patch, output rows per patch, row bands per image
+  int32_t hr, hc, plane;      // patch rows / cols per image; LDS pixels per channel group (x16)
+  int32_t ih0s, rs, cs;       // input row of patch row 0 = oh0 * stride + ih0s; row / col step
+  int32_t ps;                 // patch pixels per output pixel step (3x3: the stride; 1x1: 1)
+  int32_t pimg, p;            // output pixels per image-band and per patch
+  int32_t nf, nf0;            // 16-column fragments of the patch; of them, the wn = 0 waves'
+  int32_t stride;             // int32 pitch of the LDS staging rows
+  int32_t mchunks, nsub;      // workgroups per patch (channel ranges), sub-tiles per workgroup
+  int32_t wgs, wgs8;          // spatial patches * mchunks; rounded up to 8
+  int32_t steps, spt;         // 64-byte K steps; steps per tap (cin_pad / 64)
+  int32_t chunks;             // LDS-DMA chunks of the patch (cin_pad/16 * plane, rounded up to 64)
   uint64_t mg_plane, mg_img, mg_hc, mg_pimg, mg_ow, mg_hw, mg_runq;  // (x * mg) >> 40 == x / d
-  int32_t runq;            // 4-element groups per epilogue run
-  int32_t whole;           // tiles hold whole images (run = an image's 64 channels), else a row band
-  int32_t rowc_off;        // LDS byte offset of the row constants (past the halo and the staging)
+  int32_t runq;               // 4-element groups per epilogue run
+  int32_t whole;              // whole-image patches (run = an image's R channels), else row bands
+  int32_t stage_off, rowc_off, lut_off;  // LDS byte offsets
 };
 
 __device__ __forceinline__ uint32_t fdiv40(uint32_t x, uint64_t mg) { return (uint32_t)(((uint64_t)x * mg) >> 40); }
 
-template <int NFW>
-__global__ __launch_bounds__(kGemmThreads, 2) void conv3x3_halo_kernel(GemmArgs g, HaloArgs h) {
+template <int MF, int NFW, int KT>
+__global__ __launch_bounds__(kGemmThreads, 2) void conv_patch_kernel(GemmArgs g, PatchArgs h) {
   extern __shared__ __attribute__((aligned(16))) int8_t hsm[];
   __shared__ int s_fast;
-  constexpr int MF = 2;  // 16-row fragments per wave
-  // K steps of weight fragments in flight per wave (covers the L2 latency; even, see below; 6 where
-  // 7 column fragments leave fewer registers)
-  constexpr int D = NFW >= 7 ? 6 : 8;
+  constexpr int R = 32 * MF;                 // rows of a sub-tile
+  constexpr int D = MF == 2 ? 4 : NFW >= 7 ? 6 : 8;  // weight steps in flight per wave (even, see the loop)
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches below
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
   const int wm = wave >> 1, wn = wave & 1;
   [[maybe_unused]] const int abl = g.ablate;
-  // XCD x runs a contiguous chunk of tiles, the M tiles of one patch adjacent (they share it in L2)
+  // XCD x runs a contiguous chunk of workgroups; those of one patch are adjacent (its input in L2)
   const int L = blockIdx.x;
-  const int t = (L & 7) * (h.tiles8 >> 3) + (L >> 3);
-  if (t >= h.tiles) return;
-  const int mtile = t % g.mtiles, sp = t / g.mtiles;
+  const int w = (L & 7) * (h.wgs8 >> 3) + (L >> 3);
+  if (w >= h.wgs) return;
+  const int mc = w % h.mchunks, sp = w / h.mchunks;
   const int band = sp % h.bands;
   const int img0 = (sp / h.bands) * h.ipt;
   const int nimg = min(h.ipt, h.nimg - img0);
-  const int m0 = mtile * 64;
   const int oh0 = band * h.th;
-  if (tid == 0) s_fast = 1;
+  const int mbase = mc * h.nsub * R;
+  int32_t* tileI = reinterpret_cast<int32_t*>(hsm + h.stage_off);
+  EpiRow* rowc = reinterpret_cast<EpiRow*>(hsm + h.rowc_off);
+  int32_t* lut = reinterpret_cast<int32_t*>(hsm + h.lut_off);
+  uint32_t* resw = reinterpret_cast<uint32_t*>(hsm + h.lut_off + 2048);  // residual words (joins only)
 
-  // ---- the halo: lane-linear LDS-DMA, chunk q = grp * plane + (kk * hr + r) * hc + c
+  // ---- the patch: lane-linear LDS-DMA, chunk q = grp * plane + (kk * hr + r) * hc + c
   {
     const int8_t* fill_src = reinterpret_cast<const int8_t*>(tk_fill_rows.v + 16 * (g.fill & 0xFFu));
     const int per_img = h.hr * h.hc;
+    const int ihb = oh0 * g.sh + h.ih0s, iwb = KT == 3 ? -g.pl : 0;
     for (int q0 = wave * 64; q0 < h.chunks; q0 += kGemmThreads) {
       const uint32_t q = q0 + lane;
       const uint32_t grp = fdiv40(q, h.mg_plane);
@@ -1178,7 +1186,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv3x3_halo_kernel(GemmArgs 
       if (grp < (uint32_t)g.cgroups && pix < (uint32_t)(h.ipt * per_img)) {
         const uint32_t kk = fdiv40(pix, h.mg_img), r = pix - kk * per_img;
         const uint32_t hrow = fdiv40(r, h.mg_hc), hcol = r - hrow * h.hc;
-        const int ih = oh0 - 1 + (int)hrow, iw = (int)hcol - 1;
+        const int ih = ihb + (int)hrow * h.rs, iw = iwb + (int)hcol * h.cs;
         const int img = img0 + (int)kk;
         if (img < h.nimg && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
           src = g.B + ((int64_t)grp * g.in_pix + ((int64_t)img * g.H + ih) * g.W + iw) * 16;
@@ -1186,224 +1194,260 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv3x3_halo_kernel(GemmArgs 
       if (!TK_ABL(256)) __builtin_amdgcn_global_load_lds((const void*)src, (void*)(hsm + q0 * 16), 16, 0, 0);
     }
   }
-  // ---- weight fragments: lane l holds row (l & 15) of a 16-row fragment, K bytes 16 (l >> 4) ..
-  const int8_t* ap[MF];
-#pragma unroll
-  for (int i = 0; i < MF; ++i)
-    ap[i] = g.A + (int64_t)(m0 + 32 * wm + 16 * i + (lane & 15)) * g.lda + 16 * (lane >> 4);
-  v4i abuf[D][MF];
-#pragma unroll
-  for (int u = 0; u < D; ++u)
-#pragma unroll
-    for (int i = 0; i < MF; ++i) abuf[u][i] = ldg(reinterpret_cast<const v4i*>(ap[i] + u * kBK));
-  // per-lane row constants of the epilogue, loaded now (they land during the K loop)
-  EpiRow row_pre{};
   const bool rq_axis = g.rq.mode >= TK_RQ_AXIS_UPWARD;
-  if (tid < 64) {
-    const int row = min(m0 + tid, g.M - 1);
-    row_pre.ra = (uint32_t)ldg(g.RA + row);
-    row_pre.bias = ldg(g.bias + row);
-    row_pre.m = ldg(rq_axis ? g.rq.ms + row : tk_zero_words);
-    row_pre.s = ldg(rq_axis ? g.rq.ss + row : tk_zero_words);
-    row_pre.zp = ldg(g.rq.zps ? g.rq.zps + row : tk_zero_words);
+  const bool has_add = g.has_add;
+  if (tid == 0) s_fast = 1;
+  if (has_add) {
+    // RequantizeOrUpcast of every 8-bit value of both qnn.add operands (op_common.h:186-200)
+    const int32_t x = g.rq.qmin == 0 ? tid : (int32_t)(int8_t)(uint8_t)tid;
+    lut[tid] = g.add_up_b ? x : rq_tensor(x, g.add_pb);
+    lut[256 + tid] = g.add_up_r ? x : rq_tensor(x, g.add_pr);
   }
-  // the halo chunks are this wave's oldest loads: wait for them, then for every wave's
-  wait_vm(0);
-  __syncthreads();
 
-  // ---- B fragments: column c = output pixel, lane l reads channel group (l >> 4) of its pixel's
-  // tap; byte offsets at tap (0, 0) / channel block 0, the step adds the rest.  Every wave runs
-  // NFW = nf0 fragments (the wn = 1 waves' surplus ones read a valid pixel and are not stored:
-  // the wn = 0 waves set the pace anyway), so the K loop has no lane-dependent branch.
+  // ---- per-lane constants of the K loop
   const int jbase = wn ? h.nf0 : 0;
-  int boff[NFW];
+  int boff[NFW];  // B fragment j: byte offset of the lane's pixel, channel group (lane >> 4), tap (0, 0)
 #pragma unroll
   for (int j = 0; j < NFW; ++j) {
     const uint32_t c = min((jbase + j) * 16 + (lane & 15), h.p - 1);
     const uint32_t kk = fdiv40(c, h.mg_pimg), r = c - kk * h.pimg;
     const uint32_t oh = fdiv40(r, h.mg_ow), ow = r - oh * g.OW;
-    boff[j] = (int)(((lane >> 4) * h.plane + (kk * h.hr + oh) * h.hc + ow) * 16);
+    boff[j] = (int)(((lane >> 4) * h.plane + (kk * h.hr + oh * h.ps) * h.hc + ow * h.ps) * 16);
   }
-  v4i acc[MF][NFW];
-#pragma unroll
-  for (int i = 0; i < MF; ++i)
-#pragma unroll
-    for (int j = 0; j < NFW; ++j) acc[i][j] = v4i{0};
-  const int cblk = 4 * h.plane * 16;  // bytes between 64-channel blocks of the halo
-  // B fragments double-buffered: step s + 1's are read from LDS while step s's MFMAs run.  Step s
-  // uses weight buffer s % D and B buffer s % 2; loads past the end re-read the last step, so the
-  // body has no branch and every wait is a counted one.
-  v4i b[2][NFW];
-#pragma unroll
-  for (int j = 0; j < NFW; ++j) b[0][j] = *reinterpret_cast<const v4i*>(hsm + boff[j]);
-  int c64 = 0, kh = 0, kw = 0;  // position of step s + 1
+  const int cblk = 4 * h.plane * 16;  // bytes between 64-channel blocks of the patch
   const int last = (h.steps - 1) * kBK;
-  auto step = [&](auto u_c, int s) __attribute__((always_inline)) {
-    constexpr int u = decltype(u_c)::value;
-    v4i a[MF];
+  const int hw = g.OH * g.OW, OW = g.OW, Mrows = g.M;
+  const int total = (h.whole ? nimg : R) * h.runq;  // epilogue groups of a sub-tile
+  v4i abuf[D][MF];
+  auto prefetch_a = [&](int m0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < MF; ++i) a[i] = abuf[u % D][i];
-    if (!TK_ABL(128)) {
+    for (int u = 0; u < D; ++u)
 #pragma unroll
       for (int i = 0; i < MF; ++i)
-        abuf[u % D][i] = ldg(reinterpret_cast<const v4i*>(ap[i] + min((s + D) * kBK, last)));
-    }
-    if (++c64 == h.spt) {
-      c64 = 0;
-      if (++kw == 3) kw = 0, ++kh;
-    }
-    const int soff = kh < 3 ? (kh * h.hc + kw) * 16 + c64 * cblk : 0;
-#pragma unroll
-    for (int j = 0; j < NFW; ++j) b[(u + 1) & 1][j] = *reinterpret_cast<const v4i*>(hsm + boff[j] + soff);
-    __builtin_amdgcn_sched_barrier(0);  // the next step's reads go out before this step's MFMAs
-    if (!TK_ABL(512)) {
-#pragma unroll
-      for (int j = 0; j < NFW; ++j)
-#pragma unroll
-        for (int i = 0; i < MF; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], b[u & 1][j], acc[i][j], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+        abuf[u][i] = ldg(reinterpret_cast<const v4i*>(g.A + (int64_t)(m0 + 16 * (MF * wm + i) + (lane & 15)) * g.lda +
+                                                      16 * (lane >> 4) + min(u * kBK, last)));
   };
-  // D steps per iteration (D is even, so B buffer parity carries over), then the tail guarded
-  int s0 = 0;
-  for (; s0 + D <= h.steps; s0 += D)
+  prefetch_a(mbase);
+  // the patch chunks are this wave's oldest loads; then every wave's
+  wait_vm(0);
+  __syncthreads();
+
+  for (int sub = 0; sub < h.nsub; ++sub) {
+    const int m0 = mbase + sub * R;
+    // row constants and residual bytes of this sub-tile: issued now, they land during the K loop
+    EpiRow row_pre{};
+    if (tid < R) {
+      const int row = min(m0 + tid, g.M - 1);
+      row_pre.ra = (uint32_t)ldg(g.RA + row);
+      row_pre.bias = ldg(g.bias + row);
+      row_pre.m = ldg(rq_axis ? g.rq.ms + row : tk_zero_words);
+      row_pre.s = ldg(rq_axis ? g.rq.ss + row : tk_zero_words);
+      row_pre.zp = ldg(g.rq.zps ? g.rq.zps + row : tk_zero_words);
+    }
+    if (has_add) {
+      if (sub > 0) lds_barrier();  // the previous sub-tile's epilogue is done reading resw
+      // the residual's 4-byte words of this sub-tile's epilogue groups, LDS-DMA'd in group order
+      // (group gi's word at resw[gi]); waited for before the epilogue
+      for (int q0 = wave * 64; q0 < total; q0 += kGemmThreads) {
+        const int gi = q0 + lane;
+        const int8_t* src = reinterpret_cast<const int8_t*>(tk_zero_words);
+        if (gi < total) {
+          const uint32_t run = fdiv40((uint32_t)gi, h.mg_runq);
+          const int f = (gi - (int)run * h.runq) * 4;
+          const uint32_t o = h.whole ? (uint32_t)(((img0 + (int)run) * Mrows + m0) * hw + f)
+                                     : (uint32_t)(((img0 * Mrows) + m0 + (int)run) * hw + oh0 * OW + f);
+          src = reinterpret_cast<const int8_t*>(g.add_res) + o;
+        }
+        __builtin_amdgcn_global_load_lds((const void*)src, (void*)(resw + q0), 4, 0, 0);
+      }
+    }
+
+    // ---- K loop: B fragments double-buffered (step s + 1's read while step s's MFMAs run); step
+    // s uses weight buffer s % D and B buffer s % 2; loads past the end re-read the last step, so
+    // the body has no branch and every wait is a counted one
+    v4i acc[MF][NFW];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int j = 0; j < NFW; ++j) acc[i][j] = v4i{0};
+    const int8_t* ap[MF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+      ap[i] = g.A + (int64_t)(m0 + 16 * (MF * wm + i) + (lane & 15)) * g.lda + 16 * (lane >> 4);
+    v4i b[2][NFW];
+#pragma unroll
+    for (int j = 0; j < NFW; ++j) b[0][j] = *reinterpret_cast<const v4i*>(hsm + boff[j]);
+    int c64 = 0, kh = 0, kw = 0;  // position of step s + 1
+    auto step = [&](auto u_c, int s) __attribute__((always_inline)) {
+      constexpr int u = decltype(u_c)::value;
+      v4i a[MF];
+#pragma unroll
+      for (int i = 0; i < MF; ++i) a[i] = abuf[u % D][i];
+      if (!TK_ABL(128)) {
+#pragma unroll
+        for (int i = 0; i < MF; ++i) abuf[u % D][i] = ldg(reinterpret_cast<const v4i*>(ap[i] + min((s + D) * kBK, last)));
+      }
+      if (++c64 == h.spt) {
+        c64 = 0;
+        if (KT == 3 && ++kw == 3) kw = 0, ++kh;
+      }
+      const int soff = (KT == 1 || kh < 3) ? (kh * h.hc + kw) * 16 + c64 * cblk : 0;
+#pragma unroll
+      for (int j = 0; j < NFW; ++j) b[(u + 1) & 1][j] = *reinterpret_cast<const v4i*>(hsm + boff[j] + soff);
+      __builtin_amdgcn_sched_barrier(0);  // the next step's reads go out before this step's MFMAs
+      if (!TK_ABL(512)) {
+#pragma unroll
+        for (int j = 0; j < NFW; ++j)
+#pragma unroll
+          for (int i = 0; i < MF; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], b[u & 1][j], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    int s0 = 0;
+    for (; s0 + D <= h.steps; s0 += D)
+      [&]<int... U>(std::integer_sequence<int, U...>) __attribute__((always_inline)) {
+        (step(std::integral_constant<int, U>{}, s0 + U), ...);
+      }(std::make_integer_sequence<int, D>{});
+    const int rem = h.steps - s0;
     [&]<int... U>(std::integer_sequence<int, U...>) __attribute__((always_inline)) {
-      (step(std::integral_constant<int, U>{}, s0 + U), ...);
-    }(std::make_integer_sequence<int, D>{});
-  const int rem = h.steps - s0;
-  [&]<int... U>(std::integer_sequence<int, U...>) __attribute__((always_inline)) {
-    ((rem > U ? step(std::integral_constant<int, U>{}, s0 + U) : void()), ...);
-  }(std::make_integer_sequence<int, D - 1>{});
-
-  // ---- epilogue: stage the tile (over the halo), row constants next to it
-  if (TK_ABL(4)) return;
-  int32_t* tileI = reinterpret_cast<int32_t*>(hsm);
-  EpiRow* rowc = reinterpret_cast<EpiRow*>(hsm + h.rowc_off);
-  lds_barrier();
-  if (tid < 64) {
-    EpiRow r = row_pre;
-    if (!rq_axis) r.m = g.rq.multiplier, r.s = g.rq.shift;
-    if (!g.rq.zps) r.zp = g.rq.zp_in;
-    r.fold = (uint32_t)0 - (uint32_t)g.zB * r.ra;  // zero weight zero point: the fold is -za * rowsum
-    if (r.s > -2) s_fast = 0;
-    rowc[tid] = r;
-  }
-#pragma unroll
-  for (int i = 0; i < MF; ++i)
-#pragma unroll
-    for (int j = 0; j < NFW; ++j) {
-      const int col = (jbase + j) * 16 + (lane & 15);
-      if (col < h.p && (wn == 0 || j < h.nf - h.nf0)) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) tileI[(32 * wm + 16 * i + 4 * (lane >> 4) + r) * h.stride + col] = acc[i][j][r];
-      }
-    }
-  lds_barrier();
-
-  const int hw = g.OH * g.OW, OW = g.OW;
-  const uint32_t n4 = g.out_elems * 4u;
-  const auto r_conv = rec_rsrc(g.C, n4), r_bias = rec_rsrc(g.bias_out, n4);
-  const auto r_rq = rec_rsrc(g.rq_out, g.out_elems);
-  const auto r_clip = rec_rsrc(g.clip_out, g.has_clip ? g.out_elems : 0u);
-  const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
-  const int32_t clip_lo = g.clip_lo, clip_hi = g.clip_hi;
-  const bool has_clip = g.has_clip;
-  const int mode = g.rq.mode, Mrows = g.M, stride = h.stride, whole = h.whole;
-  const int runq = h.runq;
-  const uint64_t mg_runq = h.mg_runq, mg_hw = h.mg_hw;
-  // runs (M % 64 == 0, so every tile has 64 rows): whole-image tiles: run k = image img0 + k, its
-  // channels m0.. x all hw pixels (contiguous); band tiles: run k = channel m0 + k, its pixels
-  // oh0 * OW .. (+ pimg)
-  const int total = (whole ? nimg : 64) * runq;
-  auto groups = [&](auto fast_c) __attribute__((always_inline)) {
-    constexpr bool FAST = decltype(fast_c)::value;
-    for (int gi = tid; gi < total; gi += kGemmThreads) {
-      const uint32_t k = fdiv40((uint32_t)gi, mg_runq);
-      const int f = (gi - (int)k * runq) * 4;
-      uint32_t o;
-      int row0, col0;
-      if (whole) {
-        o = (uint32_t)(((img0 + (int)k) * Mrows + m0) * hw + f);
-        row0 = (int)fdiv40((uint32_t)f, mg_hw);
-        col0 = (int)k * hw + (f - row0 * hw);
-      } else {
-        o = (uint32_t)(((img0 * Mrows) + m0 + (int)k) * hw + oh0 * OW + f);
-        row0 = (int)k;
-        col0 = f;
-      }
-      int slot[4];
-      EpiRow rr[4];
-      v4u v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int re = row0, ce = col0 + e;
-        if (whole) {
-#pragma unroll
-          for (int w = 0; w < 3; ++w)  // a run of 4 crosses at most 3 plane ends (hw >= 2)
-            if (ce - (int)k * hw >= hw) ce -= hw, ++re;
-        }
-        slot[e] = re * stride + ce;
-        rr[e] = rowc[re];
-        v[e] = (uint32_t)tileI[slot[e]];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += rr[e].fold;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += (uint32_t)rr[e].bias;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
-      int32_t q[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int32_t tt = (int32_t)(v[e] - (uint32_t)rr[e].zp);
-        int32_t y;
-        if constexpr (FAST) {
-          const int sh2 = -rr[e].s - 1;
-          y = (int32_t)((uint32_t)__mulhi(tt, rr[e].m) + (1u << (sh2 - 1))) >> sh2;
-        } else {
-          y = rq_core(tt, mode, rr[e].m, rr[e].s);
-        }
-        q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
-      }
-      __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
-      if (has_clip) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
-        __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) tileI[slot[e]] = q[e];
-    }
-  };
-  if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) groups(std::true_type{});
-  else groups(std::false_type{});
-
-  // ---- the next conv's shadow: 16 channels of one pixel per 16-byte store
-  if (g.shadow_out) {
+      ((rem > U ? step(std::integral_constant<int, U>{}, s0 + U) : void()), ...);
+    }(std::make_integer_sequence<int, D - 1>{});
+    if (TK_ABL(4)) continue;
+    // ---- epilogue: stage the sub-tile (the previous one's shadow pass must be done reading it);
+    // the residual words must have landed (the LDS-DMA is not tracked by the compiler's waits)
+    if (has_add) wait_vm(0);
+    // the next sub-tile's first weight steps land during this epilogue
+    if (sub + 1 < h.nsub) prefetch_a(m0 + R);
     lds_barrier();
-    const int items = 4 * h.p;
-    for (int it = tid; it < items; it += kGemmThreads) {
-      const int grp = it / h.p, col = it - grp * h.p;
-      const int ch0 = m0 + grp * 16;
-      const uint32_t kk = fdiv40((uint32_t)col, h.mg_pimg);
-      if ((int)kk >= nimg || ch0 >= g.shadow_cpad) continue;
-      const int pix = (img0 + (int)kk) * hw + oh0 * g.OW + (col - (int)kk * h.pimg);
-      uint32_t w[4];
+    if (tid < R) {
+      EpiRow r = row_pre;
+      if (!rq_axis) r.m = g.rq.multiplier, r.s = g.rq.shift;
+      if (!g.rq.zps) r.zp = g.rq.zp_in;
+      r.fold = (uint32_t)0 - (uint32_t)g.zB * r.ra;  // zero weight zero point: the fold is -za * rowsum
+      if (r.s > -2) s_fast = 0;
+      rowc[tid] = r;
+    }
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        uint32_t word = 0;
+    for (int i = 0; i < MF; ++i)
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const int ch = ch0 + d * 4 + qq;
-          uint32_t b = (uint32_t)tileI[(grp * 16 + d * 4 + qq) * stride + col] ^ g.shadow_xor;
-          if (ch >= g.M) b = 0;
-          word |= (b & 0xFFu) << (8 * qq);
+      for (int j = 0; j < NFW; ++j) {
+        const int col = (jbase + j) * 16 + (lane & 15);
+        if (col < h.p && (wn == 0 || j < h.nf - h.nf0)) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tileI[(16 * (MF * wm + i) + 4 * (lane >> 4) + r) * h.stride + col] = acc[i][j][r];
         }
-        w[d] = word;
       }
-      *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)(ch0 >> 4) * g.N + pix) * 16) =
-          v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    lds_barrier();
+
+    const uint32_t n4 = g.out_elems * 4u;
+    const auto r_conv = rec_rsrc(g.C, n4), r_bias = rec_rsrc(g.bias_out, n4);
+    const auto r_rq = rec_rsrc(g.rq_out, g.out_elems);
+    const auto r_add = rec_rsrc(g.add_out, has_add ? g.out_elems : 0u);
+    const auto r_clip = rec_rsrc(g.clip_out, g.has_clip ? g.out_elems : 0u);
+    const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
+    const int32_t clip_lo = g.clip_lo, clip_hi = g.clip_hi, add_zp = g.add_zp;
+    const bool has_clip = g.has_clip;
+    const int mode = g.rq.mode, stride = h.stride, whole = h.whole, runq = h.runq;
+    const uint64_t mg_runq = h.mg_runq, mg_hw = h.mg_hw;
+    // runs: whole-image patches: run k = image img0 + k, its channels m0 .. m0 + R x all hw pixels
+    // (contiguous); band patches: run k = channel m0 + k, its pixels oh0 * OW .. (+ pimg)
+    auto groups = [&](auto fast_c) __attribute__((always_inline)) {
+      constexpr bool FAST = decltype(fast_c)::value;
+      for (int gi = tid; gi < total; gi += kGemmThreads) {
+        const uint32_t k = fdiv40((uint32_t)gi, mg_runq);
+        const int f = (gi - (int)k * runq) * 4;
+        uint32_t o;
+        int row0, col0;
+        if (whole) {
+          o = (uint32_t)(((img0 + (int)k) * Mrows + m0) * hw + f);
+          row0 = (int)fdiv40((uint32_t)f, mg_hw);
+          col0 = (int)k * hw + (f - row0 * hw);
+        } else {
+          o = (uint32_t)(((img0 * Mrows) + m0 + (int)k) * hw + oh0 * OW + f);
+          row0 = (int)k;
+          col0 = f;
+        }
+        int slot[4];
+        EpiRow rr[4];
+        v4u v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int re = row0, ce = col0 + e;
+          if (whole) {
+#pragma unroll
+            for (int x = 0; x < 3; ++x)  // a run of 4 crosses at most 3 plane ends
+              if (ce - (int)k * hw >= hw) ce -= hw, ++re;
+          }
+          slot[e] = re * stride + ce;
+          rr[e] = rowc[re];
+          v[e] = (uint32_t)tileI[slot[e]];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += rr[e].fold;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (uint32_t)rr[e].bias;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
+        int32_t q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int32_t tt = (int32_t)(v[e] - (uint32_t)rr[e].zp);
+          int32_t y;
+          if constexpr (FAST) {
+            const int sh2 = -rr[e].s - 1;
+            y = (int32_t)((uint32_t)__mulhi(tt, rr[e].m) + (1u << (sh2 - 1))) >> sh2;
+          } else {
+            y = rq_core(tt, mode, rr[e].m, rr[e].s);
+          }
+          q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
+        if (has_add) {
+          // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((resw[gi] >> (8 * e)) & 0xFFu)] - add_zp, qmin, qmax);
+          __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
+        }
+        if (has_clip) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
+          __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tileI[slot[e]] = q[e];
+      }
+    };
+    if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) groups(std::true_type{});
+    else groups(std::false_type{});
+
+    // ---- the next conv's shadow: 16 channels of one pixel per 16-byte store
+    if (g.shadow_out) {
+      lds_barrier();
+      const int items = (R / 16) * h.p;
+      for (int it = tid; it < items; it += kGemmThreads) {
+        const int grp = it / h.p, col = it - grp * h.p;
+        const int ch0 = m0 + grp * 16;
+        const uint32_t kk = fdiv40((uint32_t)col, h.mg_pimg);
+        if ((int)kk >= nimg || ch0 >= g.shadow_cpad) continue;
+        const int pix = (img0 + (int)kk) * hw + oh0 * OW + (col - (int)kk * h.pimg);
+        uint32_t wd[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          uint32_t word = 0;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int ch = ch0 + d * 4 + qq;
+            uint32_t bb = (uint32_t)tileI[(grp * 16 + d * 4 + qq) * stride + col] ^ g.shadow_xor;
+            if (ch >= g.M) bb = 0;
+            word |= (bb & 0xFFu) << (8 * qq);
+          }
+          wd[d] = word;
+        }
+        *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)(ch0 >> 4) * g.N + pix) * 16) =
+            v4i{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+      }
     }
   }
 }
@@ -1933,66 +1977,100 @@ static bool conv_wide(const ConvGeom& g, bool block, int ipt) {
   return tiles <= env_int("TK_WIDE_MAX_TILES", 512);
 }
 
-// 3x3 halo-tile blocks (conv3x3_halo_kernel): stride-1, pad-1, undilated 3x3 conv blocks without a
-// kernel zero point or residual join, 64-channel multiples in and out.  The tile's pixel count P
-// (<= 224) is the largest that still gives every CU a tile (256 tiles), else the one with the
-// most tiles; LDS = max(halo, staging) + row constants.
-static bool halo_plan(const ConvGeom& g, const tk_conv2d_attrs* a, const BlockIO* blk, bool patch, HaloArgs* h,
-                      size_t* lds) {
-  if (!blk || patch || blk->attrs->has_add || !env_int("TK_HALO", 1)) return false;
-  if (g.KH != 3 || g.KW != 3 || a->strides[0] != 1 || a->strides[1] != 1 || a->dilation[0] != 1 ||
-      a->dilation[1] != 1 || a->padding[0] != 1 || a->padding[1] != 1 || a->padding[2] != 1 || a->padding[3] != 1)
+// Patch-tile blocks (conv_patch_kernel): 1x1 (pad 0) and 3x3 (pad 1) convs, stride 1 or 2, with
+// 64-channel input steps, 32-channel output multiples, no kernel zero point.  Candidate patches:
+// whole images (ipt of them, <= 224 pixels) or bands of th output rows (th | OH).  For each, the
+// channel range of a workgroup is split so that >= 256 workgroups run and each walks several
+// sub-tiles where it can (their stores drain under the next sub-tile's K loop); the largest patch
+// that reaches 256 workgroups wins (else the one with the most).
+struct PatchPlan {
+  PatchArgs a;
+  size_t lds;
+  int mf, nfw, kt;
+};
+
+static bool patch_plan(const ConvGeom& g, const tk_conv2d_attrs* a, const BlockIO* blk, bool patch, PatchPlan* out) {
+  // off by default: on ResNet-50's layers it measured slower than the im2col kernel at one
+  // workgroup per CU (profiles/r02g_patch_ab.txt); TK_PATCH=1 in the ablation build for A/Bs
+  if (!blk || patch || !env_int("TK_PATCH", 0)) return false;
+  const int st = a->strides[0];
+  if (a->strides[1] != st || (st != 1 && st != 2) || a->dilation[0] != 1 || a->dilation[1] != 1) return false;
+  int kt;
+  if (g.KH == 3 && g.KW == 3 && a->padding[0] == 1 && a->padding[1] == 1 && a->padding[2] == 1 && a->padding[3] == 1)
+    kt = 3;
+  else if (g.KH == 1 && g.KW == 1 && !a->padding[0] && !a->padding[1] && !a->padding[2] && !a->padding[3])
+    kt = 1;
+  else
     return false;
+  if (kt == 3 && !env_int("TK_PATCH3", 1)) return false;
+  if (kt == 1 && !env_int("TK_PATCH1", 1)) return false;
   const int64_t hw = (int64_t)g.OH * g.OW;
-  if (g.cin_pad % 64 || g.O % 64 || g.OH != g.H || g.OW != g.W || (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll)
-    return false;
-  const int mtiles = g.O / 64, cgroups = g.cin_pad / 16;
+  if (g.cin_pad % 64 || g.O % 32 || (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll) return false;
+  const int cgroups = g.cin_pad / 16;
+  const int R = g.O % 64 == 0 ? 64 : 32;
+  const int msub = g.O / R;
+  const bool add = blk->attrs->has_add;
   auto magic = [](uint64_t d) -> uint64_t { return ((1ull << 40) + d - 1) / d; };
   struct Cand {
     int ipt, th;
   };
-  Cand cands[64];
+  Cand cands[96];
   int nc = 0;
   for (int ipt = (int)std::min<int64_t>(224 / std::max<int64_t>(hw, 1), g.N); ipt >= 1 && nc < 32; --ipt)
-    cands[nc++] = {ipt, g.OH};  // whole images, largest first
+    cands[nc++] = {ipt, g.OH};
   if (hw % 4 == 0)
-    for (int th = g.OH - 1; th >= 1 && nc < 64; --th)
+    for (int th = g.OH - 1; th >= 1 && nc < 96; --th)
       if (g.OH % th == 0 && th * g.OW <= 224 && (th * g.OW) % 4 == 0) cands[nc++] = {1, th};
-  int pick = -1;
-  int64_t best_tiles = -1;
+  int pick = -1, pick_chunks = 1;
+  int64_t best = -1;
   for (int c = 0; c < nc; ++c) {
     const int ipt = cands[c].ipt, th = cands[c].th;
-    const int64_t tiles = ((g.N + ipt - 1) / ipt) * (int64_t)(g.OH / th) * mtiles;
-    const int hr = th + 2, hc = g.OW + 2;
+    const int hr = kt == 3 ? (th - 1) * st + 3 : th, hc = kt == 3 ? (g.OW - 1) * st + 3 : g.OW;
     const int plane = (ipt * hr * hc + 15) / 16 * 16;
     const int64_t chunks = ((int64_t)cgroups * plane + 63) / 64 * 64;
     const int p = ipt * th * g.OW;
     const int stride = (p + 31) / 32 * 32 + 4;
-    const size_t bytes = (size_t)std::max<int64_t>(chunks * 16, (int64_t)64 * stride * 4) + 64 * sizeof(EpiRow);
-    if (bytes > 160 * 1024 - 256 || p > 224) continue;  // (the static s_fast word shares the LDS)
-    if (tiles >= 256) {  // largest P that still fills the chip
-      pick = c;
+    const size_t bytes = (size_t)chunks * 16 + (size_t)R * stride * 4 + R * sizeof(EpiRow) + 2048 + (size_t)R * p + 256;
+    if (p > 224 || bytes > 160 * 1024 - 256) continue;
+    const int64_t spatial = ((g.N + ipt - 1) / ipt) * (int64_t)(g.OH / th);
+    // channel ranges per patch: the fewest that reach 256 workgroups (at most one per sub-tile)
+    int mchunks = msub;
+    for (int d = 1; d <= msub; ++d)
+      if (msub % d == 0 && spatial * d >= 256) {
+        mchunks = d;
+        break;
+      }
+    const int64_t wgs = spatial * mchunks;
+    if (wgs >= 256) {
+      pick = c, pick_chunks = mchunks;
       break;
     }
-    if (tiles > best_tiles) best_tiles = tiles, pick = c;
+    if (wgs > best) best = wgs, pick = c, pick_chunks = mchunks;
   }
   if (pick < 0) return false;
   const int ipt = cands[pick].ipt, th = cands[pick].th;
-  HaloArgs& x = *h;
+  PatchArgs& x = out->a;
+  x = PatchArgs{};
   x.nimg = g.N;
   x.ipt = ipt;
   x.th = th;
   x.bands = g.OH / th;
-  x.hr = th + 2;
-  x.hc = g.OW + 2;
+  x.hr = kt == 3 ? (th - 1) * st + 3 : th;
+  x.hc = kt == 3 ? (g.OW - 1) * st + 3 : g.OW;
   x.plane = (ipt * x.hr * x.hc + 15) / 16 * 16;
+  x.ih0s = kt == 3 ? -a->padding[0] : 0;
+  x.rs = kt == 3 ? 1 : st;
+  x.cs = kt == 3 ? 1 : st;
+  x.ps = kt == 3 ? st : 1;
   x.pimg = th * g.OW;
   x.p = ipt * x.pimg;
   x.nf = (x.p + 15) / 16;
   x.nf0 = (x.nf + 1) / 2;
   x.stride = (x.p + 31) / 32 * 32 + 4;
-  x.tiles = (int32_t)(((g.N + ipt - 1) / ipt) * (int64_t)x.bands * mtiles);
-  x.tiles8 = (x.tiles + 7) / 8 * 8;
+  x.mchunks = pick_chunks;
+  x.nsub = msub / pick_chunks;
+  x.wgs = (int32_t)(((g.N + ipt - 1) / ipt) * (int64_t)x.bands * pick_chunks);
+  x.wgs8 = (x.wgs + 7) / 8 * 8;
   x.steps = g.k_pad / kBK;
   x.spt = g.cin_pad / kBK;
   x.chunks = (int32_t)(((int64_t)cgroups * x.plane + 63) / 64 * 64);
@@ -2003,10 +2081,15 @@ static bool halo_plan(const ConvGeom& g, const tk_conv2d_attrs* a, const BlockIO
   x.mg_ow = magic(g.OW);
   x.mg_hw = magic(hw);
   x.whole = th == g.OH;
-  x.runq = x.whole ? (int32_t)(64 * hw / 4) : x.pimg / 4;
+  x.runq = x.whole ? (int32_t)(R * hw / 4) : x.pimg / 4;
   x.mg_runq = magic(x.runq);
-  x.rowc_off = (int32_t)std::max<int64_t>((int64_t)x.chunks * 16, (int64_t)64 * x.stride * 4);
-  *lds = (size_t)x.rowc_off + 64 * sizeof(EpiRow);
+  x.stage_off = x.chunks * 16;
+  x.rowc_off = x.stage_off + R * x.stride * 4;
+  x.lut_off = x.rowc_off + R * (int)sizeof(EpiRow);
+  out->lds = (size_t)x.lut_off + (add ? 2048 + (size_t)R * x.p + 256 : 0);  // LUTs + residual words
+  out->mf = R / 32;
+  out->nfw = x.nf0 <= 2 ? 2 : x.nf0 <= 4 ? 4 : 7;
+  out->kt = kt;
   return true;
 }
 
@@ -2191,22 +2274,29 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     ga.zA_vec = a->kernel_zero_points;
   }
   {
-    HaloArgs ha{};
-    size_t lds = 0;
-    if (halo_plan(g, a, blk, conv_needs_patch(weight, a), &ha, &lds)) {
-      auto kern = ha.nf0 <= 2 ? &conv3x3_halo_kernel<2> : ha.nf0 <= 4 ? &conv3x3_halo_kernel<4> : &conv3x3_halo_kernel<7>;
-      if (lds > 64 * 1024) {
+    PatchPlan pp;
+    if (patch_plan(g, a, blk, conv_needs_patch(weight, a), &pp)) {
+      using KFn = void (*)(GemmArgs, PatchArgs);
+      static const KFn kernels[2][3][2] = {
+          {{conv_patch_kernel<1, 2, 1>, conv_patch_kernel<1, 2, 3>},
+           {conv_patch_kernel<1, 4, 1>, conv_patch_kernel<1, 4, 3>},
+           {conv_patch_kernel<1, 7, 1>, conv_patch_kernel<1, 7, 3>}},
+          {{conv_patch_kernel<2, 2, 1>, conv_patch_kernel<2, 2, 3>},
+           {conv_patch_kernel<2, 4, 1>, conv_patch_kernel<2, 4, 3>},
+           {conv_patch_kernel<2, 7, 1>, conv_patch_kernel<2, 7, 3>}}};
+      const KFn kern = kernels[pp.mf - 1][pp.nfw == 2 ? 0 : pp.nfw == 4 ? 1 : 2][pp.kt == 3];
+      if (pp.lds > 64 * 1024) {
         // dynamic LDS beyond 64 KiB must be allowed per kernel (the static s_fast word counts too)
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pp.lds);
         if (e != hipSuccess) {
           (void)hipGetLastError();
-          set_error(std::string("conv3x3 halo: LDS attribute failed: ") + hipGetErrorString(e));
+          set_error(std::string("conv patch kernel: LDS attribute failed: ") + hipGetErrorString(e));
           return TK_ERR_HIP;
         }
       }
-      ga.mtiles = g.O / 64;
-      hipLaunchKernelGGL(kern, dim3((unsigned)ha.tiles8), dim3(kGemmThreads), lds, s, ga, ha);
+      ga.mtiles = g.O / 32;
+      hipLaunchKernelGGL(kern, dim3((unsigned)pp.a.wgs8), dim3(kGemmThreads), pp.lds, s, ga, pp.a);
       TK_LAUNCH_CHECK();
       return TK_OK;
     }

@@ -297,6 +297,54 @@ def test_conv3x3_halo_block(tk, case):
     np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
 
 
+# 1x1 / 3x3 blocks of every ResNet stage shape on the patch kernel: strided 1x1 (downsample) and
+# strided 3x3, residual joins on whole-image and row-band patches, several sub-tiles per
+# workgroup (the 1x1 expand layers), 32-row sub-tiles (96 channels), uint8
+PATCH_CASES = [
+    # N, C, H, O, K, stride, dx, za, residual add params or None, clip
+    (3, 256, 28, 512, 1, 2, "int8", -2, None, None),
+    (2, 512, 14, 1024, 1, 2, "int8", 3, None, None),
+    (3, 128, 28, 128, 3, 2, "int8", 1, None, (0, 127)),
+    (2, 512, 14, 512, 3, 2, "int8", -1, None, (0, 127)),
+    (3, 64, 56, 256, 1, 1, "int8", 2, (0.05, -3, 0.06, 4, 0.08, -1), (-1, 127)),
+    (2, 128, 28, 512, 1, 1, "int8", -4, (0.05, 3, 0.07, -2, 0.09, 1), (1, 127)),
+    (5, 256, 14, 1024, 1, 1, "int8", 1, (0.04, 0, 0.04, 0, 0.04, 0), (0, 127)),
+    (3, 512, 7, 2048, 1, 1, "uint8", 130, (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
+    (2, 1024, 14, 256, 1, 1, "int8", 2, None, (0, 127)),
+    (3, 2048, 7, 512, 1, 1, "int8", -3, None, (0, 127)),
+    (2, 64, 56, 64, 1, 1, "int8", 5, None, (0, 127)),
+    (4, 192, 10, 96, 3, 1, "int8", 0, (0.05, -3, 0.06, 4, 0.08, -1), None),
+]
+
+
+@pytest.mark.parametrize("case", PATCH_CASES, ids=[f"patch{i}" for i in range(len(PATCH_CASES))])
+def test_conv_patch_block(tk, case):
+    n, c, h, o, k, st, dt, za, ap, clip = case
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
+    x = _rand(rng, (n, c, h, h), dt)
+    wt = _rand(rng, (o, c, k, k), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_in = rng.uniform(1e-5, 1e-3, size=o).astype(np.float32)
+    s_out = np.float32(0.01)
+    p = k // 2
+    pad = (p, p, p, p)
+    oh = (h + 2 * p - k) // st + 1
+    residual = _rand(rng, (n, o, oh, oh), dt) if ap is not None else None
+    outs = tk.conv2d_block(x, wt, bias, za, 0, s_in, s_out, 3, clip=clip, strides=(st, st), padding=pad,
+                           out_dtype=dt, want_shadow=True, residual=residual, add_params=ap)
+    conv = ref.qnn_conv2d(x, wt, za, 0, strides=(st, st), padding=pad)
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(3), axis=1, out_dtype=dt)
+    exp = [conv, badd, rq]
+    if ap is not None:
+        exp.append(ref.qnn_add(rq, residual, *ap))
+    if clip is not None:
+        exp.append(ref.clip(exp[-1], *clip))
+    for got, e in zip(outs, exp):
+        np.testing.assert_array_equal(got, e)
+    np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
+
+
 @pytest.mark.parametrize("rounding", ["UPWARD", "TONEAREST"])
 def test_conv3x3_halo_shift_regimes(tk, rounding):
     """The halo kernel's general requantize path (right shifts 0..8, left shifts) and the
