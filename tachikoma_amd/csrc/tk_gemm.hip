@@ -94,6 +94,7 @@ struct GemmArgs {
   // tile's 64 channels x OH*OW pixels are one contiguous NCHW run: see the flat epilogue
   int32_t ipt, tcols;
   int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
+                       // 32768 flat epilogue without the row-uniform groups, 65536 skip the flat groups,
                        // 8192 residual join without the LUTs, 16384 skip the add record,
                        // 8/16/32/64 skip the conv / bias_add / requantize / clip record,
                        // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs, 1024 main-loop
@@ -346,7 +347,13 @@ __device__ __forceinline__ uint32_t pack4u(uint32_t a, uint32_t b, uint32_t c, u
   return lo | hi;
 }
 
-__device__ __forceinline__ int32_t clamp_i32(int32_t x, int32_t lo, int32_t hi) { return min(max(x, lo), hi); }
+// min(max(x, lo), hi) in one v_med3_i32 (the compiler only forms it for constant bounds); needs
+// lo <= hi, which setup_block guarantees for the clip bounds (see there) and the dtype ranges are
+__device__ __forceinline__ int32_t clamp_i32(int32_t x, int32_t lo, int32_t hi) {
+  int32_t r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+  return r;
+}
 
 // counted wait for this wave's global loads (vmcnt immediate): at most n outstanding
 __device__ __forceinline__ void wait_vm(int n) {
@@ -358,6 +365,8 @@ __device__ __forceinline__ void wait_vm(int n) {
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -365,12 +374,21 @@ __device__ __forceinline__ void wait_vm(int n) {
 // kWide (im2col LDS-DMA path): 128-byte K stages instead of 64, i.e. half the
 // barrier-separated steps of long reductions (each step pays a fixed LDS / barrier / address
 // latency that the 1-2 workgroups per CU of the small-grid layers cannot hide).
-template <int MT, bool kIm2col, bool kBlock, int kMode = 0, int kRing = 3, bool kWide = false>
-__global__ __launch_bounds__(kGemmThreads, MT == 1 ? (kWide ? 2 : kRing == 3 ? 4 : kRing == 4 ? 3 : 2) : 2) void
+// BN = 256 (image tiles of 65..256 pixels, conv blocks only): each wave owns 4 32-col tiles, and a
+// tile's 64 channels x one image are one contiguous run of every NCHW record (see the flat
+// epilogue): on 14x14 planes such runs store 2x faster than 128-column tiles that cross images
+// (tools/probe_store3.hip, profiles/r02j_store_patterns.txt).
+template <int MT, bool kIm2col, bool kBlock, int kMode = 0, int kRing = 3, bool kWide = false, int BN = 128>
+__global__ __launch_bounds__(kGemmThreads, BN == 256 ? (kWide ? 1 : 2)
+                                           : MT == 1 ? (kWide ? (kRing == 3 ? 2 : 1) : kRing == 3 ? 4 : kRing == 4 ? 3 : 2)
+                                                     : 2) void
 gemm_i8_kernel(GemmArgs g) {
-  static_assert(!kWide || (kIm2col && MT == 1 && kRing == 3), "wide stages: im2col, MT = 1, ring 3");
+  static_assert(!kWide || (kIm2col && MT == 1), "wide stages: im2col, MT = 1");
+  static_assert(BN == 128 || (BN == 256 && MT == 1 && kIm2col && kBlock && kMode == 0), "256-column tiles: conv blocks");
   constexpr int BM = 64 * MT;   // rows of A per block (2 waves along M, MT 32-row tiles each)
-  constexpr int BN = 128;       // rows of B per block (2 waves along N, 2 32-col tiles each)
+  constexpr int NJ = BN / 64;   // 32-col tiles per wave (2 waves along N)
+  constexpr int kStr = BN + 4;  // dwords per LDS row of the epilogue tile (breaks the 64-bank period)
+  constexpr int kFlat = BM * BN / 1024;  // 4-element groups per thread of the flat epilogue
   constexpr int A_CHUNKS = BM * kBK / 16 / kGemmThreads;  // 16-byte loads per thread per stage (plain path)
   constexpr int B_CHUNKS = BN * kBK / 16 / kGemmThreads;
   constexpr int SBK = kWide ? 2 * kBK : kBK;              // K bytes per stage
@@ -380,7 +398,7 @@ gemm_i8_kernel(GemmArgs g) {
   constexpr int kStageBytes = (BM + BN) * SBK;
   // kRing: LDS-DMA stages of the im2col path (kRing - 1 in flight); the plain path double-buffers
   constexpr int kStage = (kIm2col ? kRing : 2) * kStageBytes;
-  constexpr int kEpi = BM * kEpiStride * 4 + BM * (int)sizeof(EpiRow) + (kBlock ? 512 * 4 : 0);
+  constexpr int kEpi = BM * kStr * 4 + BM * (int)sizeof(EpiRow) + (kBlock ? 512 * 4 + 16 : 0);  // + flat sink slot
   __shared__ __attribute__((aligned(16))) int8_t smem[kStage > kEpi ? kStage : kEpi];
   __shared__ int s_fast;  // tile-uniform: every row's requantize takes the mul_hi form (shift <= -2)
   int8_t* As = smem;
@@ -418,21 +436,21 @@ gemm_i8_kernel(GemmArgs g) {
   // residual bytes of every row this thread writes (4-column epilogue paths), issued before
   // the main loop: they are older than every stage load, so the first stage wait also
   // covers them and the epilogue never waits on HBM latency
-  uint32_t resid_pre[BM / 8];
+  uint32_t resid_pre[kFlat > BM / 8 ? kFlat : BM / 8];
   if constexpr (kBlock && kMode != 1) {
     if (g.has_add && g.ipt) {
       // flat epilogue: 4 consecutive elements of an image run per group (see there)
       const int hw = g.OH * g.OW;
       const int run = min(BM, g.M - m0) * hw;
 #pragma unroll
-      for (int k = 0; k < BM / 8; ++k) {
+      for (int k = 0; k < kFlat; ++k) {
         const int gi = tid + kGemmThreads * k;
         const int kk = gi / (16 * hw), f = (gi - kk * 16 * hw) * 4;
         const int img = n0 / hw + kk;
         const bool ok = kk < g.ipt && img < g.N / hw && f < run;
         resid_pre[k] = ok ? ldg(reinterpret_cast<const uint32_t*>(g.add_res + ((int64_t)img * g.M + m0) * hw + f)) : 0u;
       }
-    } else if (g.has_add && g.vecw >= 4) {
+    } else if (BN == 128 && g.has_add && g.vecw >= 4) {
       const int hw = g.OH * g.OW;
       const int col = n0 + (tid & 31) * 4;
       const int img = col / hw;
@@ -498,11 +516,11 @@ gemm_i8_kernel(GemmArgs g) {
     }
   };
 
-  v16i acc[MT][2];
+  v16i acc[MT][NJ];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = v16i{0};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = v16i{0};
 
   // partial tiles live in g.ws in register order: v4i r4 of fragment (i, j) of thread tid
   constexpr int kTileInts = MT * 2 * 16 * kGemmThreads;
@@ -556,7 +574,7 @@ gemm_i8_kernel(GemmArgs g) {
   // LDS latency is not hidden by other waves)
   constexpr int KS = SBK / 32;  // K = 32 MFMA steps per stage
   struct Frags {
-    v4i a[KS][MT], b[KS][2];
+    v4i a[KS][MT], b[KS][NJ];
   };
   auto read_frags = [&](const int8_t* a, const int8_t* b, Frags& f) {
 #pragma unroll
@@ -568,8 +586,8 @@ gemm_i8_kernel(GemmArgs g) {
         f.a[ks][i] = *reinterpret_cast<const v4i*>(a + lds_off_w<SBK>(row, chunk));
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        int row = wn * 64 + j * 32 + (lane & 31);
+      for (int j = 0; j < NJ; ++j) {
+        int row = wn * (BN / 2) + j * 32 + (lane & 31);
         f.b[ks][j] = *reinterpret_cast<const v4i*>(b + lds_off_w<SBK>(row, chunk));
       }
     }
@@ -580,7 +598,7 @@ gemm_i8_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f.a[ks][i], f.b[ks][j], acc[i][j], 0, 0, 0);
   };
   auto mma_stage = [&](const int8_t* a, const int8_t* b) {
@@ -793,8 +811,8 @@ gemm_i8_kernel(GemmArgs g) {
   //      stores are contiguous (channel-blocked layout).
   if (g.ablate & 4) return;
   int32_t* tileI = reinterpret_cast<int32_t*>(smem);
-  EpiRow* rowc = reinterpret_cast<EpiRow*>(smem + BM * kEpiStride * 4);
-  int32_t* lut = reinterpret_cast<int32_t*>(smem + BM * kEpiStride * 4 + BM * sizeof(EpiRow));  // [2][256]
+  EpiRow* rowc = reinterpret_cast<EpiRow*>(smem + BM * kStr * 4);
+  int32_t* lut = reinterpret_cast<int32_t*>(smem + BM * kStr * 4 + BM * sizeof(EpiRow));  // [2][256]
   const int hw = g.OH * g.OW;
   const bool zb_vec = g.zB_vec != nullptr, has_rb = g.RB != nullptr;
   const bool simple_fold = !zb_vec && !has_rb;
@@ -820,12 +838,12 @@ gemm_i8_kernel(GemmArgs g) {
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int lc = wn * 64 + j * 32 + (lane & 31);
+    for (int j = 0; j < NJ; ++j) {
+      const int lc = wn * (BN / 2) + j * 32 + (lane & 31);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int lr = wm * 32 * MT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        tileI[lr * kEpiStride + lc] = acc[i][j][r];
+        tileI[lr * kStr + lc] = acc[i][j][r];
       }
     }
   }
@@ -833,7 +851,7 @@ gemm_i8_kernel(GemmArgs g) {
 
   bool done = false;
   if constexpr (kBlock) {
-    if (g.ipt && !(g.ablate & 0x7F)) {
+    if (g.ipt && (BN == 256 || !(g.ablate & 0x7F))) {
       // ---- flat epilogue (image-aligned tiles, planes of 1..64 pixels): for image kk of the
       // tile, its channels m0.. and all OH*OW pixels are one contiguous run of the NCHW
       // records, `run` elements long.  Group gi = 4 consecutive elements of one run: b128
@@ -853,34 +871,47 @@ gemm_i8_kernel(GemmArgs g) {
       const bool has_add = g.has_add, has_clip = g.has_clip;
       const int mode = g.rq.mode;
       const int ipt = g.ipt, Mrows = g.M;  // (the lambda must not reference g: that forces it to scratch)
-      auto groups = [&](auto fast_c) __attribute__((always_inline)) {
+      // x / hw as (x * mg) >> 40, exact for x * hw < 2^40 (x here < 2^16)
+      const uint64_t mg = ((1ull << 40) + (uint64_t)hw - 1) / (uint64_t)hw;
+      auto groups = [&](auto fast_c, auto rowu_c) __attribute__((always_inline)) {
         constexpr bool FAST = decltype(fast_c)::value;
+        // ROWU (hw % 4 == 0): a group's 4 elements lie in one row, 16-byte aligned in LDS: one
+        // b128 read of the tile, one row of constants
+        constexpr bool ROWU = decltype(rowu_c)::value;
 #pragma unroll
-        for (int k = 0; k < BM / 8; ++k) {
+        for (int k = 0; k < kFlat; ++k) {
           const int gi = tid + kGemmThreads * k;
-          const int kk = gi / (16 * hw), f = (gi - kk * 16 * hw) * 4;
+          const int kk = (int)((((uint64_t)(gi >> 4)) * mg) >> 40), f = (gi - kk * 16 * hw) * 4;
           if (!(kk < ipt && img0 + kk < nimg && f < run)) continue;  // past a run or the tile's images
           const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0) * hw + f);
-          const int r0 = f / hw, p0 = f - r0 * hw;
+          const int r0 = (int)(((uint64_t)f * mg) >> 40), p0 = f - r0 * hw;
           int slot[4];
           EpiRow rr[4];
           v4u v;
+          if constexpr (ROWU) {
+            slot[0] = r0 * kStr + kk * hw + p0;
+            rr[0] = rowc[r0];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            int re = r0, pe = p0 + e;
+            for (int e = 1; e < 4; ++e) slot[e] = slot[0] + e, rr[e] = rr[0];
+            v = *reinterpret_cast<const v4u*>(tileI + slot[0]);
+          } else {
 #pragma unroll
-            for (int w = 0; w < 3; ++w)  // one row change per group when hw >= 4, up to 3 below
-              if (pe >= hw) pe -= hw, ++re;
-            slot[e] = re * kEpiStride + kk * hw + pe;
-            rr[e] = rowc[re];
-            v[e] = (uint32_t)tileI[slot[e]];
+            for (int e = 0; e < 4; ++e) {
+              int re = r0, pe = p0 + e;
+#pragma unroll
+              for (int w = 0; w < 3; ++w)  // one row change per group when hw >= 4, up to 3 below
+                if (pe >= hw) pe -= hw, ++re;
+              slot[e] = re * kStr + kk * hw + pe;
+              rr[e] = rowc[re];
+              v[e] = (uint32_t)tileI[slot[e]];
+            }
           }
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += rr[e].fold;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
+          if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += (uint32_t)rr[e].bias;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
+          if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
           int32_t q[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -894,7 +925,7 @@ gemm_i8_kernel(GemmArgs g) {
             }
             q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
           }
-          __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
+          if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
           if (has_add) {
             // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
 #pragma unroll
@@ -903,20 +934,118 @@ gemm_i8_kernel(GemmArgs g) {
               q[e] = clamp_i32(TK_ABL(8192) ? q[e] + (int32_t)rb - add_zp : lut[q[e] & 0xFF] + lut[256 + rb] - add_zp,
                                qmin, qmax);
             }
-            if (!TK_ABL(16384)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
+            if (!TK_ABL(16384 | 2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
           }
           if (has_clip) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
-            __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
+            if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
           }
+          if constexpr (ROWU) {
+            *reinterpret_cast<v4i*>(tileI + slot[0]) = v4i{q[0], q[1], q[2], q[3]};
+          } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) tileI[slot[e]] = q[e];
+            for (int e = 0; e < 4; ++e) tileI[slot[e]] = q[e];
+          }
         }
       };
-      if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) groups(std::true_type{});
-      else groups(std::false_type{});
-    } else if (g.fast_epi && simple_fold && s_fast && !(g.ablate & 0x7F)) {
+      // Lean form for planes of >= 16 pixels, hw % 4 == 0 (the 14x14 256-column tiles, 8x8): the
+      // group -> (image, row, column) walk advances incrementally (256 groups = 1024 elements per
+      // step: dr rows + dp columns, at most one image wrap since an image run holds >= 256
+      // groups), one b128 LDS read of the 4 values and one row of constants per group, the
+      // residual join / clip decided at compile time.  The epilogue is VALU-issue-bound at the 1-2
+      // waves per SIMD of these launches (profiles/r02m_flat_epilogue_ablations.txt).
+      auto lean = [&](auto fast_c, auto add_c, auto clip_c) __attribute__((always_inline)) {
+        constexpr bool FAST = decltype(fast_c)::value, ADD = decltype(add_c)::value, CLIP = decltype(clip_c)::value;
+        const int runG = 16 * hw;             // 4-element groups per image run (BM = 64 rows)
+        const int dr = 1024 / hw, dp = 1024 - dr * hw;
+        // walk state of a group; its LDS slot is read unconditionally (in bounds of the epilogue
+        // area for every lane), lanes past a run store out of range and write back to the sink
+        int fg = tid, kk = 0;                  // group within the image run (tid < 256 <= runG)
+        int r0 = (int)(((uint64_t)(4 * fg) * mg) >> 40);
+        int p0 = 4 * fg - r0 * hw;
+        auto slot_of = [&]() __attribute__((always_inline)) { return r0 * kStr + kk * hw + p0; };
+        // software pipeline by one group: group k+1's tile values and row constants are read
+        // from LDS before group k's arithmetic and stores
+        int sl = slot_of();
+        v4u vn = *reinterpret_cast<const v4u*>(tileI + sl);
+        EpiRow rn = rowc[r0];
+#pragma unroll
+        for (int k = 0; k < kFlat; ++k) {
+          const bool ok = kk < ipt && img0 + kk < nimg && 4 * fg < run;
+          const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0) * hw + 4 * fg) | (ok ? 0u : kOffDrop);
+          int32_t* wslot = ok ? tileI + sl : lut + 512;
+          v4u v = vn;
+          const EpiRow rr = rn;
+          if (k + 1 < kFlat) {
+            fg += kGemmThreads;
+            r0 += dr;
+            p0 += dp;
+            if (p0 >= hw) p0 -= hw, ++r0;
+            if (fg >= runG) fg -= runG, ++kk, r0 -= BM;
+            sl = slot_of();
+            vn = *reinterpret_cast<const v4u*>(tileI + sl);
+            rn = rowc[r0];
+          }
+          v += rr.fold;
+          if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
+          v += (uint32_t)rr.bias;
+          if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
+          int32_t q[4];
+          if constexpr (FAST) {
+            const int sh2 = -rr.s - 1;
+            const uint32_t rnd = 1u << (sh2 - 1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              q[e] = clamp_i32(zpo + ((int32_t)((uint32_t)__mulhi((int32_t)(v[e] - (uint32_t)rr.zp), rr.m) + rnd) >> sh2),
+                               qmin, qmax);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)rq_core((int32_t)(v[e] - (uint32_t)rr.zp), mode, rr.m, rr.s)),
+                               qmin, qmax);
+          }
+          if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
+          if constexpr (ADD) {
+            // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
+            const uint32_t res = resid_pre[k];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((res >> (8 * e)) & 0xFFu)] - add_zp, qmin, qmax);
+            if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
+          }
+          if constexpr (CLIP) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
+            if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
+          }
+          *reinterpret_cast<v4i*>(wslot) = v4i{q[0], q[1], q[2], q[3]};
+        }
+      };
+      auto lean_fast = [&](auto fast_c) __attribute__((always_inline)) {
+        using T = std::true_type;
+        using F = std::false_type;
+        if (has_add) {
+          if (has_clip) lean(fast_c, T{}, T{});
+          else lean(fast_c, T{}, F{});
+        } else {
+          if (has_clip) lean(fast_c, F{}, T{});
+          else lean(fast_c, F{}, F{});
+        }
+      };
+      const bool fastrq = s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD);
+      if (TK_ABL(65536)) {
+      } else if (hw % 4 == 0 && hw >= 16 && !TK_ABL(32768)) {
+        if (fastrq) lean_fast(std::true_type{});
+        else lean_fast(std::false_type{});
+      } else if (hw % 4 == 0 && !TK_ABL(32768)) {
+        if (fastrq) groups(std::true_type{}, std::true_type{});
+        else groups(std::false_type{}, std::true_type{});
+      } else {
+        if (fastrq) groups(std::true_type{}, std::false_type{});
+        else groups(std::false_type{}, std::false_type{});
+      }
+    } else if (BN == 128 && g.fast_epi && simple_fold && s_fast && !(g.ablate & 0x7F)) {
       // ---- fast path (tile-uniform): 4 consecutive columns x rows (tid>>5) + 8k, every
       // record through a buffer descriptor (masked lanes get an out-of-range offset),
       // requantize in the mul_hi form: ((x - zp)·m + 2^(sh2-1)) >> sh2 over the high word
@@ -949,7 +1078,7 @@ gemm_i8_kernel(GemmArgs g) {
         for (int k = 0; k < BM / 8; ++k) {
           const int lr = (tid >> 5) + 8 * k;
           const EpiRow r = rowc[lr];
-          int32_t* slot = tileI + lr * kEpiStride + c4;
+          int32_t* slot = tileI + lr * kStr + c4;
           const v4i t = *reinterpret_cast<const v4i*>(slot);
           const uint32_t o = offs[k];
           // int32 wrap-around arithmetic in unsigned lanes (the reference accumulates mod 2^32)
@@ -1015,7 +1144,7 @@ gemm_i8_kernel(GemmArgs g) {
   };
   const bool store_on = !(g.ablate & 2);
   if (done) {
-  } else if (g.vecw >= 4) {
+  } else if (BN == 128 && g.vecw >= 4) {
     // 4 consecutive columns x rows (tid>>5) + 8k; the 4 never straddle an image plane
     const int c4 = (tid & 31) * 4;
     const int col = n0 + c4;
@@ -1040,14 +1169,14 @@ gemm_i8_kernel(GemmArgs g) {
       const bool ok = colok && row < g.M;
       const int64_t off = cbase + (int64_t)row * rstride;
       const uint32_t resid = (kBlock && g.has_add) ? resid_pre[k] : 0u;
-      int32_t* slot = tileI + lr * kEpiStride + c4;
+      int32_t* slot = tileI + lr * kStr + c4;
       const v4i t = *reinterpret_cast<const v4i*>(slot);
       int32_t v[4] = {t.x, t.y, t.z, t.w};
       fold(v, r, col, 4);
       epi_apply<4, kBlock>(g, r, v, off, store_on && ok, col, resid, lut, cc);
       if (kBlock && g.shadow_out) *reinterpret_cast<v4i*>(slot) = v4i{v[0], v[1], v[2], v[3]};
     }
-  } else {
+  } else if (BN == 128) {
     // one column x rows (tid>>7) + 2k (planes whose length is not a multiple of 4)
     const int lc = tid & (BN - 1);
     const int col = n0 + lc;
@@ -1069,7 +1198,7 @@ gemm_i8_kernel(GemmArgs g) {
       const int64_t off = cbase + (int64_t)row * rstride;
       uint32_t resid = 0;
       if (kBlock && g.has_add && ok) resid = g.add_res[off];
-      int32_t* slot = tileI + lr * kEpiStride + lc;
+      int32_t* slot = tileI + lr * kStr + lc;
       int32_t v[1] = {*slot};
       fold(v, r, col, 1);
       epi_apply<1, kBlock>(g, r, v, off, store_on && ok, col, resid, lut, &cc1);
@@ -1094,7 +1223,7 @@ gemm_i8_kernel(GemmArgs g) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int ch = ch0 + d * 4 + q;
-            uint32_t b = (uint32_t)tileI[(grp * 16 + d * 4 + q) * kEpiStride + lc] ^ g.shadow_xor;
+            uint32_t b = (uint32_t)tileI[(grp * 16 + d * 4 + q) * kStr + lc] ^ g.shadow_xor;
             if (ch >= g.M) b = 0;  // padded channels of a partial group stay zero
             word |= (b & 0xFFu) << (8 * q);
           }
@@ -1865,7 +1994,9 @@ static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out
   bool u8 = is_uint(rq, 8);
   int64_t lo = u8 ? 0 : -128, hi = u8 ? 255 : 127;
   ga.clip_lo = (int32_t)std::max(at->clip_min, lo);
-  ga.clip_hi = (int32_t)std::min(at->clip_max, hi);
+  // clip is max(min(x, a_max), a_min) (topi/math.py:634-638): a_min wins when a_min > a_max, which
+  // the kernels' min(max(x, lo), hi) reproduces with hi raised to lo (and clamp_i32 needs lo <= hi)
+  ga.clip_hi = (int32_t)std::max<int64_t>(std::min(at->clip_max, hi), ga.clip_lo);
   RqParams& p = ga.rq;
   p.mode = at->requantize.mode;
   p.multiplier = at->requantize.multiplier;
@@ -1951,11 +2082,14 @@ static bool conv_needs_patch(const tk_tensor* weight, const tk_conv2d_attrs* a) 
   return (a->kernel_zero_point - (is_uint(weight, 8) ? 128 : 0)) != 0 || a->kernel_zero_points;
 }
 
+static int conv_bn256_ipt(const ConvGeom& g, bool block, bool patch);
+
 // Images per N tile of a conv block whose planes hold 1..64 pixels (0: plain 128-column
 // tiles).  Needs the flat epilogue's preconditions: no per-pixel zero-point patch, a channel
 // count that keeps every image run 16-byte aligned, and 32-bit record offsets.
 static int conv_image_tiles(const ConvGeom& g, bool block, bool patch) {
   const int64_t hw = (int64_t)g.OH * g.OW;
+  if (const int ipt = conv_bn256_ipt(g, block, patch)) return ipt;
   if (!block || patch || hw > 64 || g.O % 4 != 0 || (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll ||
       !env_int("TK_IMGTILE", 1))
     return 0;
@@ -1966,15 +2100,34 @@ static int64_t conv_ntiles(const ConvGeom& g, int ipt) {
   return ipt ? ((int64_t)g.N + ipt - 1) / ipt : ((int64_t)g.N * g.OH * g.OW + 127) / 128;
 }
 
+// 256-column image tiles (BN = 256) for conv blocks whose planes hold 65..256 pixels (14x14):
+// floor(256 / HW) whole images per tile, so that each tile's records are contiguous runs
+// (probe: 2x the store rate of 128-column tiles that cross images on 14x14 planes,
+// profiles/r02j_store_patterns.txt).  Only where the grid still gives every CU a tile (no
+// split-K), with the flat epilogue's preconditions.  Returns images per tile, or 0.
+static int conv_bn256_ipt(const ConvGeom& g, bool block, bool patch) {
+  const int64_t hw = (int64_t)g.OH * g.OW;
+  // short reductions only (the store-bound expand layers): a long K loop at the one or two
+  // workgroups per CU of these tiles ran 15-20 % slower than 128-column tiles (3x3 256->256 and
+  // 1x1 1024->256 at 14x14, profiles/r02n_bn256_ab.txt)
+  if (!block || patch || hw <= 64 || hw > 256 || g.O % 4 != 0 || (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll ||
+      g.k_pad > env_int("TK_BN256_KMAX", 256) || !env_int("TK_BN256", 1))
+    return 0;
+  const int ipt = (int)(256 / hw);
+  const int64_t tiles = ((int64_t)g.N + ipt - 1) / ipt * ((g.O + 63) / 64);
+  return tiles >= 256 ? ipt : 0;
+}
+
 // Wide (128-byte) K stages for conv blocks with long reductions on small grids: >= 8 steps of
 // 64 bytes, every stage within one tap (cin_pad % 128 == 0), and few enough tiles that the
 // 2 workgroups per CU the wide ring's LDS allows hold the whole grid (TK_WIDE_MAX_TILES).
 static bool conv_wide(const ConvGeom& g, bool block, int ipt) {
-  if (!block || g.KH * g.KW > 64 || g.cin_pad % 128 != 0 || g.k_pad / kBK < 8 || ring_depth() != 3 ||
+  if (!block || g.KH * g.KW > 64 || g.cin_pad % 128 != 0 || g.k_pad / kBK < 8 ||
       !env_int("TK_WIDE", 1) || !env_int("TK_UNITAP", 1) || tune_env("TK_MT2"))
     return false;
   const int64_t tiles = conv_ntiles(g, ipt) * ((g.O + 63) / 64);
-  return tiles <= env_int("TK_WIDE_MAX_TILES", 512);
+  // (256-column tiles: the wide ring holds one workgroup per CU)
+  return tiles <= (conv_bn256_ipt(g, block, false) ? 256 : env_int("TK_WIDE_MAX_TILES", 512));
 }
 
 // Patch-tile blocks (conv_patch_kernel): 1x1 (pad 0) and 3x3 (pad 1) convs, stride 1 or 2, with
@@ -2305,6 +2458,7 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   const int ipt = mt1 ? conv_image_tiles(g, blk != nullptr, conv_needs_patch(weight, a)) : 0;
   ga.ipt = ipt;
   ga.tcols = ipt ? ipt * g.OH * g.OW : 128;
+  const bool bn256 = mt1 && conv_bn256_ipt(g, blk != nullptr, conv_needs_patch(weight, a)) != 0;
   ga.ntiles = (int32_t)conv_ntiles(g, ipt);
   ga.ntiles8 = (ga.ntiles + 7) / 8 * 8;
   ga.mtiles = (g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128);
@@ -2327,10 +2481,17 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     TK_LAUNCH_CHECK();
     if (blk) hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 2>), grid, dim3(kGemmThreads), 0, s, ga);
     else hipLaunchKernelGGL((gemm_i8_kernel<1, true, false, 2>), grid, dim3(kGemmThreads), 0, s, ga);
+  } else if (bn256) {
+    if (wide) hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 3, true, 256>), grid, dim3(kGemmThreads), 0, s, ga);
+    else hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 3, false, 256>), grid, dim3(kGemmThreads), 0, s, ga);
   } else if (mt1) {
     if (blk) {
       const unsigned pad = (unsigned)env_int("TK_LDS_PAD", 0);  // profiling: extra LDS per workgroup
-      if (wide) hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 3, true>), grid, dim3(kGemmThreads), pad, s, ga);
+      if (wide) switch (ring) {
+        case 4: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 4, true>), grid, dim3(kGemmThreads), pad, s, ga); break;
+        case 5: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 5, true>), grid, dim3(kGemmThreads), pad, s, ga); break;
+        default: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 3, true>), grid, dim3(kGemmThreads), pad, s, ga);
+      }
       else switch (ring) {
         case 4: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 4>), grid, dim3(kGemmThreads), pad, s, ga); break;
         case 5: hipLaunchKernelGGL((gemm_i8_kernel<1, true, true, 0, 5>), grid, dim3(kGemmThreads), pad, s, ga); break;

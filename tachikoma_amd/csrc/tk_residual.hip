@@ -241,7 +241,8 @@ int add_block_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* const* out
   int64_t lo = g.is_u8 ? 0 : -128, hi = g.is_u8 ? 255 : 127;
   g.has_clip = at->has_clip;
   g.clip_lo = (int32_t)std::max<int64_t>(at->has_clip ? at->clip_min : lo, lo);
-  g.clip_hi = (int32_t)std::min<int64_t>(at->has_clip ? at->clip_max : hi, hi);
+  // max(min(x, a_max), a_min) (topi/math.py:634-638): a_min wins when a_min > a_max
+  g.clip_hi = (int32_t)std::max<int64_t>(std::min<int64_t>(at->has_clip ? at->clip_max : hi, hi), g.clip_lo);
   g.zp_c = ad.output_zero_point;
   g.pa = add_rq(ad.lhs);
   g.pb = add_rq(ad.rhs);

@@ -258,6 +258,8 @@ BLOCK_CASES = [
     (2, 64, 56, 56, 64, 3, 1, 1, 64, "int8", 3, "int8", (0, 127)),    # depthwise band kernel, 4-pixel vectors, last band partial
     (1, 16, 112, 112, 16, 3, 2, 1, 16, "uint8", 130, "uint8", (128, 255)),  # depthwise stride 2, uint8
     (3, 32, 14, 14, 32, 3, 1, 1, 32, "int8", -4, "int8", None),       # depthwise, whole plane per group, scalar pixels
+    (2, 64, 7, 7, 64, 1, 1, 0, 1, "int8", 1, "int8", (100, 20)),      # a_min > a_max: clip gives a_min (flat epilogue)
+    (2, 64, 16, 16, 64, 1, 1, 0, 1, "uint8", 129, "uint8", (200, 150)),  # a_min > a_max, 4-column epilogue
 ]
 
 
@@ -420,6 +422,53 @@ def test_conv_block_residual_join(tk, case):
     exp = [conv, badd, rq, add]
     if clip is not None:
         exp.append(ref.clip(add, *clip))
+    for got, e in zip(outs, exp):
+        np.testing.assert_array_equal(got, e)
+    np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
+
+
+# 256-column image tiles (planes of 65..256 pixels, K <= 256, grids of >= 256 tiles): one image per
+# tile on 14x14 / 12x12 planes, two on 10x10 and three on 9x9 (last tile ragged), strided 1x1
+# (downsample 28 -> 14), residual joins, uint8, the general im2col walk (Cin not a multiple of 64)
+BN256_CASES = [
+    # N, C, H, O, K, stride, pad, dtype, residual add params or None, clip
+    (16, 64, 14, 1024, 1, 1, 0, "int8", (0.05, 3, 0.07, -2, 0.09, 1), (0, 127)),
+    (32, 256, 12, 512, 1, 1, 0, "int8", None, (0, 127)),
+    (33, 64, 10, 1024, 1, 1, 0, "uint8", (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
+    (16, 128, 28, 1024, 1, 2, 0, "int8", None, None),
+    (16, 512, 28, 1024, 1, 2, 0, "int8", None, (0, 127)),               # K = 512 (TK_BN256_KMAX A/Bs)
+    (48, 32, 9, 1024, 3, 1, 1, "int8", None, (-3, 120)),
+    (64, 256, 14, 256, 1, 1, 0, "int8", (0.04, 0, 0.04, 0, 0.04, 0), None),
+]
+
+
+@pytest.mark.parametrize("case", BN256_CASES, ids=[f"bn256_{i}" for i in range(len(BN256_CASES))])
+def test_conv_block_bn256(tk, case):
+    """Every record (and the shadow of the last one) of a block on 256-column image tiles
+    against the unfused oracle ops."""
+    n, c, h, o, k, s, p, dt, ap, clip = case
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
+    x = _rand(rng, (n, c, h, h), dt)
+    wt = _rand(rng, (o, c, k, k), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_in = rng.uniform(1e-5, 1e-3, size=o).astype(np.float32)
+    s_out = np.float32(0.01)
+    za = 130 if dt == "uint8" else 2
+    oh = (h + 2 * p - k) // s + 1
+    kw = dict(clip=clip, strides=(s, s), padding=(p, p, p, p), out_dtype=dt, want_shadow=True)
+    residual = None
+    if ap is not None:
+        residual = _rand(rng, (n, o, oh, oh), dt)
+        kw.update(residual=residual, add_params=ap, block_is_rhs=False)
+    outs = tk.conv2d_block(x, wt, bias, za, 0, s_in, s_out, 3, **kw)
+    conv = ref.qnn_conv2d(x, wt, za, 0, strides=(s, s), padding=(p, p, p, p))
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(3), axis=1, out_dtype=dt)
+    exp = [conv, badd, rq]
+    if ap is not None:
+        exp.append(ref.qnn_add(rq, residual, *ap))
+    if clip is not None:
+        exp.append(ref.clip(exp[-1], *clip))
     for got, e in zip(outs, exp):
         np.testing.assert_array_equal(got, e)
     np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))

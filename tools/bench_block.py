@@ -19,6 +19,8 @@ SHAPES = [  # name, C, H, O, K, stride, pad
     ("3x3 256->256 14", 256, 14, 256, 3, 1, 1),
     ("1x1 1024->256 14", 1024, 14, 256, 1, 1, 0),
     ("1x1 256->1024 14", 256, 14, 1024, 1, 1, 0),
+    ("ds 1x1 512->1024 s2 14", 512, 28, 1024, 1, 2, 0),
+    ("1x1 512->256 s2 14", 512, 28, 256, 1, 2, 0),
     ("3x3 512->512 7", 512, 7, 512, 3, 1, 1),
     ("1x1 512->2048 7", 512, 7, 2048, 1, 1, 0),
     ("1x1 2048->512 7", 2048, 7, 512, 1, 1, 0),
