@@ -2072,10 +2072,14 @@ struct SplitPlan {
 // 64-row (MT = 1) tiles for conv blocks, except 128-channel layers with K >= 512, where one
 // 128-row tile (MT = 2) per N tile measured 7-18% faster (ResNet-50's 28x28 stage: the B
 // operand is staged once for both M halves); plain convs use MT = 2 above 64 channels.
+// The 256-channel 3x3 layers of the 14x14 stage (K = 2304) also take 128-row tiles while the grid
+// keeps >= 192 of them: half the im2col B re-reads per CU, -10 % (profiles/r02q_mt2_ab.txt).
 static bool conv_mt1(const ConvGeom& g, bool block) {
   if (g.O <= 64) return true;
   if (!block || tune_env("TK_MT2")) return false;
-  return !(g.O == 128 && g.k_eff >= 512 && env_int("TK_MT2_128", 1));
+  if (g.O == 128 && g.k_eff >= 512 && env_int("TK_MT2_128", 1)) return false;
+  const int64_t mt2_tiles = ((int64_t)g.N * g.OH * g.OW + 127) / 128 * ((g.O + 127) / 128);
+  return !(g.O == 256 && g.k_eff >= 2048 && mt2_tiles >= 192 && env_int("TK_MT2_256", 1));
 }
 
 static bool conv_needs_patch(const tk_tensor* weight, const tk_conv2d_attrs* a) {

@@ -474,6 +474,31 @@ def test_conv_block_bn256(tk, case):
     np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
 
 
+@pytest.mark.parametrize("dt", ["int8", "uint8"])
+def test_conv_block_mt2_256(tk, dt):
+    """ResNet-50's 14x14 3x3 256->256 layer at batch 64 on 128-row tiles (K = 2304, 196 tiles): every
+    record and the shadow against the oracle (the C restatement of the conv, for its size)."""
+    from oracle import graph_ref
+    rng = np.random.default_rng(zlib.crc32(f"mt2_256 {dt}".encode()))
+    x = _rand(rng, (64, 256, 14, 14), dt)
+    wt = _rand(rng, (256, 256, 3, 3), "int8")
+    bias = rng.integers(-2**14, 2**14, size=256).astype(np.int32)
+    s_in = rng.uniform(1e-5, 1e-4, size=256).astype(np.float32)
+    s_out = np.float32(0.02)
+    za = 131 if dt == "uint8" else -3
+    clip = (128, 255) if dt == "uint8" else (0, 127)
+    outs = tk.conv2d_block(x, wt, bias, za, 0, s_in, s_out, 3, clip=clip, padding=(1, 1, 1, 1), out_dtype=dt,
+                           want_shadow=True)
+    conv = graph_ref._conv_c(x, wt, za, 0, {"strides": (1, 1), "dilation": (1, 1), "padding": (1, 1, 1, 1),
+                                            "groups": 1}, 16)
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(3), axis=1, out_dtype=dt)
+    exp = [conv, badd, rq, ref.clip(rq, *clip)]
+    for got, e in zip(outs, exp):
+        np.testing.assert_array_equal(got, e)
+    np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
+
+
 @pytest.mark.parametrize("case", BLOCK_CASES, ids=[f"block{i}" for i in range(len(BLOCK_CASES))])
 def test_conv_block_matches_unfused_ops(tk, case):
     n, c, h, w, o, k, s, p, g, dx, za, odt, clip = case
