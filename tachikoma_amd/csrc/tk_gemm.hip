@@ -389,6 +389,8 @@ gemm_i8_kernel(GemmArgs g) {
   constexpr int NJ = BN / 64;   // 32-col tiles per wave (2 waves along N)
   constexpr int kStr = BN + 4;  // dwords per LDS row of the epilogue tile (breaks the 64-bank period)
   constexpr int kFlat = BM * BN / 1024;  // 4-element groups per thread of the flat epilogue
+  // 4-column epilogues: kLPR lanes per tile row (4 columns each), kRPI rows per pass, kRows passes
+  constexpr int kLPR = BN / 4, kRPI = kGemmThreads / kLPR, kRows = BM / kRPI;
   constexpr int A_CHUNKS = BM * kBK / 16 / kGemmThreads;  // 16-byte loads per thread per stage (plain path)
   constexpr int B_CHUNKS = BN * kBK / 16 / kGemmThreads;
   constexpr int SBK = kWide ? 2 * kBK : kBK;              // K bytes per stage
@@ -436,7 +438,7 @@ gemm_i8_kernel(GemmArgs g) {
   // residual bytes of every row this thread writes (4-column epilogue paths), issued before
   // the main loop: they are older than every stage load, so the first stage wait also
   // covers them and the epilogue never waits on HBM latency
-  uint32_t resid_pre[kFlat > BM / 8 ? kFlat : BM / 8];
+  uint32_t resid_pre[kFlat > kRows ? kFlat : kRows];
   if constexpr (kBlock && kMode != 1) {
     if (g.has_add && g.ipt) {
       // flat epilogue: 4 consecutive elements of an image run per group (see there)
@@ -450,14 +452,14 @@ gemm_i8_kernel(GemmArgs g) {
         const bool ok = kk < g.ipt && img < g.N / hw && f < run;
         resid_pre[k] = ok ? ldg(reinterpret_cast<const uint32_t*>(g.add_res + ((int64_t)img * g.M + m0) * hw + f)) : 0u;
       }
-    } else if (BN == 128 && g.has_add && g.vecw >= 4) {
+    } else if (g.has_add && g.vecw >= 4) {
       const int hw = g.OH * g.OW;
-      const int col = n0 + (tid & 31) * 4;
+      const int col = n0 + (tid % kLPR) * 4;
       const int img = col / hw;
       const int64_t cbase = (int64_t)img * g.M * hw + (col - img * hw);
 #pragma unroll
-      for (int k = 0; k < BM / 8; ++k) {
-        const int row = m0 + (tid >> 5) + 8 * k;
+      for (int k = 0; k < kRows; ++k) {
+        const int row = m0 + tid / kLPR + kRPI * k;
         const bool ok = col < g.N && row < g.M;
         resid_pre[k] = ldg(reinterpret_cast<const uint32_t*>(g.add_res + (ok ? cbase + (int64_t)row * hw : 0)));
       }
@@ -1045,12 +1047,12 @@ gemm_i8_kernel(GemmArgs g) {
         if (fastrq) groups(std::true_type{}, std::false_type{});
         else groups(std::false_type{}, std::false_type{});
       }
-    } else if (BN == 128 && g.fast_epi && simple_fold && s_fast && !(g.ablate & 0x7F)) {
+    } else if (g.fast_epi && simple_fold && s_fast && !(g.ablate & 0x7F)) {
       // ---- fast path (tile-uniform): 4 consecutive columns x rows (tid>>5) + 8k, every
       // record through a buffer descriptor (masked lanes get an out-of-range offset),
       // requantize in the mul_hi form: ((x - zp)·m + 2^(sh2-1)) >> sh2 over the high word
       done = true;
-      const int c4 = (tid & 31) * 4;
+      const int c4 = (tid % kLPR) * 4;
       const int col = n0 + c4;
       const bool colok = col < g.N;
       const int img = col / hw;
@@ -1065,18 +1067,18 @@ gemm_i8_kernel(GemmArgs g) {
       // store, the compiler reloads them (s_load + lgkmcnt(0), which also drains the LDS reads)
       const int32_t add_zp = g.add_zp, clip_lo = g.clip_lo, clip_hi = g.clip_hi;
       const bool want_shadow = g.shadow_out != nullptr;
-      uint32_t offs[BM / 8];
+      uint32_t offs[kRows];
 #pragma unroll
-      for (int k = 0; k < BM / 8; ++k) {
-        const int row = m0 + (tid >> 5) + 8 * k;
+      for (int k = 0; k < kRows; ++k) {
+        const int row = m0 + tid / kLPR + kRPI * k;
         offs[k] = (colok && row < g.M) ? cbase + (uint32_t)row * (uint32_t)hw : kOffDrop;
       }
       auto rows = [&](auto add_c, auto clip_c, auto aux_c) __attribute__((always_inline)) {
         constexpr bool ADD = decltype(add_c)::value, CLIP = decltype(clip_c)::value;
         constexpr int AUX = decltype(aux_c)::value;
 #pragma unroll
-        for (int k = 0; k < BM / 8; ++k) {
-          const int lr = (tid >> 5) + 8 * k;
+        for (int k = 0; k < kRows; ++k) {
+          const int lr = tid / kLPR + kRPI * k;
           const EpiRow r = rowc[lr];
           int32_t* slot = tileI + lr * kStr + c4;
           const v4i t = *reinterpret_cast<const v4i*>(slot);
@@ -1144,9 +1146,10 @@ gemm_i8_kernel(GemmArgs g) {
   };
   const bool store_on = !(g.ablate & 2);
   if (done) {
-  } else if (BN == 128 && g.vecw >= 4) {
-    // 4 consecutive columns x rows (tid>>5) + 8k; the 4 never straddle an image plane
-    const int c4 = (tid & 31) * 4;
+  } else if (g.vecw >= 4) {
+    // 4 consecutive columns x rows (tid>>5) + 8k (BN = 256: (tid>>6) + 4k); the 4 never straddle
+    // an image plane
+    const int c4 = (tid % kLPR) * 4;
     const int col = n0 + c4;
     const bool colok = col < g.N;
     int64_t cbase, rstride;
@@ -1162,8 +1165,8 @@ gemm_i8_kernel(GemmArgs g) {
     if (kBlock && !g.ch_is_row)
       for (int q = 0; q < 4; ++q) cc[q] = col_consts(g, col + q);
 #pragma unroll
-    for (int k = 0; k < BM / 8; ++k) {
-      const int lr = (tid >> 5) + 8 * k;
+    for (int k = 0; k < kRows; ++k) {
+      const int lr = tid / kLPR + kRPI * k;
       const int row = m0 + lr;
       const EpiRow r = rowc[lr];
       const bool ok = colok && row < g.M;
@@ -2088,6 +2091,21 @@ static bool conv_needs_patch(const tk_tensor* weight, const tk_conv2d_attrs* a) 
 
 static int conv_bn256_ipt(const ConvGeom& g, bool block, bool patch);
 
+// 256-column tiles over the flattened pixel axis (BN = 256, no image alignment) for the short-K,
+// >= 256-channel conv blocks on planes of more than 256 pixels (the 56x56 / 28x28 expand and
+// downsample layers): each store instruction writes one 1 KB segment of a channel row instead of
+// two 512-byte ones (store probe: -10 % on these layers' record writes,
+// profiles/r02j_store_patterns.txt "span 64x256").  Off (TK_BN256_ROWS=1 in the ablation build):
+// on the kernel the halved occupancy (2 workgroups per CU for 70 KB of LDS) costs more than the
+// store pattern gains, the 56x56 expand with its residual join +19 % (profiles/r02s_bn256_rows_ab.txt).
+static bool conv_bn256_rows(const ConvGeom& g, bool block, bool patch) {
+  const int64_t hw = (int64_t)g.OH * g.OW, P = (int64_t)g.N * hw;
+  if (!block || patch || hw <= 256 || hw % 4 != 0 || g.O < 256 || g.k_pad > 256 ||
+      P * g.O * 4 >= 0xFFFFFFC0ll || !env_int("TK_BN256_ROWS", 0))
+    return false;
+  return (P + 255) / 256 * ((g.O + 63) / 64) >= 256;
+}
+
 // Images per N tile of a conv block whose planes hold 1..64 pixels (0: plain 128-column
 // tiles).  Needs the flat epilogue's preconditions: no per-pixel zero-point patch, a channel
 // count that keeps every image run 16-byte aligned, and 32-bit record offsets.
@@ -2461,9 +2479,10 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   const bool mt1 = conv_mt1(g, blk != nullptr);
   const int ipt = mt1 ? conv_image_tiles(g, blk != nullptr, conv_needs_patch(weight, a)) : 0;
   ga.ipt = ipt;
-  ga.tcols = ipt ? ipt * g.OH * g.OW : 128;
-  const bool bn256 = mt1 && conv_bn256_ipt(g, blk != nullptr, conv_needs_patch(weight, a)) != 0;
-  ga.ntiles = (int32_t)conv_ntiles(g, ipt);
+  const bool bn_rows = mt1 && !ipt && conv_bn256_rows(g, blk != nullptr, conv_needs_patch(weight, a));
+  ga.tcols = ipt ? ipt * g.OH * g.OW : bn_rows ? 256 : 128;
+  const bool bn256 = bn_rows || (mt1 && conv_bn256_ipt(g, blk != nullptr, conv_needs_patch(weight, a)) != 0);
+  ga.ntiles = bn_rows ? (int32_t)((P + 255) / 256) : (int32_t)conv_ntiles(g, ipt);
   ga.ntiles8 = (ga.ntiles + 7) / 8 * 8;
   ga.mtiles = (g.O + (mt1 ? 63 : 127)) / (mt1 ? 64 : 128);
   dim3 grid((unsigned)((int64_t)ga.mtiles * ga.ntiles8));

@@ -439,6 +439,12 @@ BN256_CASES = [
     (16, 512, 28, 1024, 1, 2, 0, "int8", None, (0, 127)),               # K = 512 (TK_BN256_KMAX A/Bs)
     (48, 32, 9, 1024, 3, 1, 1, "int8", None, (-3, 120)),
     (64, 256, 14, 256, 1, 1, 0, "int8", (0.04, 0, 0.04, 0, 0.04, 0), None),
+    # planes > 256 pixels, >= 256 channels (256-column row tiles with TK_BN256_ROWS=1 in the
+    # ablation build, 128-column tiles in the product): tiles cross images, the last one ragged;
+    # residual join, uint8, strided downsample
+    (2, 64, 96, 256, 1, 1, 0, "int8", (0.05, 3, 0.07, -2, 0.09, 1), (0, 127)),
+    (12, 128, 28, 512, 1, 1, 0, "uint8", (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
+    (12, 256, 56, 512, 1, 2, 0, "int8", None, None),
 ]
 
 
