@@ -94,7 +94,8 @@ struct GemmArgs {
   // tile's 64 channels x OH*OW pixels are one contiguous NCHW run: see the flat epilogue
   int32_t ipt, tcols;
   int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
-                       // 32768 flat epilogue without the row-uniform groups, 65536 skip the flat groups,
+                       // 32768 flat epilogue without the lean groups, 65536 skip the flat groups,
+                       // 131072 flat epilogue without the lean row-crossing groups (hw % 4 != 0),
                        // 8192 residual join without the LUTs, 16384 skip the add record,
                        // 8/16/32/64 skip the conv / bias_add / requantize / clip record,
                        // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs, 1024 main-loop
@@ -957,8 +958,11 @@ gemm_i8_kernel(GemmArgs g) {
       // groups), one b128 LDS read of the 4 values and one row of constants per group, the
       // residual join / clip decided at compile time.  The epilogue is VALU-issue-bound at the 1-2
       // waves per SIMD of these launches (profiles/r02m_flat_epilogue_ablations.txt).
-      auto lean = [&](auto fast_c, auto add_c, auto clip_c) __attribute__((always_inline)) {
+      // XR (hw % 4 != 0, the 7x7 stage): a group may cross into the next row; its elements then
+      // take that row's constants (per-element selects) and four b32 tile reads.
+      auto lean = [&](auto fast_c, auto add_c, auto clip_c, auto xr_c) __attribute__((always_inline)) {
         constexpr bool FAST = decltype(fast_c)::value, ADD = decltype(add_c)::value, CLIP = decltype(clip_c)::value;
+        constexpr bool XR = decltype(xr_c)::value;
         const int runG = 16 * hw;             // 4-element groups per image run (BM = 64 rows)
         const int dr = 1024 / hw, dp = 1024 - dr * hw;
         // walk state of a group; its LDS slot is read unconditionally (in bounds of the epilogue
@@ -967,18 +971,32 @@ gemm_i8_kernel(GemmArgs g) {
         int r0 = (int)(((uint64_t)(4 * fg) * mg) >> 40);
         int p0 = 4 * fg - r0 * hw;
         auto slot_of = [&]() __attribute__((always_inline)) { return r0 * kStr + kk * hw + p0; };
+        // element e of a group starting at column p0 lies in the next row when p0 + e >= hw
+        auto load = [&](int sl, int r, int p, v4u& v, EpiRow& ra, EpiRow& rb) __attribute__((always_inline)) {
+          if constexpr (XR) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (uint32_t)tileI[sl + e + (p + e >= hw ? kStr - hw : 0)];
+            ra = rowc[r];
+            rb = rowc[min(r + 1, BM - 1)];
+          } else {
+            v = *reinterpret_cast<const v4u*>(tileI + sl);
+            ra = rowc[r];
+          }
+        };
         // software pipeline by one group: group k+1's tile values and row constants are read
         // from LDS before group k's arithmetic and stores
         int sl = slot_of();
-        v4u vn = *reinterpret_cast<const v4u*>(tileI + sl);
-        EpiRow rn = rowc[r0];
+        v4u vn;
+        EpiRow rn, rn1;
+        load(sl, r0, p0, vn, rn, rn1);
 #pragma unroll
         for (int k = 0; k < kFlat; ++k) {
           const bool ok = kk < ipt && img0 + kk < nimg && 4 * fg < run;
           const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0) * hw + 4 * fg) | (ok ? 0u : kOffDrop);
           int32_t* wslot = ok ? tileI + sl : lut + 512;
+          const int pc = p0;                   // this group's first column
           v4u v = vn;
-          const EpiRow rr = rn;
+          const EpiRow rr = rn, rr1 = rn1;
           if (k + 1 < kFlat) {
             fg += kGemmThreads;
             r0 += dr;
@@ -986,25 +1004,38 @@ gemm_i8_kernel(GemmArgs g) {
             if (p0 >= hw) p0 -= hw, ++r0;
             if (fg >= runG) fg -= runG, ++kk, r0 -= BM;
             sl = slot_of();
-            vn = *reinterpret_cast<const v4u*>(tileI + sl);
-            rn = rowc[r0];
+            load(sl, r0, p0, vn, rn, rn1);
           }
-          v += rr.fold;
+          // per-element row constants (XR: elements past the row end take the next row's)
+          uint32_t fold[4], zp[4];
+          int32_t bias[4], m[4], sh[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool nx = XR && pc + e >= hw;
+            fold[e] = nx ? rr1.fold : rr.fold;
+            bias[e] = nx ? rr1.bias : rr.bias;
+            zp[e] = nx ? (uint32_t)rr1.zp : (uint32_t)rr.zp;
+            m[e] = nx ? rr1.m : rr.m;
+            sh[e] = nx ? rr1.s : rr.s;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += fold[e];
           if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
-          v += (uint32_t)rr.bias;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (uint32_t)bias[e];
           if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
           int32_t q[4];
           if constexpr (FAST) {
-            const int sh2 = -rr.s - 1;
-            const uint32_t rnd = 1u << (sh2 - 1);
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              q[e] = clamp_i32(zpo + ((int32_t)((uint32_t)__mulhi((int32_t)(v[e] - (uint32_t)rr.zp), rr.m) + rnd) >> sh2),
+            for (int e = 0; e < 4; ++e) {
+              const int sh2 = -sh[e] - 1;
+              q[e] = clamp_i32(zpo + ((int32_t)((uint32_t)__mulhi((int32_t)(v[e] - zp[e]), m[e]) + (1u << (sh2 - 1))) >> sh2),
                                qmin, qmax);
+            }
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)rq_core((int32_t)(v[e] - (uint32_t)rr.zp), mode, rr.m, rr.s)),
+              q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)rq_core((int32_t)(v[e] - zp[e]), mode, m[e], sh[e])),
                                qmin, qmax);
           }
           if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
@@ -1021,25 +1052,33 @@ gemm_i8_kernel(GemmArgs g) {
             for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
             if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
           }
-          *reinterpret_cast<v4i*>(wslot) = v4i{q[0], q[1], q[2], q[3]};
+          if constexpr (XR) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) wslot[e + (ok && pc + e >= hw ? kStr - hw : 0)] = q[e];
+          } else {
+            *reinterpret_cast<v4i*>(wslot) = v4i{q[0], q[1], q[2], q[3]};
+          }
         }
       };
-      auto lean_fast = [&](auto fast_c) __attribute__((always_inline)) {
+      auto lean_fast = [&](auto fast_c, auto xr_c) __attribute__((always_inline)) {
         using T = std::true_type;
         using F = std::false_type;
         if (has_add) {
-          if (has_clip) lean(fast_c, T{}, T{});
-          else lean(fast_c, T{}, F{});
+          if (has_clip) lean(fast_c, T{}, T{}, xr_c);
+          else lean(fast_c, T{}, F{}, xr_c);
         } else {
-          if (has_clip) lean(fast_c, F{}, T{});
-          else lean(fast_c, F{}, F{});
+          if (has_clip) lean(fast_c, F{}, T{}, xr_c);
+          else lean(fast_c, F{}, F{}, xr_c);
         }
       };
       const bool fastrq = s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD);
       if (TK_ABL(65536)) {
       } else if (hw % 4 == 0 && hw >= 16 && !TK_ABL(32768)) {
-        if (fastrq) lean_fast(std::true_type{});
-        else lean_fast(std::false_type{});
+        if (fastrq) lean_fast(std::true_type{}, std::false_type{});
+        else lean_fast(std::false_type{}, std::false_type{});
+      } else if (hw >= 16 && !TK_ABL(32768 | 131072)) {
+        if (fastrq) lean_fast(std::true_type{}, std::true_type{});
+        else lean_fast(std::false_type{}, std::true_type{});
       } else if (hw % 4 == 0 && !TK_ABL(32768)) {
         if (fastrq) groups(std::true_type{}, std::true_type{});
         else groups(std::false_type{}, std::true_type{});
