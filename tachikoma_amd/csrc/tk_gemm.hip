@@ -1086,7 +1086,7 @@ gemm_i8_kernel(GemmArgs g) {
         if (fastrq) groups(std::true_type{}, std::false_type{});
         else groups(std::false_type{}, std::false_type{});
       }
-    } else if (g.fast_epi && simple_fold && s_fast && !(g.ablate & 0x7F)) {
+    } else if (g.fast_epi && simple_fold && s_fast && !(g.ablate & 0x7D)) {
       // ---- fast path (tile-uniform): 4 consecutive columns x rows (tid>>5) + 8k, every
       // record through a buffer descriptor (masked lanes get an out-of-range offset),
       // requantize in the mul_hi form: ((x - zp)·m + 2^(sh2-1)) >> sh2 over the high word
@@ -1124,9 +1124,9 @@ gemm_i8_kernel(GemmArgs g) {
           const uint32_t o = offs[k];
           // int32 wrap-around arithmetic in unsigned lanes (the reference accumulates mod 2^32)
           v4u v = __builtin_bit_cast(v4u, t) + r.fold;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, AUX);
+          if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, AUX);
           v += (uint32_t)r.bias;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, AUX);
+          if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, AUX);
           const int sh2 = -r.s - 1;
           const uint32_t rnd = 1u << (sh2 - 1);
           int32_t q[4];
@@ -1134,7 +1134,7 @@ gemm_i8_kernel(GemmArgs g) {
           for (int e = 0; e < 4; ++e)
             q[e] = clamp_i32(zpo + ((int32_t)((uint32_t)__mulhi((int32_t)(v[e] - (uint32_t)r.zp), r.m) + rnd) >> sh2),
                              qmin, qmax);
-          __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, AUX);
+          if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, AUX);
           if constexpr (ADD) {
             // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
 #pragma unroll
@@ -1143,12 +1143,12 @@ gemm_i8_kernel(GemmArgs g) {
               q[e] = clamp_i32(TK_ABL(8192) ? q[e] + (int32_t)rb - add_zp : lut[q[e] & 0xFF] + lut[256 + rb] - add_zp,
                                qmin, qmax);
             }
-            if (!TK_ABL(16384)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, AUX);
+            if (!TK_ABL(16384 | 2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, AUX);
           }
           if constexpr (CLIP) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
-            __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, AUX);
+            if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, AUX);
           }
           if (want_shadow) *reinterpret_cast<v4i*>(slot) = v4i{q[0], q[1], q[2], q[3]};
         }
