@@ -382,9 +382,9 @@ __device__ __forceinline__ void wait_vm(int n) {
 template <int MT, bool kIm2col, bool kBlock, int kMode = 0, int kRing = 3, bool kWide = false, int BN = 128>
 __global__ __launch_bounds__(kGemmThreads, BN == 256 ? (kWide ? 1 : 2)
                                            : MT == 1 ? (kWide ? (kRing == 3 ? 2 : 1) : kRing == 3 ? 4 : kRing == 4 ? 3 : 2)
-                                                     : 2) void
+                                                     : (kWide ? 1 : 2)) void
 gemm_i8_kernel(GemmArgs g) {
-  static_assert(!kWide || (kIm2col && MT == 1), "wide stages: im2col, MT = 1");
+  static_assert(!kWide || (kIm2col && (MT == 1 || (kBlock && kMode == 0 && kRing == 3))), "wide stages: im2col");
   static_assert(BN == 128 || (BN == 256 && MT == 1 && kIm2col && kBlock && kMode == 0), "256-column tiles: conv blocks");
   constexpr int BM = 64 * MT;   // rows of A per block (2 waves along M, MT 32-row tiles each)
   constexpr int NJ = BN / 64;   // 32-col tiles per wave (2 waves along N)
@@ -2191,6 +2191,12 @@ static bool conv_wide(const ConvGeom& g, bool block, int ipt) {
   return tiles <= (conv_bn256_ipt(g, block, false) ? 256 : env_int("TK_WIDE_MAX_TILES", 512));
 }
 
+// 128-row tiles with 128-byte K stages (96 KB ring, one workgroup per CU) where the grid fits one
+// round: the 14x14 3x3 256-channel layers, -5.5 % (profiles/r02z_wide_mt2_ab.txt)
+static bool wide_mt2(const ConvGeom& g, int64_t tiles) {
+  return g.KH * g.KW <= 64 && g.cin_pad % 128 == 0 && g.k_pad / kBK >= 8 && tiles <= 256 && env_int("TK_WIDE_MT2", 1);
+}
+
 // Patch-tile blocks (conv_patch_kernel): 1x1 (pad 0) and 3x3 (pad 1) convs, stride 1 or 2, with
 // 64-channel input steps, 32-channel output multiples, no kernel zero point.  Candidate patches:
 // whole images (ipt of them, <= 224 pixels) or bands of th output rows (th | OH).  For each, the
@@ -2563,7 +2569,9 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
       hipLaunchKernelGGL((gemm_i8_kernel<1, true, false>), grid, dim3(kGemmThreads), 0, s, ga);
     }
   } else {
-    if (blk) hipLaunchKernelGGL((gemm_i8_kernel<2, true, true>), grid, dim3(kGemmThreads), 0, s, ga);
+    if (blk && wide_mt2(g, ga.mtiles * (int64_t)ga.ntiles))
+      hipLaunchKernelGGL((gemm_i8_kernel<2, true, true, 0, 3, true>), grid, dim3(kGemmThreads), 0, s, ga);
+    else if (blk) hipLaunchKernelGGL((gemm_i8_kernel<2, true, true>), grid, dim3(kGemmThreads), 0, s, ga);
     else hipLaunchKernelGGL((gemm_i8_kernel<2, true, false>), grid, dim3(kGemmThreads), 0, s, ga);
   }
   TK_LAUNCH_CHECK();
