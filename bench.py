@@ -15,8 +15,9 @@ Launch: python bench.py [--gpus N --steps K --warmup W]
   * --dist-backend gloo rehearses N ranks on one GPU (all ranks share cuda:0).
 
 After the timed region, the trace image is checked record for record against the CPU
-oracle (every record of the CPU baseline's samples at N = 1; the first and last sample of
-every shard at N > 1); any mismatch makes the run exit non-zero.
+oracle: at N > 1 every rank checks ceil(64 / N) samples spread over its shard (64 samples,
+14,912 records in all, as at N = 1), and rank 0 then times the CPU baseline at every N
+(checking each sample it traces too); any mismatch makes the run exit non-zero.
 """
 from __future__ import annotations
 
@@ -129,24 +130,30 @@ def cpu_quota() -> float | None:
     return None
 
 
-def d2h_probe(device, nbytes: int = 1 << 30, reps: int = 4) -> float:
-    """Pinned device→host bandwidth (GB/s) of one large hipMemcpyAsync, measured with HIP
-    events on a side stream: the PCIe ceiling the traced steps are compared with."""
+def d2h_probe(device, nbytes: int = 1 << 30, reps: int = 4, streams: int = 1) -> float:
+    """Pinned device→host bandwidth (GB/s) of `nbytes` moved by `streams` concurrent
+    hipMemcpyAsync copies (nbytes / streams each, one side stream per copy), timed with HIP
+    events from a common start: the PCIe ceiling the traced steps are compared with."""
     import torch
     src = torch.empty(nbytes, dtype=torch.uint8, device=device)
     src.fill_(1)
     dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    s = torch.cuda.Stream(device=device)
+    ss = [torch.cuda.Stream(device=device) for _ in range(streams)]
+    part = nbytes // streams
     best = 0.0
-    with torch.cuda.stream(s):
-        dst.copy_(src, non_blocking=True)  # warm (page tables, SDMA queue)
-        for _ in range(reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            dst.copy_(src, non_blocking=True)
-            e1.record(s)
-            e1.synchronize()
-            best = max(best, nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    for r in range(reps + 1):  # the first repetition warms page tables and the SDMA queues
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(ss[0])
+        for k, s in enumerate(ss):
+            s.wait_event(e0)
+            with torch.cuda.stream(s):
+                dst[k * part:(k + 1) * part].copy_(src[k * part:(k + 1) * part], non_blocking=True)
+        for s in ss[1:]:
+            ss[0].wait_stream(s)
+        e1.record(ss[0])
+        e1.synchronize()
+        if r:
+            best = max(best, part * streams / (e0.elapsed_time(e1) * 1e-3) / 1e9)
     del src, dst
     return best
 
@@ -162,11 +169,16 @@ class Parity:
         self.n_records = 0
         self.mismatches = 0
         self.first = None
+        self.seen = set()
 
     def check(self, local_index: int, global_index: int, expected) -> None:
-        self.samples += 1
+        """A sample checked twice (parity spread, then the CPU baseline) is compared again but
+        counted once."""
+        fresh = local_index not in self.seen
+        self.seen.add(local_index)
+        self.samples += fresh
         for name, exp in expected.items():
-            self.n_records += 1
+            self.n_records += fresh
             got = self.records[name][local_index:local_index + 1]
             if got.shape != exp.shape or got.dtype != exp.dtype or not np.array_equal(got, exp):
                 self.mismatches += 1
@@ -181,6 +193,12 @@ class Parity:
     def summary(self) -> dict:
         return {"samples": self.samples, "records": self.n_records, "mismatches": self.mismatches,
                 "first_mismatch": self.first}
+
+
+def spread_samples(count: int, n: int):
+    """n local sample indices spread evenly over a shard of `count` (first and last included)."""
+    n = max(1, min(count, n))
+    return sorted(set(int(round(v)) for v in np.linspace(0, count - 1, n)))
 
 
 def cpu_baseline(model_fn, offset: int, batch: int, budget_s: float, threads: int, parity: Parity):
@@ -214,17 +232,25 @@ def cpu_baseline(model_fn, offset: int, batch: int, budget_s: float, threads: in
                       f"{dt:.1f}s timed (first sample excluded as warm-up)"}
 
 
-def pmc_traffic(model: str, batch: int, launches: int):
-    """HBM bytes per launch of the block kernel from the committed PMC summary
-    (tools/pmc.sh -> profiles/*_pmc_block.json), when it was taken on this workload."""
+def pmc_traffic(model: str, batch: int, library: str):
+    """HBM traffic of the block kernel from a committed PMC summary (tools/pmc.sh ->
+    profiles/*_pmc_block.json) taken on this workload: the one whose recorded library digest
+    equals the loaded library's; failing that the newest by its embedded UTC stamp (never by
+    file name).  Returns (bytes per launch, bytes per step, launches per step, source, match)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_block.json")), reverse=True):
+    docs = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_block.json")):
         with open(path) as f:
             doc = json.load(f)
-        if doc.get("model") == model and doc.get("batch") == batch:
-            # per layer-block node (split-K layers dispatch two kernels per node)
-            return doc["hbm_bytes_per_step"] / max(launches, 1), os.path.relpath(path, ROOT)
-    return None, None
+        if doc.get("model") == model and doc.get("batch") == batch and doc.get("created_utc"):
+            docs.append((doc.get("library") == library, doc["created_utc"], path, doc))
+    if not docs:
+        return None
+    same, _, path, doc = max(docs, key=lambda d: (d[0], d[1]))
+    launches = int(doc["launches_per_step"])  # dispatches: a split-K node launches twice
+    return {"per_launch": doc["hbm_bytes_per_step"] / max(launches, 1), "per_step": doc["hbm_bytes_per_step"],
+            "launches": launches, "source": os.path.relpath(path, ROOT), "library_match": same,
+            "library": doc.get("library")}
 
 
 # ---------------------------------------------------------------- one rank
@@ -293,22 +319,31 @@ def main(argv=None) -> int:
         cap.synchronize()
         cap.write(path)
 
-    def step(i):
+    # per-step D2H telemetry: HIP events on the capture stream bracket each timed step's copies
+    # (graph input + every record), so a slow host link shows in the line itself
+    rec_bytes = sum(int(np.prod(t.shape, dtype=np.int64)) * np.dtype(t.dtype).itemsize for t in m.plan.records)
+    d2h_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+
+    def step(i, timed=False):
         if args.no_trace:
             m.run(trace=False)
             return
         k = i % len(caps)
         cap = caps[k]
+        if writer is not None and pending[k] is not None:
+            pending[k].result()  # the writer is done with this image: it may be overwritten
+        # memory sink: the next run's kernels wait for this run's copies on the device
+        # (tk_module_run's capture event), the host does not block between steps
+        cap.capture_stream.wait_stream(stream)
+        if timed:
+            d2h_ev[i][0].record(cap.capture_stream)
+        cap.capture_inputs(stream)
+        m.module.run(stream, cap.capture_stream, cap.host_dst)
+        if timed:
+            d2h_ev[i][1].record(cap.capture_stream)
         if writer is not None:
-            if pending[k] is not None:
-                pending[k].result()  # the writer is done with this image: it may be overwritten
-            cap.capture_inputs(stream)
-            m.module.run(stream, cap.capture_stream, cap.host_dst)
             pending[k] = writer.submit(write_image, cap)
-        else:
-            # memory sink: the next run's kernels wait for this run's copies on the device
-            # (tk_module_run's capture event), the host does not block between steps
-            m.run(trace=True)
 
     def drain():
         for k, f in enumerate(pending):
@@ -330,10 +365,12 @@ def main(argv=None) -> int:
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        step(i, timed=True)
     drain()
     barrier()
     elapsed = time.perf_counter() - t0
+    step_gbps = [] if args.no_trace else \
+        [rec_bytes / (a.elapsed_time(z) * 1e-3) / 1e9 for a, z in d2h_ev]
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -415,7 +452,7 @@ def main(argv=None) -> int:
     achieved_bw = blk_bytes / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
     achieved_ops = blk_ops / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
     total_ms = step_ms
-    traffic, traffic_src = pmc_traffic(args.model, B, n_launch)
+    pmc = pmc_traffic(args.model, B, _lib.build_info())
 
     # ---- trace-digest all-gather (RCCL over xGMI): one u64 record digest per rank, computed
     # on the device over the records of one more traced step (outside the timed region); the
@@ -436,34 +473,54 @@ def main(argv=None) -> int:
         if rank == 0:
             shard.write_manifest(os.path.join(args.out_dir, "trace.manifest.json"), model.name, B * world, entries)
 
-    # ---- PCIe ceiling of this rank, measured in this run
+    # ---- PCIe ceiling of this rank, measured in this run: one 1 GiB copy, and the same bytes
+    # as two concurrent copies on two streams (do two SDMA engines beat one?)
     d2h_peak = d2h_probe(device)
+    d2h_peak2 = d2h_probe(device, streams=2)
     trace_bytes = caps[0].layout.total
     d2h_achieved = trace_bytes / (elapsed_max / args.steps) / 1e9 if not args.no_trace else 0.0
 
-    # ---- parity: the trace image vs the CPU oracle, record for record
+    # ---- parity: the trace image vs the CPU oracle, record for record.  Every rank checks
+    # ceil(B / N) samples spread over its shard (B samples in all, as many as at N = 1), with its
+    # share of the host cores; then rank 0 alone times the CPU baseline on its NUMA node's
+    # cores (capped by the cgroup quota) while the other ranks wait at a host-side barrier,
+    # and checks each sample that traces as well.
     parity = Parity(read_trace(caps[0].bytes()).records) if not args.no_trace else None
     cpu = None
     quota = cpu_quota()
+    host_group = dist.new_group(backend="gloo") if world > 1 else None
     if parity is not None:
-        if world == 1 and not args.skip_cpu:
-            # the CPU baseline runs on every core this process may use (its original affinity,
-            # capped by the cgroup's CPU quota), and checks each sample it traces
-            os.sched_setaffinity(0, home_cpus)
-            threads = len(home_cpus) if quota is None else max(1, min(len(home_cpus), int(quota)))
+        from oracle import graph_ref
+        # (at N = 1 the CPU baseline's samples are the parity set; --skip-cpu keeps two)
+        n_spread = -(-B // world) if world > 1 else (2 if args.skip_cpu else 0)
+        if n_spread:
+            mine = os.sched_getaffinity(0)
+            share = len(mine) if quota is None else max(1, min(len(mine), int(quota / world)))
+            one = model_fn(batch=1)
+            for i in spread_samples(count, n_spread):
+                rec = graph_ref.calibrate(one.mod, one.params, {"data": x[i:i + 1]}, backend="c", threads=share)
+                parity.check(i, offset + i, rec)
+                del rec
+        if world > 1:
+            dist.barrier(group=host_group)
+        if rank == 0 and not args.skip_cpu:
+            cpus = home_cpus if world == 1 else os.sched_getaffinity(0)
+            os.sched_setaffinity(0, cpus)
+            threads = len(cpus) if quota is None else max(1, min(len(cpus), int(quota)))
             _log(f"cpu baseline (oracle port, {threads} threads) + parity ...")
             cpu = cpu_baseline(model_fn, offset, count, args.cpu_budget_s, threads, parity)
-        else:
-            from oracle import graph_ref
-            one = model_fn(batch=1)
-            for i in sorted({0, count - 1}):
-                rec = graph_ref.calibrate(one.mod, one.params, {"data": x[i:i + 1]}, backend="c")
-                parity.check(i, offset + i, rec)
+            cpu["n_gpus_running"] = world
+        if world > 1:
+            dist.barrier(group=host_group)
+    per_step = {"min": round(min(step_gbps), 2), "max": round(max(step_gbps), 2),
+                "mean": round(sum(step_gbps) / len(step_gbps), 2)} if step_gbps else None
     rank_info = {"rank": rank, "pci": placement["pci"], "numa_node": placement["numa_node"],
                  "cpus": placement["cpus"], "image_pages_per_node": image_pages,
                  "d2h": {"achieved_GBps": round(trace_bytes / (elapsed / args.steps) / 1e9, 2),
                          "measured_peak_GBps": round(d2h_peak, 2),
-                         "frac": round(trace_bytes / (elapsed / args.steps) / 1e9 / d2h_peak, 4)},
+                         "measured_peak_2streams_GBps": round(d2h_peak2, 2),
+                         "frac": round(trace_bytes / (elapsed / args.steps) / 1e9 / d2h_peak, 4),
+                         "per_step_GBps": per_step},
                  "parity": parity.summary() if parity is not None else None,
                  "file_sink": file_check}
     if world > 1:
@@ -508,9 +565,13 @@ def main(argv=None) -> int:
                        "dist_backend": args.dist_backend if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved_bw / 1e9, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved_bw / 1e9 / HBM_PEAK_GBPS, 4),
-                         "traffic": None if traffic is None else int(traffic),
-                         "traffic_unit": "HBM bytes per layer-block node (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per step / nodes)",
-                         "traffic_source": traffic_src,
+                         "traffic": None if pmc is None else int(pmc["per_launch"]),
+                         "traffic_unit": "HBM bytes per block-kernel launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                                         "per step / launches per step)",
+                         "traffic_source": None if pmc is None else pmc["source"],
+                         "traffic_library_match": None if pmc is None else pmc["library_match"],
+                         "traffic_bytes_per_step": None if pmc is None else int(pmc["per_step"]),
+                         "launches_per_step": None if pmc is None else pmc["launches"],
                          "algorithmic_bytes_per_node": int(blk_bytes / max(n_launch, 1)),
                          "kernel": "gemm_i8_kernel<*,*,block> fused conv/dense layer block (v_mfma_i32_32x32x32_i8)",
                          "nodes_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
@@ -519,6 +580,8 @@ def main(argv=None) -> int:
                          "mfma_frac": round(achieved_ops / INT8_MFMA_PEAK_OPS, 4),
                          "d2h": {"achieved_GBps": round(d2h_achieved, 2), "measured_peak_GBps": round(d2h_peak, 2),
                                  "frac": round(d2h_achieved / d2h_peak, 4) if d2h_peak else None,
+                                 "measured_peak_2streams_GBps": round(d2h_peak2, 2),
+                                 "per_step_GBps": per_step,
                                  "note": "trace image bytes per step / max-over-ranks step time vs a 1 GiB pinned "
                                          "D2H copy measured on rank 0 in this run"}},
             "cpu_baseline": cpu,

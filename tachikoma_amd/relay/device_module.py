@@ -440,8 +440,10 @@ class DeviceModule:
             raise KeyError(f"set_input: {name} is not an input or param of the graph")
         buf = self.buffers[name]
         if isinstance(value, torch.Tensor):
-            if value.numel() != buf.numel():
-                raise ValueError(f"set_input {name}: {tuple(value.shape)} vs {tuple(buf.shape)}")
+            # held to the exact shape, like host arrays (a transposed or NHWC tensor of the same
+            # element count must not be reinterpreted silently)
+            if tuple(value.shape) != tuple(buf.shape):
+                raise ValueError(f"set_input {name}: shape {tuple(value.shape)} vs {tuple(buf.shape)}")
             return value
         v = np.asarray(value.numpy() if hasattr(value, "numpy") else value)
         if tuple(v.shape) != tuple(buf.shape):

@@ -168,7 +168,18 @@ def run(tracer: Tracer, global_samples: int, chunk: int, out_dir: str, rank: int
         kept[c.index] = e
 
     for c in todo:
-        pending.append((c, tracer(c.sample_offset, c.n_samples, c.file + ".partial")))
+        try:
+            fut = tracer(c.sample_offset, c.n_samples, c.file + ".partial")
+        except BaseException:
+            # chunks already handed to the tracer still complete: journal those whose files do
+            # before the failure propagates (a resume then re-traces only what was lost)
+            for pc, pf in pending:
+                try:
+                    finish(pc, pf)
+                except Exception:  # noqa: BLE001 - the original failure is the one to report
+                    break
+            raise
+        pending.append((c, fut))
         # journal entries are appended in chunk order, as soon as each file is complete
         while pending and (len(pending) > 1 or pending[0][1].done()):
             finish(*pending.pop(0))
@@ -190,6 +201,7 @@ class GraphModuleTracer:
         self.modules: Dict[int, list] = {}  # n_samples -> [GraphModule, [TraceCapture x2], next slot]
         self.writer = concurrent.futures.ThreadPoolExecutor(max_workers=1)
         self.busy: Dict[int, "concurrent.futures.Future"] = {}
+        self.digest_slots: Dict[int, "object"] = {}  # per trace image: pinned host copy of its digest
 
     def _module(self, n: int):
         if n not in self.modules:
@@ -216,7 +228,14 @@ class GraphModuleTracer:
         stream = torch.cuda.current_stream(m.module.device)
         cap.capture_inputs(stream)
         m.module.run(stream, cap.capture_stream, cap.host_dst)
-        digest = m.module.records_digest(stream)  # device digest of exactly these records
+        # device digest of exactly these records, copied on the stream into this image's own
+        # pinned slot: the module's digest tensor is reused by the next chunk's run, which the
+        # stream may reach before the writer thread reads the value
+        digest = m.module.records_digest(stream)
+        slot_t = self.digest_slots.get(id(cap))
+        if slot_t is None:
+            slot_t = self.digest_slots[id(cap)] = torch.empty(digest.shape, dtype=digest.dtype, pin_memory=True)
+        slot_t.copy_(digest, non_blocking=True)
         done = torch.cuda.Event()
         done.record(stream)
 
@@ -224,7 +243,7 @@ class GraphModuleTracer:
             done.synchronize()
             cap.synchronize()
             cap.write(path)
-            return int(digest.item()) & 0xFFFFFFFFFFFFFFFF
+            return int(slot_t.reshape(-1)[0].item()) & 0xFFFFFFFFFFFFFFFF
 
         fut = self.writer.submit(write)
         self.busy[id(cap)] = fut

@@ -68,3 +68,46 @@ def test_host_placement_helpers():
     assert pages is None or sum(pages.values()) >= (1 << 24) // 4096
     q = bench.cpu_quota()
     assert q is None or q > 0
+
+
+def test_parity_counts_a_rechecked_sample_once():
+    rec = {"%0": np.arange(6, dtype=np.int32).reshape(3, 2)}
+    p = bench.Parity(rec)
+    p.check(0, 0, {"%0": rec["%0"][0:1].copy()})
+    p.check(0, 0, {"%0": rec["%0"][0:1].copy()})  # the CPU baseline traces a spread sample again
+    p.check(2, 2, {"%0": rec["%0"][2:3].copy()})
+    assert p.summary()["samples"] == 2 and p.summary()["records"] == 2
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_parity_spread_covers_the_n1_sample_count(world):
+    """ceil(64 / N) samples per rank over N shards of 64 = at least the 64 samples of N = 1,
+    each rank's first and last sample included."""
+    per_rank = bench.spread_samples(64, -(-64 // world))
+    assert len(per_rank) * world >= 64 and per_rank[0] == 0 and per_rank[-1] == 63
+    assert len(set(per_rank)) == len(per_rank)
+
+
+def test_pmc_traffic_picks_library_then_stamp(tmp_path, monkeypatch):
+    """bench.pmc_traffic: the summary taken with the loaded library wins; failing that the
+    newest by embedded UTC stamp (not by file name); traffic per launch divides by the PMC's
+    own dispatch count."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    base = {"model": "resnet50", "batch": 64, "launches_per_step": 55}
+
+    def put(name, **kw):
+        (prof / name).write_text(json.dumps(dict(base, **kw)))
+
+    put("r09_pmc_block.json", hbm_bytes_per_step=110.0, created_utc="2026-01-01T00:00:00Z", library="old")
+    put("r02z_pmc_block.json", hbm_bytes_per_step=220.0, created_utc="2026-02-01T00:00:00Z", library="older")
+    put("r00_pmc_block.json", hbm_bytes_per_step=330.0)  # no stamp: never chosen
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    got = bench.pmc_traffic("resnet50", 64, "current")
+    assert got["source"] == os.path.join("profiles", "r02z_pmc_block.json") and not got["library_match"]
+    assert got["per_launch"] == 4.0 and got["launches"] == 55
+    put("r01_pmc_block.json", hbm_bytes_per_step=55.0, created_utc="2025-01-01T00:00:00Z", library="current")
+    got = bench.pmc_traffic("resnet50", 64, "current")
+    assert got["source"] == os.path.join("profiles", "r01_pmc_block.json") and got["library_match"]
+    assert got["per_launch"] == 1.0
+    assert bench.pmc_traffic("resnet18", 64, "current") is None

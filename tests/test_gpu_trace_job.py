@@ -63,3 +63,25 @@ def test_device_trace_job_resume_bit_exact(device, tmp_path, name, samples, chun
         assert len(exp) == len(tr.records)
         for k, v in exp.items():
             assert np.array_equal(tr.records[k], v), (e.file, k)
+
+
+def test_journal_digests_survive_a_slow_writer(device, tmp_path, monkeypatch):
+    """Every chunk's journal digest is that chunk's own: the writer thread is slowed so the
+    next same-size chunk's run (and digest) lands on the device before the value is read."""
+    import time
+    orig = graph_executor.TraceCapture.write
+
+    def slow_write(self, path):
+        time.sleep(0.3)
+        orig(self, path)
+
+    monkeypatch.setattr(graph_executor.TraceCapture, "write", slow_write)
+    d = str(tmp_path)
+    proto, tracer = _tracer("lenet5")
+    try:
+        entries = trace_job.run(tracer, 16, 4, d)
+    finally:
+        tracer.close()
+    assert len(entries) == 4
+    for e in entries:
+        assert shard.hex64(tf.trace_file_digest(f"{d}/{e.file}")) == e.digest, e.file

@@ -14,6 +14,8 @@ import csv
 import glob
 import json
 import os
+import sys
+import time
 from collections import defaultdict
 
 KIB = 1024
@@ -77,6 +79,16 @@ def main():
     s["bench_args"] = wl
     s["model"] = wl[wl.index("--model") + 1] if "--model" in wl else "resnet50"
     s["batch"] = int(wl[wl.index("--batch") + 1]) if "--batch" in wl else 64
+    # which kernels these counters belong to: bench.py takes the traffic from the summary whose
+    # library digest equals the loaded library's (else the newest by this UTC stamp)
+    s["created_utc"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+    try:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from tachikoma_amd import _lib
+        s["library"] = _lib.build_info()
+    except Exception as e:  # noqa: BLE001 - a summary without a digest is still a summary
+        s["library"] = None
+        print(f"  (library digest unavailable: {e})")
     print(f"per-step totals over {s['launches_per_step']} dispatches:")
     print(f"  HBM fetch {s['fetch_bytes_per_step'] / 1e9:.3f} GB (x2 corrected), write "
           f"{s['write_bytes_per_step'] / 1e9:.3f} GB, per launch {s['hbm_bytes_per_launch'] / 1e6:.2f} MB")
