@@ -523,6 +523,21 @@ def main(argv=None) -> int:
                          "per_step_GBps": per_step},
                  "parity": parity.summary() if parity is not None else None,
                  "file_sink": file_check}
+    if file_check is not None:
+        # disk-write probe on the same filesystem, same writer (tk_write_file: O_DIRECT, 64 MiB
+        # pieces, 4 threads), no GPU work beside it: the sink's ceiling on this box
+        probe_path = path + ".probe"
+        best = float("inf")
+        for _ in range(2):
+            t0 = time.perf_counter()
+            caps[0].write(probe_path)
+            best = min(best, time.perf_counter() - t0)
+        os.remove(probe_path)
+        achieved = trace_bytes / (elapsed / args.steps) / 1e9
+        probe = trace_bytes / best / 1e9
+        file_check.update(achieved_GBps=round(achieved, 2), probe_GBps=round(probe, 2), frac=round(achieved / probe, 4),
+                          note="trace image bytes per traced step (written while the next step runs) vs the same "
+                               "image written alone by the same writer, best of 2")
     if world > 1:
         ranks = [None] * world
         dist.all_gather_object(ranks, rank_info)
@@ -573,7 +588,8 @@ def main(argv=None) -> int:
                          "traffic_bytes_per_step": None if pmc is None else int(pmc["per_step"]),
                          "launches_per_step": None if pmc is None else pmc["launches"],
                          "algorithmic_bytes_per_node": int(blk_bytes / max(n_launch, 1)),
-                         "kernel": "gemm_i8_kernel<*,*,block> fused conv/dense layer block (v_mfma_i32_32x32x32_i8)",
+                         "kernel": "fused conv/dense layer blocks: conv_img_kernel (whole-image tiles, 7x7/14x14 "
+                                   "planes) and gemm_i8_kernel<*,*,block> (im2col tiles), v_mfma_i32_32x32x32_i8",
                          "nodes_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
                          "algorithmic_bytes_per_step": int(blk_bytes),
                          "mfma_tops": round(achieved_ops / 1e12, 1),
@@ -586,6 +602,8 @@ def main(argv=None) -> int:
                                          "D2H copy measured on rank 0 in this run"}},
             "cpu_baseline": cpu,
             "parity": par,
+            "file_sink": None if args.sink != "file" else
+            {k: ranks[0]["file_sink"].get(k) for k in ("achieved_GBps", "probe_GBps", "frac", "equal")},
             "ranks": ranks,
             "extra": {
                 "compute_only_ms_per_step": round(compute_ms, 3),

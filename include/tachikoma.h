@@ -253,6 +253,15 @@ int tk_avg_pool2d(const tk_tensor* data, tk_tensor* out, const tk_pool2d_attrs* 
 int tk_global_avg_pool2d(const tk_tensor* data, tk_tensor* out, void* stream);
 /* batch_flatten / reshape: byte copy (kept as a node so it is traced). */
 int tk_copy(const tk_tensor* data, tk_tensor* out, void* stream);
+/* nn.pad, constant mode (src/relay/op/nn/pad.cc, python/tvm/topi/nn/pad.py:24-82): up to 6-D, any
+ * 1/2/4/8-byte dtype; out[i] = data[i - before] inside the data's range, else the pad value
+ * (already cast to the dtype: value_i for integer tensors, value_f for float32). */
+typedef struct {
+  int64_t before[6], after[6];
+  int64_t value_i;
+  double value_f;
+} tk_pad_attrs;
+int tk_pad(const tk_tensor* data, tk_tensor* out, const tk_pad_attrs* attrs, void* stream);
 
 /* tachikoma BYOC composite post-ops: the float32 tail of a tachikoma.qnn.conv2d /
  * tachikoma.qnn.dense composite after LegalizeQnnOpForTachikoma
@@ -300,7 +309,8 @@ enum {
 };
 typedef struct {
   int32_t op;                   /* TK_EW_* */
-  int32_t rhs_kind;             /* 0: unary, 1: scalar (scalar_f / scalar_i), 2: tensor of x's shape */
+  int32_t rhs_kind;             /* 0: unary, 1: scalar (scalar_f / scalar_i), 2: tensor of x's shape,
+                                   3: one value per channel (axis 1) of x, add / multiply only */
   double scalar_f;              /* float32 tensors */
   int64_t scalar_i;             /* integer tensors */
   double lo, hi;                /* TK_EW_CLIP */
@@ -346,6 +356,7 @@ enum {
   TK_NODE_EWISE = 17,      /* in: x, [rhs tensor]; attrs.ewise */
   TK_NODE_CONV2D_F32 = 18, /* in: data, weight (float32); attrs.conv2d */
   TK_NODE_DENSE_F32 = 19,  /* in: data, weight (float32) */
+  TK_NODE_PAD = 20,        /* in: data; attrs.pad */
 };
 
 #define TK_MAX_NODE_INPUTS 4
@@ -368,6 +379,7 @@ typedef struct {
     tk_add_block_attrs add_block;
     tk_postops_attrs postops;
     tk_ewise_attrs ewise;
+    tk_pad_attrs pad;
     struct { int64_t a_min, a_max; } clip;
     struct { int32_t axis; } bias_add;
   } attrs;
@@ -443,8 +455,10 @@ int64_t tk_trace_layout(const char* json, const tk_array_meta* params, int n_par
                         int64_t* record_offsets);
 int tk_trace_write_headers(const char* json, const tk_array_meta* params, int n_params,
                            const tk_array_meta* records, int n_records, void* image, int64_t image_size);
-/* Writes `size` bytes of `image` to `path` (O_TRUNC): the file is sized once and up to 8
- * threads pwrite disjoint ranges of 256 MB or more. */
+/* Writes `size` bytes of `image` to `path` (O_TRUNC): the file is sized once; a 4 KiB-aligned
+ * image of 64 MiB or more goes out with O_DIRECT in 64 MiB pieces from 4 threads (the < 4 KiB
+ * tail buffered), otherwise (or where the filesystem refuses direct I/O) buffered pwrites of
+ * 256 MiB pieces from up to 8 threads. */
 int tk_write_file(const char* path, const void* image, int64_t size);
 
 /* ---------------------------------------------------------------- digest

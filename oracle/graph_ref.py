@@ -154,6 +154,8 @@ def eval_call(call, args, backend: str = "numpy", threads: int = 1):
         return ref.batch_flatten(args[0])
     if op == "reshape":
         return ref.reshape(args[0], a["newshape"])
+    if op == "nn.pad":
+        return ref.pad(args[0], a["pad_width"], args[1])
     raise NotImplementedError(op)
 
 

@@ -140,6 +140,15 @@ TK_EW = {"add": 0, "multiply": 1, "left_shift": 2, "right_shift": 3, "round": 4,
          "fixed_point_multiply": 7}
 
 
+class tk_pad_attrs(ctypes.Structure):
+    _fields_ = [
+        ("before", ctypes.c_int64 * 6),
+        ("after", ctypes.c_int64 * 6),
+        ("value_i", ctypes.c_int64),
+        ("value_f", ctypes.c_double),
+    ]
+
+
 class tk_pool2d_attrs(ctypes.Structure):
     _fields_ = [
         ("pool_size", ctypes.c_int32 * 2),
@@ -169,6 +178,7 @@ class tk_node_attrs(ctypes.Union):
         ("add_block", tk_add_block_attrs),
         ("postops", tk_postops_attrs),
         ("ewise", tk_ewise_attrs),
+        ("pad", tk_pad_attrs),
         ("clip", _clip),
         ("bias_add", _bias_add),
     ]
@@ -205,7 +215,7 @@ NODE_KINDS = {
     "qnn.conv2d": 1, "qnn.dense": 2, "qnn.requantize": 3, "nn.bias_add": 4, "clip": 5, "cast": 6,
     "qnn.add": 7, "nn.max_pool2d": 8, "nn.avg_pool2d": 9, "nn.global_avg_pool2d": 10, "copy": 11, "shadow": 12,
     "conv_block": 13, "dense_block": 14, "add_block": 15, "postops": 16,
-    "ewise": 17, "conv2d_f32": 18, "dense_f32": 19,
+    "ewise": 17, "conv2d_f32": 18, "dense_f32": 19, "nn.pad": 20,
 }
 MAX_NODE_INPUTS = 4
 MAX_NODE_OUTPUTS = 6
@@ -248,6 +258,7 @@ SIGNATURES = {
     "tk_avg_pool2d": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_pool2d_attrs), _VP]),
     "tk_global_avg_pool2d": (ctypes.c_int, [_PT, _PT, _VP]),
     "tk_copy": (ctypes.c_int, [_PT, _PT, _VP]),
+    "tk_pad": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_pad_attrs), _VP]),
     "tk_tachikoma_postops": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_postops_attrs), _VP]),
     "tk_ewise": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_ewise_attrs), _VP]),
     "tk_conv2d_f32": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_conv2d_attrs), _VP]),

@@ -6,10 +6,11 @@ exported symbols are exactly the ``extern "C"`` entry points of
 ``include/tachikoma.h``.
 
 Rebuilds are decided by content, not by file times: ``source_hash()`` digests every
-source, header and the compile flags; each object carries a stamp of the digest it was
-built from, and the digest is compiled into the library (``tk_build_info()``), so
-``_lib.load()`` can refuse a library that does not match the tree it is imported from
-(a stale binary pushed to a GPU box).
+source, header and the compile flags and is compiled into the library (``tk_build_info()``,
+tk_host.cc only), so ``_lib.load()`` can refuse a library that does not match the tree it is
+imported from (a stale binary pushed to a GPU box).  Each object carries a stamp of what it was
+built from -- its own source, the shared headers, the flags (and, for tk_host.cc, the tree
+digest) -- so an edit to one kernel file recompiles that file, not the whole library.
 """
 from __future__ import annotations
 
@@ -30,8 +31,8 @@ LIB = os.path.join(HERE, "libtachikoma.so")
 ARCH = "gfx950"
 
 SOURCES = ["tk_host.cc", "tk_calibrate.cc", "tk_format.cc", "tk_runtime.cc", "tk_elementwise.hip", "tk_gemm.hip",
-           "tk_residual.hip", "tk_realize.hip"]
-HEADERS = ["tk_common.h"]
+           "tk_residual.hip", "tk_realize.hip", "tk_conv_img.hip"]
+HEADERS = ["tk_common.h", "tk_conv.h"]
 BASE_FLAGS = ["-std=c++20", "-O3", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-Wall",
               "-Wno-unused-function"]
 
@@ -108,6 +109,19 @@ def _write(path: str, text: str) -> None:
         f.write(text)
 
 
+def _object_stamp(src: str, defines, build_id: str) -> str:
+    """What one object is compiled from: its source, the shared headers, the flags; tk_host.cc
+    also embeds the tree digest (tk_build_info)."""
+    h = hashlib.sha256()
+    h.update(" ".join(BASE_FLAGS + list(defines)).encode())
+    for path in [os.path.join(CSRC, src)] + [p for p in _hash_inputs() if not p.endswith(tuple(SOURCES))]:
+        with open(path, "rb") as f:
+            h.update(os.path.basename(path).encode() + b"\0" + f.read() + b"\0")
+    if src == "tk_host.cc":
+        h.update(build_id.encode())
+    return h.hexdigest()[:16]
+
+
 def _build_into(obj_dir: str, lib: str, defines, tag: str, force: bool, verbose: bool) -> str:
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(os.path.dirname(lib), exist_ok=True)
@@ -115,13 +129,14 @@ def _build_into(obj_dir: str, lib: str, defines, tag: str, force: bool, verbose:
     build_id = digest + tag
     if not force and os.path.exists(lib) and _read(_stamp(lib)) == build_id:
         return lib  # up to date (objects are only consulted when something must be rebuilt)
-    extra = list(defines) + [f'-DTK_SOURCE_HASH="{build_id}"']
     jobs, objs = [], []
     for s in SOURCES:
         obj = os.path.join(obj_dir, s + ".o")
         objs.append(obj)
-        if force or not os.path.exists(obj) or _read(_stamp(obj)) != build_id:
-            jobs.append((os.path.join(CSRC, s), obj))
+        stamp = _object_stamp(s, list(defines), build_id)
+        if force or not os.path.exists(obj) or _read(_stamp(obj)) != stamp:
+            extra = list(defines) + ([f'-DTK_SOURCE_HASH="{build_id}"'] if s == "tk_host.cc" else [])
+            jobs.append((os.path.join(CSRC, s), obj, extra, stamp))
     if jobs:
         workers = min(len(jobs), int(os.environ.get("MAX_JOBS", "8")))
         res = {}
@@ -129,10 +144,10 @@ def _build_into(obj_dir: str, lib: str, defines, tag: str, force: bool, verbose:
             with open(RESOURCES) as f:
                 res = json.load(f)
         with concurrent.futures.ThreadPoolExecutor(max_workers=workers) as ex:
-            futs = [(os.path.basename(s), o, ex.submit(_compile, s, o, extra)) for s, o in jobs]
-            for name, o, f in futs:
+            futs = [(os.path.basename(s), o, st, ex.submit(_compile, s, o, extra)) for s, o, extra, st in jobs]
+            for name, o, st, f in futs:
                 r = f.result()
-                _write(_stamp(o), build_id)
+                _write(_stamp(o), st)
                 if name.endswith(".hip") and not tag:
                     res[name] = r
         if not tag:

@@ -1,0 +1,577 @@
+// Image-tile conv blocks: qnn.conv2d (1x1 or 3x3, stride 1 or 2) -> bias_add -> requantize
+// [-> qnn.add(residual)] [-> clip] in one launch, for the small planes of a CNN's later stages
+// (ResNet-50's 14x14 and 7x7 layers at 64 samples per GPU).
+//
+// What differs from gemm_i8_kernel (tk_gemm.hip), whose 64x128 im2col tiles gather every input
+// pixel once per tap through each CU's LDS-DMA path and end with one store burst:
+//   * a workgroup owns R = 32 or 64 output channels x `ipt` WHOLE images, so each of its records
+//     is one contiguous NCHW run per image (the store pattern that writes at ~5.3 TB/s on 14x14
+//     planes against ~2.4 for image-crossing 128-column tiles, profiles/r02j_store_patterns.txt);
+//   * the K loop walks the input channels in stages of CC channels (32 for 3x3, 128 for 1x1);
+//     each stage brings the patch of those channels for the tile's images -- the output pixels'
+//     receptive field incl. the one-pixel halo, out-of-image pixels holding the input zero point --
+//     and the R weight rows of all taps of those channels, both by LDS-DMA into one ring slot that
+//     all four waves read: every input pixel crosses L2 -> LDS once per stage, not once per tap,
+//     and every weight byte once per workgroup, not once per wave (which sank the round-2
+//     patch-tile kernel, profiles/r02g_patch_ab.txt);
+//   * the 3x3 weights are read from a second, chunked packing [rows][cin_pad/32][9][32] so that a
+//     stage's rows are contiguous (conv_img_pack); 1x1 weights use the plain packing.
+// Arithmetic: the same zero-point fold (weights' zero point 0: out = Σ a'w − za·Σw, out-of-bounds
+// taps hold a' = za, python/tvm/relay/qnn/op/legalizations.py:195-226), bias_add, RequantizeLowerInt
+// (src/relay/qnn/op/requantize.cc:195-273), qnn.add (src/relay/qnn/op/add.cc:40-96) and clip
+// (python/tvm/topi/math.py:615-640) as the other conv-block kernels; parity: tests/test_gpu_ops.py.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <type_traits>
+
+#include "tk_conv.h"
+
+namespace tk {
+
+constexpr int kImgNI = 12;  // most LDS-DMA wave-instructions per wave and stage
+
+struct ImgArgs {
+  const int8_t* wimg;          // weight rows: chunked packing (3x3) or the plain one (1x1)
+  int32_t ldw;                 // bytes per weight row
+  int32_t nimg, ipt;           // images of the batch; whole images per workgroup
+  int32_t hr, hc, pl;          // patch rows / cols per image; patch pixels per channel group (ipt*hr*hc)
+  int32_t ih0, iw0, ls;        // input pixel of patch (0, 0); input pixels per patch pixel (strided 1x1)
+  int32_t ps;                  // patch pixels per output pixel (the stride of a 3x3)
+  int32_t hw, p, nct;          // output pixels per image and per workgroup; 32-column tiles
+  int32_t mtiles, wgs, wgs8;   // channel ranges; workgroups (rounded up to 8)
+  int32_t stages, ns;          // cin_pad / CC; ring slots
+  int32_t pslots, wslot, sslots, ni, stage_bytes;  // 16-byte LDS slots of a stage: patch, per weight
+                                                   // row, all; DMA instructions per wave; ring slot bytes
+  int32_t pstep;               // patch source bytes per stage (CC/16 shadow channel groups)
+  int32_t tstride;             // int32 pitch of the epilogue staging rows
+  int32_t rowc_off, lut_off, res_off;  // LDS byte offsets (the staging tile aliases the ring at 0)
+  uint64_t mg_pl, mg_img, mg_hc, mg_ws, mg_hw, mg_ow, mg_runq, mg_pe;  // (x * mg) >> 40 == x / d
+  int32_t runq;                // 4-element epilogue groups per image run (R * hw / 4)
+};
+
+// KT: 1 or 3 taps per axis; WM: 32-row wave groups (R = 32 * WM); CT: 32-column tiles per wave
+// (the waves of a row group take columns wn, wn + WN, ...).
+template <int KT, int WM, int CT>
+__global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, ImgArgs h) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  __shared__ int s_fast;
+  constexpr int R = 32 * WM;
+  constexpr int WN = 4 / WM;
+  constexpr int CC = KT == 3 ? 32 : 128;  // input channels per stage
+  constexpr int TAPS = KT * KT;
+  constexpr int SUB = CC / 32;             // K = 32 MFMA steps per tap and stage
+  constexpr int KS = TAPS * SUB;           // K = 32 MFMA steps per stage
+  constexpr int WROW = TAPS * CC + 16;     // LDS bytes per weight row: one pad chunk (bank spread)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  [[maybe_unused]] const int abl = g.ablate;
+  // XCD x runs a contiguous chunk of workgroups; the channel ranges of one patch are adjacent
+  const int L = blockIdx.x;
+  const int w = (L & 7) * (h.wgs8 >> 3) + (L >> 3);
+  if (w >= h.wgs) return;
+  const int mt = w % h.mtiles;
+  const int img0 = (w / h.mtiles) * h.ipt;
+  const int nimg = min(h.ipt, h.nimg - img0);
+  const int m0 = mt * R;
+  const int hw = h.hw;
+  int32_t* tileI = reinterpret_cast<int32_t*>(smem);  // epilogue staging, over the ring
+  EpiRow* rowc = reinterpret_cast<EpiRow*>(smem + h.rowc_off);
+  int32_t* lut = reinterpret_cast<int32_t*>(smem + h.lut_off);
+  uint32_t* resw = reinterpret_cast<uint32_t*>(smem + h.res_off);
+  const int8_t* fill_src = reinterpret_cast<const int8_t*>(tk_fill_rows.v + 16 * (g.fill & 0xFFu));
+  const bool has_add = g.has_add;
+  const int runq = h.runq;
+  const int total = nimg * runq;  // epilogue groups
+  if (tid == 0) s_fast = 1;       // visible after the first barrier; only cleared at the epilogue
+
+  // ---- residual words of every epilogue group (qnn.add joins), LDS-DMA'd in group order during
+  // the last K step (after its barrier: no counted ring wait follows, the epilogue's full wait
+  // covers them), so that they neither delay the first stages nor expose their latency
+  auto issue_residual = [&]() __attribute__((always_inline)) {
+    for (int q0 = wave * 64; q0 < total; q0 += kGemmThreads) {
+      const int gi = q0 + lane;
+      const int8_t* src = reinterpret_cast<const int8_t*>(tk_zero_words);
+      if (gi < total) {
+        const int kk = (int)fdiv40((uint32_t)gi, h.mg_runq);
+        const int f = (gi - kk * runq) * 4;
+        src = reinterpret_cast<const int8_t*>(g.add_res) + (uint32_t)(((img0 + kk) * g.M + m0) * hw + f);
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(resw + q0), 4, 0, 0);
+    }
+  };
+  // ---- row constants (threads < R): they land during the K loop
+  const bool rq_axis = g.rq.mode >= TK_RQ_AXIS_UPWARD;
+  EpiRow row_pre{};
+  if (tid < R) {
+    const int row = m0 + tid;
+    row_pre.ra = (uint32_t)ldg(g.RA + row);
+    row_pre.bias = ldg(g.bias + row);
+    row_pre.m = ldg(rq_axis ? g.rq.ms + row : tk_zero_words);
+    row_pre.s = ldg(rq_axis ? g.rq.ss + row : tk_zero_words);
+    row_pre.zp = ldg(g.rq.zps ? g.rq.zps + row : tk_zero_words);
+  }
+
+  // ---- LDS-DMA sources of this lane: slot q = (wave + 4k) * 64 + lane of every stage is patch
+  // chunk (group q / pl, pixel q % pl) or weight chunk (row, 16-byte chunk) or slack; each source
+  // advances by a fixed step per stage (0 for the zero-point fill and the pad chunks)
+  const int ni = h.ni;
+  const int8_t* srcs[kImgNI];
+  uint32_t steps[kImgNI];
+#pragma unroll
+  for (int k = 0; k < kImgNI; ++k) {
+    srcs[k] = fill_src;
+    steps[k] = 0;
+    if (k < ni) {
+      const uint32_t q = (uint32_t)((wave + 4 * k) * 64 + lane);
+      if (q < (uint32_t)h.pslots) {
+        const uint32_t grp = fdiv40(q, h.mg_pl), pix = q - grp * h.pl;
+        const uint32_t kk = fdiv40(pix, h.mg_img), r = pix - kk * (h.hr * h.hc);
+        const uint32_t hrow = fdiv40(r, h.mg_hc), hcol = r - hrow * h.hc;
+        const int ih = h.ih0 + (int)hrow * h.ls, iw = h.iw0 + (int)hcol * h.ls;
+        const int img = img0 + (int)kk;
+        if (img < h.nimg && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
+          srcs[k] = g.B + ((int64_t)grp * g.in_pix + ((int64_t)img * g.H + ih) * g.W + iw) * 16;
+          steps[k] = (uint32_t)h.pstep;
+        }
+      } else if (q < (uint32_t)h.sslots) {
+        const uint32_t wq = q - h.pslots;
+        const uint32_t row = fdiv40(wq, h.mg_ws), c = wq - row * h.wslot;
+        if (c + 1 < (uint32_t)h.wslot) {
+          srcs[k] = h.wimg + (int64_t)(m0 + row) * h.ldw + c * 16;
+          steps[k] = TAPS * CC;
+        }
+      }
+    }
+  }
+  auto issue = [&](int slot) __attribute__((always_inline)) {
+    int8_t* dst = smem + slot * h.stage_bytes + wave * 1024;
+#pragma unroll
+    for (int k = 0; k < kImgNI; ++k)
+      if (k < ni) {
+        if (!TK_ABL(128)) __builtin_amdgcn_global_load_lds((const void*)srcs[k], (void*)(dst + k * 4096), 16, 0, 0);
+        srcs[k] += steps[k];
+      }
+  };
+
+  // ---- fragment addresses: A = weights (row = lane % 32 of this wave's row group), B = patch
+  // (column = output pixel of the tile, lane % 32 of each column tile); lane / 32 = 16-byte K half
+  int jn = 0;  // column tiles of this wave (wave-uniform)
+#pragma unroll
+  for (int j = 0; j < CT; ++j) jn += (wn + WN * j < h.nct) ? 1 : 0;
+  int boff[CT];
+#pragma unroll
+  for (int j = 0; j < CT; ++j) {
+    const uint32_t c = (uint32_t)min((wn + WN * j) * 32 + (lane & 31), h.p - 1);
+    const uint32_t kk = fdiv40(c, h.mg_hw), r = c - kk * hw;
+    const uint32_t oh = fdiv40(r, h.mg_ow), ow = r - oh * g.OW;
+    boff[j] = (int)(((lane >> 5) * h.pl + kk * (h.hr * h.hc) + (oh * h.hc + ow) * h.ps) * 16);
+  }
+  const int aoff = h.pslots * 16 + (wm * 32 + (lane & 31)) * WROW + (lane >> 5) * 16;
+  const int hc = h.hc, pl16 = h.pl * 16;
+
+  v16i acc[CT];
+#pragma unroll
+  for (int j = 0; j < CT; ++j) acc[j] = v16i{0};
+  auto compute = [&](const int8_t* base) __attribute__((always_inline)) {
+    v4i a[2], b[2][CT];
+    auto rd = [&](int ks, int u) __attribute__((always_inline)) {
+      const int t = ks / SUB, s = ks - t * SUB, kh = t / KT, kw = t - kh * KT;
+      a[u] = *reinterpret_cast<const v4i*>(base + aoff + t * CC + s * 32);
+      const int bo = 2 * s * pl16 + (kh * hc + kw) * 16;
+#pragma unroll
+      for (int j = 0; j < CT; ++j)
+        if (j < jn) b[u][j] = *reinterpret_cast<const v4i*>(base + boff[j] + bo);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) rd(ks + 1, (ks + 1) & 1);
+      if (!TK_ABL(512)) {
+#pragma unroll
+        for (int j = 0; j < CT; ++j)
+          if (j < jn) acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1], b[ks & 1][j], acc[j], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- K loop: an ns-slot ring with ns - 1 stages in flight (ns from the plan: as many slots as
+  // the LDS holds, since one workgroup per CU has nothing else to hide the L2 -> LDS latency
+  // with); after the barrier of stage it, the slot read in step it - 1 is free for stage
+  // it + ns - 1
+  const int nst = h.stages, ns = h.ns;
+  for (int st = 0; st < ns - 1 && st < nst; ++st) issue(st);
+  int cur = 0, nxt = ns - 1;
+  for (int it = 0; it < nst; ++it) {
+    wait_vm_any(min(ns - 2, nst - 1 - it) * ni);
+    lds_barrier();
+    if (it + ns - 1 < nst) {
+      issue(nxt);
+      nxt = nxt == ns - 1 ? 0 : nxt + 1;
+    }
+    if (has_add && it == nst - 1) issue_residual();
+    compute(smem + cur * h.stage_bytes);
+    cur = cur == ns - 1 ? 0 : cur + 1;
+  }
+  wait_vm(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler
+  if (TK_ABL(4)) return;
+
+  // ---- epilogue: stage the tile (rows = channels m0.., columns = the images' pixels) in LDS
+  lds_barrier();  // the ring is free
+  if (tid < R) {
+    EpiRow r = row_pre;
+    if (!rq_axis) r.m = g.rq.multiplier, r.s = g.rq.shift;
+    if (!g.rq.zps) r.zp = g.rq.zp_in;
+    r.fold = (uint32_t)0 - (uint32_t)g.zB * r.ra;  // weights' zero point 0: the fold is -za * rowsum
+    if (r.s > -2) s_fast = 0;
+    rowc[tid] = r;
+  }
+  if (has_add) {
+    // RequantizeOrUpcast of every 8-bit value of both qnn.add operands (op_common.h:186-200)
+    const int32_t x = g.rq.qmin == 0 ? tid : (int32_t)(int8_t)(uint8_t)tid;
+    lut[tid] = g.add_up_b ? x : rq_tensor(x, g.add_pb);
+    lut[256 + tid] = g.add_up_r ? x : rq_tensor(x, g.add_pr);
+  }
+  const int ts = h.tstride;
+#pragma unroll
+  for (int j = 0; j < CT; ++j)
+    if (j < jn) {
+      const int lc = (wn + WN * j) * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tileI[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * ts + lc] = acc[j][r];
+    }
+  lds_barrier();
+
+  // group gi = 4 consecutive elements of image run kk = gi / runq (channels m0 .. m0 + R, all hw
+  // pixels: contiguous NCHW memory), element f = 4 (gi % runq) = row r0 (channel m0 + r0), pixel p0.
+  // A thread's groups are 256 apart: the walk advances (kk, r0, p0) by 1024 elements per step
+  // without divisions.  hw % 4 == 0: a group lies in one channel row (one b128 read of the tile,
+  // one row of constants); else (7x7) it may cross into the next row, whose elements take that
+  // row's constants.
+  const uint32_t n4 = g.out_elems * 4u;
+  const auto r_conv = rec_rsrc(g.C, n4), r_bias = rec_rsrc(g.bias_out, n4);
+  const auto r_rq = rec_rsrc(g.rq_out, g.out_elems);
+  const auto r_add = rec_rsrc(g.add_out, has_add ? g.out_elems : 0u);
+  const auto r_clip = rec_rsrc(g.clip_out, g.has_clip ? g.out_elems : 0u);
+  const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
+  const int32_t clip_lo = g.clip_lo, clip_hi = g.clip_hi, add_zp = g.add_zp;
+  const int mode = g.rq.mode, Mrows = g.M;
+  const int dr = 1024 / hw, dp = 1024 - dr * hw;
+  auto walk = [&](auto fast_c, auto add_c, auto clip_c, auto rowu_c) __attribute__((always_inline)) {
+    constexpr bool FAST = decltype(fast_c)::value, ADD = decltype(add_c)::value, CLIP = decltype(clip_c)::value;
+    constexpr bool ROWU = decltype(rowu_c)::value;
+    int kk = 0, r0 = (4 * tid) / hw, p0 = 4 * tid - r0 * hw;
+    while (r0 >= R) r0 -= R, ++kk;
+    for (int gi = tid; gi < total; gi += kGemmThreads) {
+      const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0) * hw + r0 * hw + p0);
+      const int base = r0 * ts + kk * hw + p0;
+      v4u v;
+      EpiRow ra, rb;
+      ra = rowc[r0];
+      if constexpr (ROWU) {
+        v = *reinterpret_cast<const v4u*>(tileI + base);
+        rb = ra;
+      } else {
+        rb = rowc[min(r0 + 1, R - 1)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (uint32_t)tileI[base + e + (p0 + e >= hw ? ts - hw : 0)];
+      }
+      uint32_t fold[4], zp[4];
+      int32_t bias[4], m[4], sh[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool nx = !ROWU && p0 + e >= hw;
+        fold[e] = nx ? rb.fold : ra.fold;
+        bias[e] = nx ? rb.bias : ra.bias;
+        zp[e] = nx ? (uint32_t)rb.zp : (uint32_t)ra.zp;
+        m[e] = nx ? rb.m : ra.m;
+        sh[e] = nx ? rb.s : ra.s;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += fold[e];
+      if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += (uint32_t)bias[e];
+      if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
+      int32_t q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int32_t t = (int32_t)(v[e] - zp[e]);
+        int32_t y;
+        if constexpr (FAST) {
+          // right shift >= 2: (x·m + 2^(30+rs)) >> (31+rs) only needs the high word of x·m
+          const int sh2 = -sh[e] - 1;
+          y = (int32_t)((uint32_t)__mulhi(t, m[e]) + (1u << (sh2 - 1))) >> sh2;
+        } else {
+          y = rq_core(t, mode, m[e], sh[e]);
+        }
+        q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
+      }
+      if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
+      if constexpr (ADD) {
+        // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
+        const uint32_t res = resw[gi];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((res >> (8 * e)) & 0xFFu)] - add_zp, qmin, qmax);
+        if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
+      }
+      if constexpr (CLIP) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
+        if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
+      }
+      if constexpr (ROWU) {
+        *reinterpret_cast<v4i*>(tileI + base) = v4i{q[0], q[1], q[2], q[3]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tileI[base + e + (p0 + e >= hw ? ts - hw : 0)] = q[e];
+      }
+      // next group: 1024 elements on
+      r0 += dr;
+      p0 += dp;
+      if (p0 >= hw) p0 -= hw, ++r0;
+      while (r0 >= R) r0 -= R, ++kk;
+    }
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  auto by_rowu = [&](auto fast_c, auto add_c, auto clip_c) __attribute__((always_inline)) {
+    if (hw % 4 == 0) walk(fast_c, add_c, clip_c, T{});
+    else walk(fast_c, add_c, clip_c, F{});
+  };
+  auto by_clip = [&](auto fast_c, auto add_c) __attribute__((always_inline)) {
+    if (g.has_clip) by_rowu(fast_c, add_c, T{});
+    else by_rowu(fast_c, add_c, F{});
+  };
+  auto by_add = [&](auto fast_c) __attribute__((always_inline)) {
+    if (has_add) by_clip(fast_c, T{});
+    else by_clip(fast_c, F{});
+  };
+  if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) by_add(T{});
+  else by_add(F{});
+
+  // ---- the next conv's shadow: 16 channels of one pixel per 16-byte store; the tile's columns are
+  // the images' pixels in order, so column c is shadow pixel img0 * hw + c
+  if (g.shadow_out && !TK_ABL(1)) {
+    lds_barrier();
+    const int pe = nimg * hw;
+    const int items = (R / 16) * pe;
+    for (int it = tid; it < items; it += kGemmThreads) {
+      const int grp = (int)fdiv40((uint32_t)it, h.mg_pe);
+      const int col = it - grp * pe;
+      uint32_t wd[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          word |= (((uint32_t)tileI[(grp * 16 + d * 4 + qq) * ts + col] ^ g.shadow_xor) & 0xFFu) << (8 * qq);
+        wd[d] = word;
+      }
+      *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)((m0 >> 4) + grp) * g.N + (int64_t)img0 * hw + col) * 16) =
+          v4i{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+    }
+  }
+}
+
+// ---------------------------------------------------------------- chunked weight packing
+// OIHW (int8, or uint8 stored xor 0x80) -> [rows_pad][cin_pad / 32][taps][32]: a stage of 32 input
+// channels is one contiguous run of taps * 32 bytes per row.  Padding rows / channels are 0.
+__global__ __launch_bounds__(256) void pack_chunked_kernel(const int8_t* __restrict__ w, int8_t* __restrict__ dst,
+                                                           int Cout, int Cin, int taps, int cin_pad, int xor_u8) {
+  const int o = blockIdx.x;
+  const int row = taps * cin_pad;
+  for (int k = threadIdx.x; k < row; k += blockDim.x) {
+    const int c32 = k / (taps * 32), rem = k - c32 * taps * 32;
+    const int tap = rem >> 5, c = c32 * 32 + (rem & 31);
+    int8_t v = 0;
+    if (o < Cout && c < Cin) {
+      const uint8_t raw = (uint8_t)w[((int64_t)o * Cin + c) * taps + tap];
+      v = (int8_t)(xor_u8 ? (raw ^ 0x80) : raw);
+    }
+    dst[(int64_t)o * row + k] = v;
+  }
+}
+
+int64_t conv_img_chunked_bytes(int rows_pad, int cin_pad, int taps) {
+  return taps > 1 && cin_pad % 32 == 0 ? (int64_t)rows_pad * taps * cin_pad : 0;
+}
+
+int conv_img_pack(const tk_tensor* weight, int8_t* dst, int rows_pad, int cin_pad, hipStream_t s) {
+  const int O = (int)weight->shape[0], C = (int)weight->shape[1];
+  const int taps = (int)(weight->shape[2] * weight->shape[3]);
+  if (!conv_img_chunked_bytes(rows_pad, cin_pad, taps)) return TK_OK;
+  hipLaunchKernelGGL(pack_chunked_kernel, dim3(rows_pad), dim3(256), 0, s, (const int8_t*)ptr(weight), dst, O, C, taps,
+                     cin_pad, (int)is_uint(weight, 8));
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
+// ---------------------------------------------------------------- plan + launch
+namespace {
+
+using ImgKernel = void (*)(GemmArgs, ImgArgs);
+
+template <int KT, int WM>
+ImgKernel img_kernel(int ct) {
+  switch (ct) {
+    case 2: return conv_img_kernel<KT, WM, 2>;
+    case 4: return conv_img_kernel<KT, WM, 4>;
+    default: return conv_img_kernel<KT, WM, 7>;
+  }
+}
+
+struct ImgPlan {
+  ImgArgs a;
+  size_t lds;
+  int kt, wm, ct;
+  double cost;
+};
+
+uint64_t magic40(uint64_t d) { return ((1ull << 40) + d - 1) / d; }
+
+// One candidate tiling (R rows, ipt images per workgroup); false if it does not fit.
+bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R, int ipt, ImgPlan* out) {
+  const int CC = kt == 3 ? 32 : 128;
+  const int taps = kt * kt;
+  const int hw = g.OH * g.OW;
+  const int p = ipt * hw;
+  const int nct = (p + 31) / 32;
+  const int wm = R / 32, wn = 4 / wm;
+  const int ct_need = (nct + wn - 1) / wn;
+  const int ct = ct_need <= 2 ? 2 : ct_need <= 4 ? 4 : ct_need <= 7 ? 7 : 0;
+  if (!ct || (ct == 7 && wm != 1)) return false;
+  ImgArgs x{};
+  x.nimg = g.N;
+  x.ipt = ipt;
+  x.hr = kt == 3 ? (g.OH - 1) * st + 3 : g.OH;
+  x.hc = kt == 3 ? (g.OW - 1) * st + 3 : g.OW;
+  x.pl = ipt * x.hr * x.hc;
+  x.ih0 = kt == 3 ? -1 : 0;
+  x.iw0 = kt == 3 ? -1 : 0;
+  x.ls = kt == 3 ? 1 : st;
+  x.ps = kt == 3 ? st : 1;
+  x.hw = hw;
+  x.p = p;
+  x.nct = nct;
+  x.mtiles = g.O / R;
+  x.wgs = (int32_t)(((int64_t)g.N + ipt - 1) / ipt * x.mtiles);
+  x.wgs8 = (x.wgs + 7) / 8 * 8;
+  x.stages = g.cin_pad / CC;
+  x.pslots = CC / 16 * x.pl;
+  x.wslot = taps * CC / 16 + 1;
+  x.sslots = x.pslots + R * x.wslot;
+  x.ni = ((x.sslots + 63) / 64 + 3) / 4;
+  if (x.ni > kImgNI) return false;
+  x.stage_bytes = 4 * x.ni * 1024;
+  const int64_t pstep = (int64_t)(CC / 16) * ga.in_pix * 16;
+  if (pstep >= (1ll << 31)) return false;
+  x.pstep = (int32_t)pstep;
+  x.tstride = nct * 32 + 4;
+  // ring depth: every slot the LDS holds (up to 8, no more than the stages need), at least 3 where
+  // there are more than 2 stages.  Grids of several rounds keep two workgroups per CU (80 KB each)
+  // when that still gives 3 slots: one workgroup's epilogue stores then overlap the other's K loop.
+  const size_t extra = (size_t)R * sizeof(EpiRow) + 2048 + (ga.has_add ? ((size_t)p * R + 255) / 256 * 256 : 0);
+  const size_t tile = (size_t)R * x.tstride * 4;
+  const int cap = env_int("TK_IMG_NS", 8);
+  auto slots = [&](size_t budget) -> int {
+    if (tile > budget) return 0;
+    return (int)std::min<size_t>({(size_t)cap, budget / x.stage_bytes, (size_t)x.stages + 1});
+  };
+  const int need = x.stages > 2 ? 3 : 2;
+  const size_t half = 80 * 1024 - 64 - extra, full = 160 * 1024 - 64 - extra;
+  x.ns = x.wgs > 256 && slots(half) >= need && env_int("TK_IMG_TWO", 1) ? slots(half) : slots(full);
+  if (x.ns < need) return false;
+  const size_t ring = (size_t)x.ns * x.stage_bytes;
+  x.rowc_off = (int32_t)std::max(ring, tile);
+  x.lut_off = x.rowc_off + R * (int)sizeof(EpiRow);
+  x.res_off = x.lut_off + 2048;
+  const size_t lds = (size_t)x.res_off + (ga.has_add ? ((size_t)p * R + 255) / 256 * 256 : 0);
+  if (lds > 160 * 1024 - 64) return false;
+  x.runq = R * hw / 4;
+  x.mg_pl = magic40(x.pl);
+  x.mg_img = magic40((uint64_t)x.hr * x.hc);
+  x.mg_hc = magic40(x.hc);
+  x.mg_ws = magic40(x.wslot);
+  x.mg_hw = magic40(hw);
+  x.mg_ow = magic40(g.OW);
+  x.mg_runq = magic40(x.runq);
+  x.mg_pe = magic40(p);
+  out->a = x;
+  out->lds = lds;
+  out->kt = kt;
+  out->wm = wm;
+  out->ct = ct;
+  // estimated time: rounds of one workgroup per CU x max(L2 -> LDS bytes at ~55 GB/s per CU, the
+  // busiest wave's MFMA cycles at ~2.1 GHz); the record stores are the same for every candidate
+  const double K = (double)taps * g.cin_pad;
+  const double bytes = R * K + (double)x.pl * g.cin_pad;
+  const double mfma_ns = ct_need * K / 2.1;
+  const double rounds = std::ceil(x.wgs / 256.0);
+  out->cost = rounds * std::max(bytes / 55.0, mfma_ns);
+  return true;
+}
+
+}  // namespace
+
+int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked,
+                 hipStream_t s, int* rc) {
+  if (!env_int("TK_IMG", 1) || !ga.bias_out) return 0;  // conv blocks only
+  if (ga.RB || ga.zA_vec || ga.zA != 0) return 0;       // the weights' zero point must be 0
+  if (a->dilation[0] != 1 || a->dilation[1] != 1) return 0;
+  const int st = a->strides[0];
+  if (a->strides[1] != st || (st != 1 && st != 2)) return 0;
+  int kt = 0;
+  if (g.KH == 3 && g.KW == 3 && a->padding[0] == 1 && a->padding[1] == 1 && a->padding[2] == 1 && a->padding[3] == 1)
+    kt = 3;
+  else if (g.KH == 1 && g.KW == 1 && !a->padding[0] && !a->padding[1] && !a->padding[2] && !a->padding[3])
+    kt = 1;
+  if (!kt || (kt == 3 && !chunked)) return 0;
+  if (kt == 3 && !env_int("TK_IMG3", 1)) return 0;
+  if (kt == 1 && !env_int("TK_IMG1", 1)) return 0;
+  const int CC = kt == 3 ? 32 : 128;
+  const int hw = g.OH * g.OW;
+  if (g.cin_pad % CC || g.O % 32 || hw > env_int("TK_IMG_MAXHW", 256) || hw < 4 ||
+      (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll)
+    return 0;
+  ImgPlan best{}, c{};
+  bool have = false;
+  const int force_r = env_int("TK_IMG_R", 0), force_ipt = env_int("TK_IMG_IPT", 0);
+  for (int R : {64, 32}) {
+    if (g.O % R || (force_r && R != force_r)) continue;
+    for (int ipt = std::min(256 / hw, g.N); ipt >= 1; --ipt) {
+      if (force_ipt && ipt != force_ipt) continue;
+      if (img_candidate(g, ga, kt, st, R, ipt, &c) && (!have || c.cost < best.cost)) best = c, have = true;
+    }
+  }
+  if (!have) return 0;
+  best.a.wimg = kt == 3 ? chunked : ga.A;
+  best.a.ldw = kt == 3 ? 9 * g.cin_pad : ga.lda;
+  ImgKernel kern = kt == 3 ? (best.wm == 2 ? img_kernel<3, 2>(best.ct) : img_kernel<3, 1>(best.ct))
+                           : (best.wm == 2 ? img_kernel<1, 2>(best.ct) : img_kernel<1, 1>(best.ct));
+  if (best.lds > 64 * 1024) {
+    // dynamic LDS beyond 64 KiB must be allowed per kernel (the static s_fast word counts too)
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)best.lds);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      set_error(std::string("conv image-tile kernel: LDS attribute failed: ") + hipGetErrorString(e));
+      *rc = TK_ERR_HIP;
+      return 1;
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)best.a.wgs8), dim3(kGemmThreads), best.lds, s, ga, best.a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string("conv image-tile kernel: launch failed: ") + hipGetErrorString(e));
+    *rc = TK_ERR_HIP;
+    return 1;
+  }
+  *rc = TK_OK;
+  return 1;
+}
+
+}  // namespace tk

@@ -560,6 +560,66 @@ int copy_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s) {
   return TK_OK;
 }
 
+// ---------------------------------------------------------------- nn.pad
+// One thread per output element (its index decomposed over up to 6 dimensions, innermost first):
+// inside the data's range it copies data[i - before], else writes the pad value.
+struct PadGeom {
+  int32_t ndim;
+  int64_t out_shape[6], in_shape[6], before[6];
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void pad_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n, PadGeom g,
+                                                     T value) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += stride) {
+    int64_t r = i, src = 0, pitch = 1;
+    bool inside = true;
+    for (int d = g.ndim - 1; d >= 0; --d) {
+      const int64_t c = r % g.out_shape[d] - g.before[d];
+      r /= g.out_shape[d];
+      inside = inside && c >= 0 && c < g.in_shape[d];
+      src += c * pitch;
+      pitch *= g.in_shape[d];
+    }
+    y[i] = inside ? x[src] : value;
+  }
+}
+
+int pad_impl(const tk_tensor* x, tk_tensor* y, const tk_pad_attrs* a, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a && compact(x) && compact(y), "bad arguments");
+  TK_CHECK_ARG(x->ndim == y->ndim && x->ndim >= 1 && x->ndim <= 6 && x->dtype.code == y->dtype.code &&
+                   x->dtype.bits == y->dtype.bits && x->dtype.lanes == 1,
+               "pad: same dtype, 1-6 dimensions");
+  PadGeom g{};
+  g.ndim = x->ndim;
+  for (int d = 0; d < x->ndim; ++d) {
+    TK_CHECK_ARG(a->before[d] >= 0 && a->after[d] >= 0 && y->shape[d] == x->shape[d] + a->before[d] + a->after[d],
+                 "pad: output shape must be the padded input shape");
+    g.out_shape[d] = y->shape[d];
+    g.in_shape[d] = x->shape[d];
+    g.before[d] = a->before[d];
+  }
+  const int64_t n = numel(y);
+  if (n == 0) return TK_OK;
+  auto launch = [&](auto tag, auto value) -> int {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((pad_kernel<T>), dim3(grid_for(n)), dim3(kBlock), 0, s, (const T*)ptr(x), (T*)ptr(y), n, g,
+                       (T)value);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  };
+  if (is_f32(x)) return launch(float{}, (float)a->value_f);
+  switch (x->dtype.bits) {
+    case 8: return launch(uint8_t{}, (uint8_t)a->value_i);
+    case 16: return launch(uint16_t{}, (uint16_t)a->value_i);
+    case 32: return launch(uint32_t{}, (uint32_t)a->value_i);
+    case 64: return launch(uint64_t{}, (uint64_t)a->value_i);
+  }
+  set_error("pad: unsupported dtype");
+  return TK_ERR_INVALID_ARG;
+}
+
 // ---------------------------------------------------------------- digest
 // Order-aware, parallel 64-bit digest: Σ_i mix(word_i ^ (i · φ)) mod 2^64 over
 // little-endian 8-byte words (tail zero-padded).  Host twin: trace_format.digest_bytes.

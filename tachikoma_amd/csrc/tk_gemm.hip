@@ -21,87 +21,9 @@
 #include <cstdlib>
 #include <cstring>
 
-#include "tk_common.h"
+#include "tk_conv.h"
 
 namespace tk {
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-
-constexpr int kBK = 64;          // bytes of K per stage
-constexpr int kGemmThreads = 256;
-constexpr int kEpiStride = 132;  // dwords per LDS row of the epilogue tile (128 + 4: breaks the 64-bank period)
-
-struct GemmArgs {
-  const int8_t* A;     // [rowsA_pad][lda]
-  const int8_t* B;     // plain: [rowsB_pad][ldb]; im2col: shadow [cin_pad/16][N*H*W][16]
-  int32_t* C;
-  int32_t M, N;        // real rows of A / rows of B (pixels for conv)
-  int32_t lda, ldb;    // row pitch in bytes (plain), K_pad
-  int32_t k_pad;       // multiple of kBK
-  int32_t k_eff;       // real reduction length (for the K·zA·zB term)
-  // zero-point folding: out = acc - zB[j]*RA[i] - zA[i]*RB[j] + k_eff*zA[i]*zB[j]
-  int32_t zA, zB;
-  const int32_t* zA_vec;  // per row of A (optional)
-  const int32_t* zB_vec;  // per row of B (optional)
-  const int32_t* RA;      // row sums of A (needed when zB != 0)
-  const int32_t* RB;      // row sums of B (needed when zA != 0)
-  // im2col geometry (conv)
-  int32_t H, W, cin_pad, KH, KW, sh, sw, pt, pl, dh, dw, OH, OW;
-  int64_t in_pix;                 // N*H*W of the input: pixels per channel group of the shadow
-  uint32_t fill;                  // za replicated 4x: out-of-bounds taps (padded channels multiply w = 0)
-  int32_t taps;                   // KH*KW
-  // output addressing
-  int32_t out_nchw;    // 1: C[(p/HW)*M*HW + i*HW + p%HW]; 0: C[i*N + j]
-  int32_t ldc;         // row-major pitch (elements) when !out_nchw
-  // fused block epilogue (bias_add -> requantize -> clip), see BlockEpi
-  int32_t* bias_out;
-  uint8_t* rq_out;
-  uint8_t* clip_out;
-  uint8_t* shadow_out;  // shadow [shadow_cpad/16][N][16] of the last output (conv blocks)
-  const int32_t* bias;
-  RqParams rq;
-  int32_t has_clip, clip_lo, clip_hi, shadow_cpad;
-  uint32_t shadow_xor;  // 0x80 when the block output is uint8 (shadow stores int8 = u8 ^ 0x80)
-  int32_t ch_is_row;    // channel index = row (conv: Cout) or column (dense: units)
-  int32_t vecw;         // epilogue store vector (4 or 1 elements): divides the plane / row length
-  // split-K (small grids): kMode 1 writes raw partial tiles for k-steps [z*kper, (z+1)*kper) to ws,
-  // kMode 2 sums `splits` of them and runs the epilogue
-  int32_t* ws;
-  int32_t splits, kper;
-  // tile grid: 1-D launch of mtiles * ntiles8 workgroups (ntiles rounded up to 8), see tile_of
-  int32_t mtiles, ntiles, ntiles8, xcd_order;
-  // residual join (conv blocks): add = RQ(requantize) + RQ(residual) - zp, via 256-entry LUTs
-  int32_t has_add, add_zp, add_up_b, add_up_r;
-  const uint8_t* add_res;
-  uint8_t* add_out;
-  RqParams add_pb, add_pr;
-  // lean im2col walk (unitap): every 64-byte K stage lies in one tap (cin_pad % 64 == 0, or a
-  // 1x1 conv), so the stage's source offset is uniform and each lane only tests its row's
-  // tap bitmask (taps <= 64); cgroups = cin_pad / 16
-  int32_t unitap, cgroups;
-  // p / (OH*OW) and p / OW as (p * magic) >> 40 (0: plain division), exact for p * d < 2^40
-  uint64_t mg_hw, mg_ow;
-  // fast block epilogue (conv blocks, 4-column vectors, requantize UPWARD): every record
-  // byte offset fits 32 bits, so stores go through buffer descriptors; 1 = nontemporal
-  // record stores, 2 = plain ones
-  int32_t fast_epi;
-  uint32_t out_elems;   // N * M: elements of each record
-  int32_t nt;           // nontemporal record stores
-  // image-aligned N tiles (conv blocks with planes of <= 64 pixels): a tile holds ipt whole
-  // images (tcols = ipt * OH*OW of its 128 columns are used), so that for every image the
-  // tile's 64 channels x OH*OW pixels are one contiguous NCHW run: see the flat epilogue
-  int32_t ipt, tcols;
-  int32_t ablate;       // profiling only (TK_ABLATE env): 1 skip shadow, 2 skip stores, 4 skip epilogue,
-                       // 32768 flat epilogue without the lean groups, 65536 skip the flat groups,
-                       // 131072 flat epilogue without the lean row-crossing groups (hw % 4 != 0),
-                       // 8192 residual join without the LUTs, 16384 skip the add record,
-                       // 8/16/32/64 skip the conv / bias_add / requantize / clip record,
-                       // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs, 1024 main-loop
-                       // barrier without the lgkmcnt(0) drain, 2048 skip the fragment reads, 4096 skip
-                       // the main-loop barrier (timing skeletons only: results are garbage)
-};
 
 // Writes one element of every output of a fused block.  Mirrors, per element:
 // nn.bias_add (int32 wrap), RequantizeLowerInt + clip/cast to the out dtype
@@ -132,13 +54,6 @@ __device__ __forceinline__ uint32_t pack4(const int32_t* x) {
          ((uint32_t)x[3] << 24);
 }
 
-// Per-row constants of the fused epilogue (one output channel per row for conv
-// blocks), staged once per tile in LDS: 32 bytes, read back with two ds_read_b128.
-struct EpiRow {
-  uint32_t fold;  // K·zA·zB − zB·RA[row]: the whole zero-point correction when zB and RB are uniform/absent
-  uint32_t ra, za;
-  int32_t bias, m, s, zp, pad;
-};
 
 // record stores (nontemporal: see store_nt in tk_common.h)
 template <int V>
@@ -165,16 +80,6 @@ __device__ __forceinline__ void st_i8(uint8_t* dst, const int32_t* v, bool nt) {
 // soon as it is complete, transforming v in place (conv → bias_add → requantize →
 // clip); mirrors nn.bias_add (int32 wrap), RequantizeLowerInt + clip/cast
 // (src/relay/qnn/op/requantize.cc:195-273) and clip (python/tvm/topi/math.py:615-640).
-// requantize core of one element (mode is uniform; used where constants vary per element)
-__device__ __forceinline__ int32_t rq_core(int32_t t, int mode, int32_t m, int32_t sh) {
-  switch (mode) {
-    case TK_RQ_IDENTITY: return t;
-    case TK_RQ_TENSOR_POW2: return qms_pow2(t, sh);
-    case TK_RQ_TENSOR_TONEAREST:
-    case TK_RQ_AXIS_TONEAREST: return qms_tonearest(t, m, sh);
-    default: return qms_upward(t, m, sh);
-  }
-}
 
 // Column constants of a dense block (channel = column), loaded once per thread.
 __device__ __forceinline__ EpiRow col_consts(const GemmArgs& g, int col) {
@@ -255,29 +160,6 @@ __device__ __forceinline__ void epi_apply(const GemmArgs& g, const EpiRow& r, in
   }
 }
 
-// 16-byte rows of every byte value: the LDS-DMA source of out-of-bounds im2col taps
-// (the input zero point) and of padding rows (0); constant-initialised in device memory.
-struct FillRows {
-  uint8_t v[256 * 16];
-  constexpr FillRows() : v{} {
-    for (int i = 0; i < 256 * 16; ++i) v[i] = (uint8_t)(i >> 4);
-  }
-};
-__device__ FillRows tk_fill_rows{};
-__device__ int32_t tk_zero_words[4] = {0, 0, 0, 0};
-
-// Ablation switches of the profiling build (g.ablate, see GemmArgs::ablate); compiled out of
-// the product library.  Needs a local `abl` copy of g.ablate (lambdas must not touch g).
-#ifdef TK_ABLATION_BUILD
-#define TK_ABL(flag) (abl & (flag))
-#else
-#define TK_ABL(flag) 0
-#endif
-
-// Workgroup barrier that only drains this wave's LDS traffic.  __syncthreads() also waits
-// vmcnt(0), i.e. for every outstanding global store of the epilogue to complete, which
-// serialises the store latency once per barrier; the epilogue's barriers only order LDS.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // LDS tile [rows][64 B], 16-byte chunk c of row r stored at chunk c ^ ((r >> 2) & 3):
 // the 16-lane groups of ds_read_b128 then hit 16 distinct bank slots.
@@ -313,64 +195,7 @@ __device__ __forceinline__ void tile_of(const GemmArgs& g, int& mt, int& nt) {
 
 // kMode: 0 = whole K + epilogue; 1 = split-K partial (raw accumulators to g.ws);
 //        2 = sum the split-K partials of this tile + epilogue (no main loop).
-// load through a global-address-space pointer (struct members are generic pointers: flat
-// loads would wait on both vmcnt and lgkmcnt)
-template <typename T>
-__device__ __forceinline__ T ldg(const T* p) {
-  return *(const __attribute__((address_space(1))) T*)p;
-}
 
-// per-tensor requantize core (no per-channel arrays): the qnn.add operand tables
-__device__ __forceinline__ int32_t rq_tensor(int32_t t, const RqParams& p) {
-  t = (int32_t)((uint32_t)t - (uint32_t)p.zp_in);
-  switch (p.mode) {
-    case TK_RQ_TENSOR_POW2: t = qms_pow2(t, p.shift); break;
-    case TK_RQ_TENSOR_UPWARD: t = qms_upward(t, p.multiplier, p.shift); break;
-    case TK_RQ_TENSOR_TONEAREST: t = qms_tonearest(t, p.multiplier, p.shift); break;
-    default: break;
-  }
-  return (int32_t)((uint32_t)p.zp_out + (uint32_t)t);
-}
-
-// ---- fast conv-block epilogue helpers
-// buffer descriptor of a record (uniform base and size): stores at offsets >= bytes are
-// dropped by the range check, which masks the tile edges without branches
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
-constexpr int kAuxNT = 2;  // cache policy: nontemporal
-constexpr uint32_t kOffDrop = 0x3FFFFFF0u;  // element offset of a masked lane (x4 + 15 stays out of range)
-
-__device__ __forceinline__ uint32_t pack4u(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  // low bytes of a, b, c, d -> one dword (two v_perm_b32 + v_or)
-  const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0c0c0400u);
-  const uint32_t hi = __builtin_amdgcn_perm(d, c, 0x04000c0cu);
-  return lo | hi;
-}
-
-// min(max(x, lo), hi) in one v_med3_i32 (the compiler only forms it for constant bounds); needs
-// lo <= hi, which setup_block guarantees for the clip bounds (see there) and the dtype ranges are
-__device__ __forceinline__ int32_t clamp_i32(int32_t x, int32_t lo, int32_t hi) {
-  int32_t r;
-  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
-  return r;
-}
-
-// counted wait for this wave's global loads (vmcnt immediate): at most n outstanding
-__device__ __forceinline__ void wait_vm(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
 
 // kWide (im2col LDS-DMA path): 128-byte K stages instead of 64, i.e. half the
 // barrier-separated steps of long reductions (each step pays a fixed LDS / barrier / address
@@ -1278,351 +1103,6 @@ gemm_i8_kernel(GemmArgs g) {
   }
 }
 
-// ---------------------------------------------------------------- patch-tile conv blocks
-// 1x1 and 3x3 conv blocks whose input channels come in 64-channel steps (every ResNet layer but
-// the stem).  The im2col kernel above ends every tile with one burst of record stores, in step
-// across the whole grid (each layer's workgroups run in one round), so the stores of a small-grid
-// layer do not overlap any loads or MFMAs, and a 3x3 layer re-reads each input pixel 9 times
-// through the per-CU LDS-DMA fill path (profiles/r02b_block_ablations.txt, r02f_*).  Here:
-//   * a workgroup owns one spatial patch (ipt whole images of <= 224 pixels, or a band of th
-//     output rows) and a range of output channels, walked as nsub sub-tiles of R = 32 MF rows;
-//   * the patch's input (plus the one-pixel halo of a 3x3, strided pixels of a strided 1x1) is
-//     staged in LDS ONCE for all input channels as the shadow's 16-byte chunks; every tap's B
-//     fragment is an address into it (taps outside the image hold the input zero point);
-//   * 4 waves = 2 (MF 16-row fragments each) x 2 (column halves); weight fragments go straight
-//     from the packed weights into registers, D steps ahead, so the K loop has no barrier;
-//     v_mfma_i32_16x16x64_i8;
-//   * each sub-tile's epilogue stages its accumulators in LDS and writes every record in runs
-//     that are contiguous NCHW memory (an image's R channels, or one channel's band), 4 elements
-//     per lane, then the next conv's shadow; the stores are asynchronous, so they drain while the
-//     waves run the next sub-tile's K loop;
-//   * qnn.add residual joins read the residual bytes into registers during the K loop.
-// Same arithmetic as gemm_i8_kernel's conv blocks (zero-point fold, bias_add, requantize, add, clip).
-struct PatchArgs {
-  int32_t nimg;               // images in the batch
-  int32_t ipt, th, bands;     // images per patch, output rows per patch, row bands per image
-  int32_t hr, hc, plane;      // patch rows / cols per image; LDS pixels per channel group (x16)
-  int32_t ih0s, rs, cs;       // input row of patch row 0 = oh0 * stride + ih0s; row / col step
-  int32_t ps;                 // patch pixels per output pixel step (3x3: the stride; 1x1: 1)
-  int32_t pimg, p;            // output pixels per image-band and per patch
-  int32_t nf, nf0;            // 16-column fragments of the patch; of them, the wn = 0 waves'
-  int32_t stride;             // int32 pitch of the LDS staging rows
-  int32_t mchunks, nsub;      // workgroups per patch (channel ranges), sub-tiles per workgroup
-  int32_t wgs, wgs8;          // spatial patches * mchunks; rounded up to 8
-  int32_t steps, spt;         // 64-byte K steps; steps per tap (cin_pad / 64)
-  int32_t chunks;             // LDS-DMA chunks of the patch (cin_pad/16 * plane, rounded up to 64)
-  uint64_t mg_plane, mg_img, mg_hc, mg_pimg, mg_ow, mg_hw, mg_runq;  // (x * mg) >> 40 == x / d
-  int32_t runq;               // 4-element groups per epilogue run
-  int32_t whole;              // whole-image patches (run = an image's R channels), else row bands
-  int32_t stage_off, rowc_off, lut_off;  // LDS byte offsets
-};
-
-__device__ __forceinline__ uint32_t fdiv40(uint32_t x, uint64_t mg) { return (uint32_t)(((uint64_t)x * mg) >> 40); }
-
-template <int MF, int NFW, int KT>
-__global__ __launch_bounds__(kGemmThreads, 2) void conv_patch_kernel(GemmArgs g, PatchArgs h) {
-  extern __shared__ __attribute__((aligned(16))) int8_t hsm[];
-  __shared__ int s_fast;
-  constexpr int R = 32 * MF;                 // rows of a sub-tile
-  constexpr int D = MF == 2 ? 4 : NFW >= 7 ? 6 : 8;  // weight steps in flight per wave (even, see the loop)
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
-  const int wm = wave >> 1, wn = wave & 1;
-  [[maybe_unused]] const int abl = g.ablate;
-  // XCD x runs a contiguous chunk of workgroups; those of one patch are adjacent (its input in L2)
-  const int L = blockIdx.x;
-  const int w = (L & 7) * (h.wgs8 >> 3) + (L >> 3);
-  if (w >= h.wgs) return;
-  const int mc = w % h.mchunks, sp = w / h.mchunks;
-  const int band = sp % h.bands;
-  const int img0 = (sp / h.bands) * h.ipt;
-  const int nimg = min(h.ipt, h.nimg - img0);
-  const int oh0 = band * h.th;
-  const int mbase = mc * h.nsub * R;
-  int32_t* tileI = reinterpret_cast<int32_t*>(hsm + h.stage_off);
-  EpiRow* rowc = reinterpret_cast<EpiRow*>(hsm + h.rowc_off);
-  int32_t* lut = reinterpret_cast<int32_t*>(hsm + h.lut_off);
-  uint32_t* resw = reinterpret_cast<uint32_t*>(hsm + h.lut_off + 2048);  // residual words (joins only)
-
-  // ---- the patch: lane-linear LDS-DMA, chunk q = grp * plane + (kk * hr + r) * hc + c
-  {
-    const int8_t* fill_src = reinterpret_cast<const int8_t*>(tk_fill_rows.v + 16 * (g.fill & 0xFFu));
-    const int per_img = h.hr * h.hc;
-    const int ihb = oh0 * g.sh + h.ih0s, iwb = KT == 3 ? -g.pl : 0;
-    for (int q0 = wave * 64; q0 < h.chunks; q0 += kGemmThreads) {
-      const uint32_t q = q0 + lane;
-      const uint32_t grp = fdiv40(q, h.mg_plane);
-      const uint32_t pix = q - grp * h.plane;
-      const int8_t* src = fill_src;
-      if (grp < (uint32_t)g.cgroups && pix < (uint32_t)(h.ipt * per_img)) {
-        const uint32_t kk = fdiv40(pix, h.mg_img), r = pix - kk * per_img;
-        const uint32_t hrow = fdiv40(r, h.mg_hc), hcol = r - hrow * h.hc;
-        const int ih = ihb + (int)hrow * h.rs, iw = iwb + (int)hcol * h.cs;
-        const int img = img0 + (int)kk;
-        if (img < h.nimg && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
-          src = g.B + ((int64_t)grp * g.in_pix + ((int64_t)img * g.H + ih) * g.W + iw) * 16;
-      }
-      if (!TK_ABL(256)) __builtin_amdgcn_global_load_lds((const void*)src, (void*)(hsm + q0 * 16), 16, 0, 0);
-    }
-  }
-  const bool rq_axis = g.rq.mode >= TK_RQ_AXIS_UPWARD;
-  const bool has_add = g.has_add;
-  if (tid == 0) s_fast = 1;
-  if (has_add) {
-    // RequantizeOrUpcast of every 8-bit value of both qnn.add operands (op_common.h:186-200)
-    const int32_t x = g.rq.qmin == 0 ? tid : (int32_t)(int8_t)(uint8_t)tid;
-    lut[tid] = g.add_up_b ? x : rq_tensor(x, g.add_pb);
-    lut[256 + tid] = g.add_up_r ? x : rq_tensor(x, g.add_pr);
-  }
-
-  // ---- per-lane constants of the K loop
-  const int jbase = wn ? h.nf0 : 0;
-  int boff[NFW];  // B fragment j: byte offset of the lane's pixel, channel group (lane >> 4), tap (0, 0)
-#pragma unroll
-  for (int j = 0; j < NFW; ++j) {
-    const uint32_t c = min((jbase + j) * 16 + (lane & 15), h.p - 1);
-    const uint32_t kk = fdiv40(c, h.mg_pimg), r = c - kk * h.pimg;
-    const uint32_t oh = fdiv40(r, h.mg_ow), ow = r - oh * g.OW;
-    boff[j] = (int)(((lane >> 4) * h.plane + (kk * h.hr + oh * h.ps) * h.hc + ow * h.ps) * 16);
-  }
-  const int cblk = 4 * h.plane * 16;  // bytes between 64-channel blocks of the patch
-  const int last = (h.steps - 1) * kBK;
-  const int hw = g.OH * g.OW, OW = g.OW, Mrows = g.M;
-  const int total = (h.whole ? nimg : R) * h.runq;  // epilogue groups of a sub-tile
-  v4i abuf[D][MF];
-  auto prefetch_a = [&](int m0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < D; ++u)
-#pragma unroll
-      for (int i = 0; i < MF; ++i)
-        abuf[u][i] = ldg(reinterpret_cast<const v4i*>(g.A + (int64_t)(m0 + 16 * (MF * wm + i) + (lane & 15)) * g.lda +
-                                                      16 * (lane >> 4) + min(u * kBK, last)));
-  };
-  prefetch_a(mbase);
-  // the patch chunks are this wave's oldest loads; then every wave's
-  wait_vm(0);
-  __syncthreads();
-
-  for (int sub = 0; sub < h.nsub; ++sub) {
-    const int m0 = mbase + sub * R;
-    // row constants and residual bytes of this sub-tile: issued now, they land during the K loop
-    EpiRow row_pre{};
-    if (tid < R) {
-      const int row = min(m0 + tid, g.M - 1);
-      row_pre.ra = (uint32_t)ldg(g.RA + row);
-      row_pre.bias = ldg(g.bias + row);
-      row_pre.m = ldg(rq_axis ? g.rq.ms + row : tk_zero_words);
-      row_pre.s = ldg(rq_axis ? g.rq.ss + row : tk_zero_words);
-      row_pre.zp = ldg(g.rq.zps ? g.rq.zps + row : tk_zero_words);
-    }
-    if (has_add) {
-      if (sub > 0) lds_barrier();  // the previous sub-tile's epilogue is done reading resw
-      // the residual's 4-byte words of this sub-tile's epilogue groups, LDS-DMA'd in group order
-      // (group gi's word at resw[gi]); waited for before the epilogue
-      for (int q0 = wave * 64; q0 < total; q0 += kGemmThreads) {
-        const int gi = q0 + lane;
-        const int8_t* src = reinterpret_cast<const int8_t*>(tk_zero_words);
-        if (gi < total) {
-          const uint32_t run = fdiv40((uint32_t)gi, h.mg_runq);
-          const int f = (gi - (int)run * h.runq) * 4;
-          const uint32_t o = h.whole ? (uint32_t)(((img0 + (int)run) * Mrows + m0) * hw + f)
-                                     : (uint32_t)(((img0 * Mrows) + m0 + (int)run) * hw + oh0 * OW + f);
-          src = reinterpret_cast<const int8_t*>(g.add_res) + o;
-        }
-        __builtin_amdgcn_global_load_lds((const void*)src, (void*)(resw + q0), 4, 0, 0);
-      }
-    }
-
-    // ---- K loop: B fragments double-buffered (step s + 1's read while step s's MFMAs run); step
-    // s uses weight buffer s % D and B buffer s % 2; loads past the end re-read the last step, so
-    // the body has no branch and every wait is a counted one
-    v4i acc[MF][NFW];
-#pragma unroll
-    for (int i = 0; i < MF; ++i)
-#pragma unroll
-      for (int j = 0; j < NFW; ++j) acc[i][j] = v4i{0};
-    const int8_t* ap[MF];
-#pragma unroll
-    for (int i = 0; i < MF; ++i)
-      ap[i] = g.A + (int64_t)(m0 + 16 * (MF * wm + i) + (lane & 15)) * g.lda + 16 * (lane >> 4);
-    v4i b[2][NFW];
-#pragma unroll
-    for (int j = 0; j < NFW; ++j) b[0][j] = *reinterpret_cast<const v4i*>(hsm + boff[j]);
-    int c64 = 0, kh = 0, kw = 0;  // position of step s + 1
-    auto step = [&](auto u_c, int s) __attribute__((always_inline)) {
-      constexpr int u = decltype(u_c)::value;
-      v4i a[MF];
-#pragma unroll
-      for (int i = 0; i < MF; ++i) a[i] = abuf[u % D][i];
-      if (!TK_ABL(128)) {
-#pragma unroll
-        for (int i = 0; i < MF; ++i) abuf[u % D][i] = ldg(reinterpret_cast<const v4i*>(ap[i] + min((s + D) * kBK, last)));
-      }
-      if (++c64 == h.spt) {
-        c64 = 0;
-        if (KT == 3 && ++kw == 3) kw = 0, ++kh;
-      }
-      const int soff = (KT == 1 || kh < 3) ? (kh * h.hc + kw) * 16 + c64 * cblk : 0;
-#pragma unroll
-      for (int j = 0; j < NFW; ++j) b[(u + 1) & 1][j] = *reinterpret_cast<const v4i*>(hsm + boff[j] + soff);
-      __builtin_amdgcn_sched_barrier(0);  // the next step's reads go out before this step's MFMAs
-      if (!TK_ABL(512)) {
-#pragma unroll
-        for (int j = 0; j < NFW; ++j)
-#pragma unroll
-          for (int i = 0; i < MF; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], b[u & 1][j], acc[i][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    int s0 = 0;
-    for (; s0 + D <= h.steps; s0 += D)
-      [&]<int... U>(std::integer_sequence<int, U...>) __attribute__((always_inline)) {
-        (step(std::integral_constant<int, U>{}, s0 + U), ...);
-      }(std::make_integer_sequence<int, D>{});
-    const int rem = h.steps - s0;
-    [&]<int... U>(std::integer_sequence<int, U...>) __attribute__((always_inline)) {
-      ((rem > U ? step(std::integral_constant<int, U>{}, s0 + U) : void()), ...);
-    }(std::make_integer_sequence<int, D - 1>{});
-    if (TK_ABL(4)) continue;
-    // ---- epilogue: stage the sub-tile (the previous one's shadow pass must be done reading it);
-    // the residual words must have landed (the LDS-DMA is not tracked by the compiler's waits)
-    if (has_add) wait_vm(0);
-    // the next sub-tile's first weight steps land during this epilogue
-    if (sub + 1 < h.nsub) prefetch_a(m0 + R);
-    lds_barrier();
-    if (tid < R) {
-      EpiRow r = row_pre;
-      if (!rq_axis) r.m = g.rq.multiplier, r.s = g.rq.shift;
-      if (!g.rq.zps) r.zp = g.rq.zp_in;
-      r.fold = (uint32_t)0 - (uint32_t)g.zB * r.ra;  // zero weight zero point: the fold is -za * rowsum
-      if (r.s > -2) s_fast = 0;
-      rowc[tid] = r;
-    }
-#pragma unroll
-    for (int i = 0; i < MF; ++i)
-#pragma unroll
-      for (int j = 0; j < NFW; ++j) {
-        const int col = (jbase + j) * 16 + (lane & 15);
-        if (col < h.p && (wn == 0 || j < h.nf - h.nf0)) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) tileI[(16 * (MF * wm + i) + 4 * (lane >> 4) + r) * h.stride + col] = acc[i][j][r];
-        }
-      }
-    lds_barrier();
-
-    const uint32_t n4 = g.out_elems * 4u;
-    const auto r_conv = rec_rsrc(g.C, n4), r_bias = rec_rsrc(g.bias_out, n4);
-    const auto r_rq = rec_rsrc(g.rq_out, g.out_elems);
-    const auto r_add = rec_rsrc(g.add_out, has_add ? g.out_elems : 0u);
-    const auto r_clip = rec_rsrc(g.clip_out, g.has_clip ? g.out_elems : 0u);
-    const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
-    const int32_t clip_lo = g.clip_lo, clip_hi = g.clip_hi, add_zp = g.add_zp;
-    const bool has_clip = g.has_clip;
-    const int mode = g.rq.mode, stride = h.stride, whole = h.whole, runq = h.runq;
-    const uint64_t mg_runq = h.mg_runq, mg_hw = h.mg_hw;
-    // runs: whole-image patches: run k = image img0 + k, its channels m0 .. m0 + R x all hw pixels
-    // (contiguous); band patches: run k = channel m0 + k, its pixels oh0 * OW .. (+ pimg)
-    auto groups = [&](auto fast_c) __attribute__((always_inline)) {
-      constexpr bool FAST = decltype(fast_c)::value;
-      for (int gi = tid; gi < total; gi += kGemmThreads) {
-        const uint32_t k = fdiv40((uint32_t)gi, mg_runq);
-        const int f = (gi - (int)k * runq) * 4;
-        uint32_t o;
-        int row0, col0;
-        if (whole) {
-          o = (uint32_t)(((img0 + (int)k) * Mrows + m0) * hw + f);
-          row0 = (int)fdiv40((uint32_t)f, mg_hw);
-          col0 = (int)k * hw + (f - row0 * hw);
-        } else {
-          o = (uint32_t)(((img0 * Mrows) + m0 + (int)k) * hw + oh0 * OW + f);
-          row0 = (int)k;
-          col0 = f;
-        }
-        int slot[4];
-        EpiRow rr[4];
-        v4u v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int re = row0, ce = col0 + e;
-          if (whole) {
-#pragma unroll
-            for (int x = 0; x < 3; ++x)  // a run of 4 crosses at most 3 plane ends
-              if (ce - (int)k * hw >= hw) ce -= hw, ++re;
-          }
-          slot[e] = re * stride + ce;
-          rr[e] = rowc[re];
-          v[e] = (uint32_t)tileI[slot[e]];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += rr[e].fold;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += (uint32_t)rr[e].bias;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
-        int32_t q[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int32_t tt = (int32_t)(v[e] - (uint32_t)rr[e].zp);
-          int32_t y;
-          if constexpr (FAST) {
-            const int sh2 = -rr[e].s - 1;
-            y = (int32_t)((uint32_t)__mulhi(tt, rr[e].m) + (1u << (sh2 - 1))) >> sh2;
-          } else {
-            y = rq_core(tt, mode, rr[e].m, rr[e].s);
-          }
-          q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
-        }
-        __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
-        if (has_add) {
-          // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((resw[gi] >> (8 * e)) & 0xFFu)] - add_zp, qmin, qmax);
-          __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
-        }
-        if (has_clip) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
-          __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) tileI[slot[e]] = q[e];
-      }
-    };
-    if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) groups(std::true_type{});
-    else groups(std::false_type{});
-
-    // ---- the next conv's shadow: 16 channels of one pixel per 16-byte store
-    if (g.shadow_out) {
-      lds_barrier();
-      const int items = (R / 16) * h.p;
-      for (int it = tid; it < items; it += kGemmThreads) {
-        const int grp = it / h.p, col = it - grp * h.p;
-        const int ch0 = m0 + grp * 16;
-        const uint32_t kk = fdiv40((uint32_t)col, h.mg_pimg);
-        if ((int)kk >= nimg || ch0 >= g.shadow_cpad) continue;
-        const int pix = (img0 + (int)kk) * hw + oh0 * OW + (col - (int)kk * h.pimg);
-        uint32_t wd[4];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          uint32_t word = 0;
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const int ch = ch0 + d * 4 + qq;
-            uint32_t bb = (uint32_t)tileI[(grp * 16 + d * 4 + qq) * stride + col] ^ g.shadow_xor;
-            if (ch >= g.M) bb = 0;
-            word |= (bb & 0xFFu) << (8 * qq);
-          }
-          wd[d] = word;
-        }
-        *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)(ch0 >> 4) * g.N + pix) * 16) =
-            v4i{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------- operand preparation
 
 // pack OIHW (int8/uint8) -> [Cout_rows][k_pad], k = (kh*KW + kw)*cin_pad + c ; row sums over real taps.
@@ -1897,9 +1377,6 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(const Tx* __restrict__ x, co
 
 // ---------------------------------------------------------------- host wrappers
 
-struct ConvGeom {
-  int N, C, H, W, O, KH, KW, OH, OW, cin_pad, k_pad, k_eff, rows_pad;
-};
 
 static int conv_geom(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* a, ConvGeom* g) {
   if (data->ndim != 4 || weight->ndim != 4) return TK_ERR_SHAPE;
@@ -1933,7 +1410,8 @@ int64_t conv_packed_weight_bytes(const tk_tensor* weight, int groups) {
   int cin_pad = (C + 15) / 16 * 16;
   int64_t k_pad = ((int64_t)KH * KW * cin_pad + kBK - 1) / kBK * kBK;
   int64_t rows = (O + 127) / 128 * 128;
-  return rows * k_pad;
+  // + the chunked image of a KHxKW > 1 weight for the image-tile kernel (tk_conv_img.hip)
+  return rows * k_pad + conv_img_chunked_bytes((int)rows, cin_pad, KH * KW);
 }
 
 int conv_pack_weight(const tk_tensor* weight, int groups, void* packed, int32_t* sums, hipStream_t s) {
@@ -1946,7 +1424,7 @@ int conv_pack_weight(const tk_tensor* weight, int groups, void* packed, int32_t*
   hipLaunchKernelGGL(pack_weight_kernel, dim3(rows), dim3(256), 0, s, (const int8_t*)ptr(weight), (int8_t*)packed, sums,
                      O, C, KH, KW, cin_pad, k_pad, (int)is_uint(weight, 8));
   TK_LAUNCH_CHECK();
-  return TK_OK;
+  return conv_img_pack(weight, (int8_t*)packed + (int64_t)rows * k_pad, rows, cin_pad, s);
 }
 
 int64_t conv_shadow_bytes(const tk_tensor* data) {
@@ -1972,14 +1450,6 @@ static inline uint32_t rep4(int v) {
   return b | (b << 8) | (b << 16) | (b << 24);
 }
 
-// Block outputs (NULL `b` = plain conv/dense writing only the int32 contraction).
-struct BlockIO {
-  const tk_tensor* bias;
-  tk_tensor* const* outs;  // conv, bias_add, requantize, [clip]
-  int n_outs;
-  const tk_block_attrs* attrs;
-  void* shadow_out;
-};
 
 // Validates a fused block and fills the epilogue part of GemmArgs.
 static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out, int channels, int ch_axis) {
@@ -2072,11 +1542,6 @@ static int setup_block(GemmArgs& ga, const BlockIO* b, const tk_tensor* conv_out
 // only: they are read from the environment in the ablation build (build.py --ablation,
 // -DTK_ABLATION_BUILD, loaded by the tools through TK_LIB_PATH).  The product library
 // compiles them to their defaults, so no variable on a box changes what it runs.
-#ifdef TK_ABLATION_BUILD
-static const char* tune_env(const char* name) { return getenv(name); }
-#else
-static const char* tune_env(const char*) { return nullptr; }
-#endif
 
 static int xcd_order(int64_t out_hw) {
   const char* e = tune_env("TK_XCD");
@@ -2088,10 +1553,6 @@ static int nt_stores() {
   return e ? atoi(e) : 1;
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* e = tune_env(name);
-  return e ? atoi(e) : dflt;
-}
 
 static int ring_depth() {
   const char* e = tune_env("TK_RING");
@@ -2195,122 +1656,6 @@ static bool conv_wide(const ConvGeom& g, bool block, int ipt) {
 // round: the 14x14 3x3 256-channel layers, -5.5 % (profiles/r02z_wide_mt2_ab.txt)
 static bool wide_mt2(const ConvGeom& g, int64_t tiles) {
   return g.KH * g.KW <= 64 && g.cin_pad % 128 == 0 && g.k_pad / kBK >= 8 && tiles <= 256 && env_int("TK_WIDE_MT2", 1);
-}
-
-// Patch-tile blocks (conv_patch_kernel): 1x1 (pad 0) and 3x3 (pad 1) convs, stride 1 or 2, with
-// 64-channel input steps, 32-channel output multiples, no kernel zero point.  Candidate patches:
-// whole images (ipt of them, <= 224 pixels) or bands of th output rows (th | OH).  For each, the
-// channel range of a workgroup is split so that >= 256 workgroups run and each walks several
-// sub-tiles where it can (their stores drain under the next sub-tile's K loop); the largest patch
-// that reaches 256 workgroups wins (else the one with the most).
-struct PatchPlan {
-  PatchArgs a;
-  size_t lds;
-  int mf, nfw, kt;
-};
-
-static bool patch_plan(const ConvGeom& g, const tk_conv2d_attrs* a, const BlockIO* blk, bool patch, PatchPlan* out) {
-  // off by default: on ResNet-50's layers it measured slower than the im2col kernel at one
-  // workgroup per CU (profiles/r02g_patch_ab.txt); TK_PATCH=1 in the ablation build for A/Bs
-  if (!blk || patch || !env_int("TK_PATCH", 0)) return false;
-  const int st = a->strides[0];
-  if (a->strides[1] != st || (st != 1 && st != 2) || a->dilation[0] != 1 || a->dilation[1] != 1) return false;
-  int kt;
-  if (g.KH == 3 && g.KW == 3 && a->padding[0] == 1 && a->padding[1] == 1 && a->padding[2] == 1 && a->padding[3] == 1)
-    kt = 3;
-  else if (g.KH == 1 && g.KW == 1 && !a->padding[0] && !a->padding[1] && !a->padding[2] && !a->padding[3])
-    kt = 1;
-  else
-    return false;
-  if (kt == 3 && !env_int("TK_PATCH3", 1)) return false;
-  if (kt == 1 && !env_int("TK_PATCH1", 1)) return false;
-  const int64_t hw = (int64_t)g.OH * g.OW;
-  if (g.cin_pad % 64 || g.O % 32 || (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll) return false;
-  const int cgroups = g.cin_pad / 16;
-  const int R = g.O % 64 == 0 ? 64 : 32;
-  const int msub = g.O / R;
-  const bool add = blk->attrs->has_add;
-  auto magic = [](uint64_t d) -> uint64_t { return ((1ull << 40) + d - 1) / d; };
-  struct Cand {
-    int ipt, th;
-  };
-  Cand cands[96];
-  int nc = 0;
-  for (int ipt = (int)std::min<int64_t>(224 / std::max<int64_t>(hw, 1), g.N); ipt >= 1 && nc < 32; --ipt)
-    cands[nc++] = {ipt, g.OH};
-  if (hw % 4 == 0)
-    for (int th = g.OH - 1; th >= 1 && nc < 96; --th)
-      if (g.OH % th == 0 && th * g.OW <= 224 && (th * g.OW) % 4 == 0) cands[nc++] = {1, th};
-  int pick = -1, pick_chunks = 1;
-  int64_t best = -1;
-  for (int c = 0; c < nc; ++c) {
-    const int ipt = cands[c].ipt, th = cands[c].th;
-    const int hr = kt == 3 ? (th - 1) * st + 3 : th, hc = kt == 3 ? (g.OW - 1) * st + 3 : g.OW;
-    const int plane = (ipt * hr * hc + 15) / 16 * 16;
-    const int64_t chunks = ((int64_t)cgroups * plane + 63) / 64 * 64;
-    const int p = ipt * th * g.OW;
-    const int stride = (p + 31) / 32 * 32 + 4;
-    const size_t bytes = (size_t)chunks * 16 + (size_t)R * stride * 4 + R * sizeof(EpiRow) + 2048 + (size_t)R * p + 256;
-    if (p > 224 || bytes > 160 * 1024 - 256) continue;
-    const int64_t spatial = ((g.N + ipt - 1) / ipt) * (int64_t)(g.OH / th);
-    // channel ranges per patch: the fewest that reach 256 workgroups (at most one per sub-tile)
-    int mchunks = msub;
-    for (int d = 1; d <= msub; ++d)
-      if (msub % d == 0 && spatial * d >= 256) {
-        mchunks = d;
-        break;
-      }
-    const int64_t wgs = spatial * mchunks;
-    if (wgs >= 256) {
-      pick = c, pick_chunks = mchunks;
-      break;
-    }
-    if (wgs > best) best = wgs, pick = c, pick_chunks = mchunks;
-  }
-  if (pick < 0) return false;
-  const int ipt = cands[pick].ipt, th = cands[pick].th;
-  PatchArgs& x = out->a;
-  x = PatchArgs{};
-  x.nimg = g.N;
-  x.ipt = ipt;
-  x.th = th;
-  x.bands = g.OH / th;
-  x.hr = kt == 3 ? (th - 1) * st + 3 : th;
-  x.hc = kt == 3 ? (g.OW - 1) * st + 3 : g.OW;
-  x.plane = (ipt * x.hr * x.hc + 15) / 16 * 16;
-  x.ih0s = kt == 3 ? -a->padding[0] : 0;
-  x.rs = kt == 3 ? 1 : st;
-  x.cs = kt == 3 ? 1 : st;
-  x.ps = kt == 3 ? st : 1;
-  x.pimg = th * g.OW;
-  x.p = ipt * x.pimg;
-  x.nf = (x.p + 15) / 16;
-  x.nf0 = (x.nf + 1) / 2;
-  x.stride = (x.p + 31) / 32 * 32 + 4;
-  x.mchunks = pick_chunks;
-  x.nsub = msub / pick_chunks;
-  x.wgs = (int32_t)(((g.N + ipt - 1) / ipt) * (int64_t)x.bands * pick_chunks);
-  x.wgs8 = (x.wgs + 7) / 8 * 8;
-  x.steps = g.k_pad / kBK;
-  x.spt = g.cin_pad / kBK;
-  x.chunks = (int32_t)(((int64_t)cgroups * x.plane + 63) / 64 * 64);
-  x.mg_plane = magic(x.plane);
-  x.mg_img = magic((uint64_t)x.hr * x.hc);
-  x.mg_hc = magic(x.hc);
-  x.mg_pimg = magic(x.pimg);
-  x.mg_ow = magic(g.OW);
-  x.mg_hw = magic(hw);
-  x.whole = th == g.OH;
-  x.runq = x.whole ? (int32_t)(R * hw / 4) : x.pimg / 4;
-  x.mg_runq = magic(x.runq);
-  x.stage_off = x.chunks * 16;
-  x.rowc_off = x.stage_off + R * x.stride * 4;
-  x.lut_off = x.rowc_off + R * (int)sizeof(EpiRow);
-  out->lds = (size_t)x.lut_off + (add ? 2048 + (size_t)R * x.p + 256 : 0);  // LUTs + residual words
-  out->mf = R / 32;
-  out->nfw = x.nf0 <= 2 ? 2 : x.nf0 <= 4 ? 4 : 7;
-  out->kt = kt;
-  return true;
 }
 
 static SplitPlan conv_split_plan(const ConvGeom& g, bool mt1, int ipt, int sbk = kBK) {
@@ -2493,33 +1838,13 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     ga.RB = ps;
     ga.zA_vec = a->kernel_zero_points;
   }
-  {
-    PatchPlan pp;
-    if (patch_plan(g, a, blk, conv_needs_patch(weight, a), &pp)) {
-      using KFn = void (*)(GemmArgs, PatchArgs);
-      static const KFn kernels[2][3][2] = {
-          {{conv_patch_kernel<1, 2, 1>, conv_patch_kernel<1, 2, 3>},
-           {conv_patch_kernel<1, 4, 1>, conv_patch_kernel<1, 4, 3>},
-           {conv_patch_kernel<1, 7, 1>, conv_patch_kernel<1, 7, 3>}},
-          {{conv_patch_kernel<2, 2, 1>, conv_patch_kernel<2, 2, 3>},
-           {conv_patch_kernel<2, 4, 1>, conv_patch_kernel<2, 4, 3>},
-           {conv_patch_kernel<2, 7, 1>, conv_patch_kernel<2, 7, 3>}}};
-      const KFn kern = kernels[pp.mf - 1][pp.nfw == 2 ? 0 : pp.nfw == 4 ? 1 : 2][pp.kt == 3];
-      if (pp.lds > 64 * 1024) {
-        // dynamic LDS beyond 64 KiB must be allowed per kernel (the static s_fast word counts too)
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pp.lds);
-        if (e != hipSuccess) {
-          (void)hipGetLastError();
-          set_error(std::string("conv patch kernel: LDS attribute failed: ") + hipGetErrorString(e));
-          return TK_ERR_HIP;
-        }
-      }
-      ga.mtiles = g.O / 32;
-      hipLaunchKernelGGL(kern, dim3((unsigned)pp.a.wgs8), dim3(kGemmThreads), pp.lds, s, ga, pp.a);
-      TK_LAUNCH_CHECK();
-      return TK_OK;
-    }
+  if (blk) {
+    // whole-image tiles with the patch staged per channel stage (tk_conv_img.hip) where they apply
+    const int8_t* chunked = conv_img_chunked_bytes(g.rows_pad, g.cin_pad, g.KH * g.KW)
+                                ? (const int8_t*)packed + (int64_t)g.rows_pad * g.k_pad
+                                : nullptr;
+    int irc = TK_OK;
+    if (conv_img_try(g, a, ga, chunked, s, &irc)) return irc;
   }
   const bool mt1 = conv_mt1(g, blk != nullptr);
   const int ipt = mt1 ? conv_image_tiles(g, blk != nullptr, conv_needs_patch(weight, a)) : 0;

@@ -94,8 +94,43 @@ __global__ __launch_bounds__(kEwBlock) void ewise_kernel(const T* __restrict__ x
     y[i] = ew_apply<T, OP>(x[i], rt ? rt[i] : rs, a);
 }
 
+// rhs_kind 3: a per-channel vector along axis 1 (element i takes rhs[(i / inner) % C]), e.g. the
+// scale of a batch norm that FoldScaleAxis could not fold into a conv
+template <typename T, int OP>
+__global__ __launch_bounds__(kEwBlock) void ewise_axis_kernel(const T* __restrict__ x, const T* __restrict__ rt,
+                                                              T* __restrict__ y, int64_t n, int64_t inner, int64_t C,
+                                                              tk_ewise_attrs a) {
+  const int64_t stride = (int64_t)gridDim.x * kEwBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kEwBlock + threadIdx.x; i < n; i += stride)
+    y[i] = ew_apply<T, OP>(x[i], rt[(i / inner) % C], a);
+}
+
+template <typename T>
+static int launch_ewise_axis(const tk_tensor* x, const tk_tensor* r, tk_tensor* y, const tk_ewise_attrs* a,
+                             hipStream_t s) {
+  const int64_t n = numel(x), C = x->shape[1], inner = n / (x->shape[0] * C);
+  const dim3 grid(ew_grid(n)), block(kEwBlock);
+  const T* rt = (const T*)ptr(r);
+  switch (a->op) {
+    case TK_EW_ADD:
+      hipLaunchKernelGGL((ewise_axis_kernel<T, TK_EW_ADD>), grid, block, 0, s, (const T*)ptr(x), rt, (T*)ptr(y), n,
+                         inner, C, *a);
+      break;
+    case TK_EW_MULTIPLY:
+      hipLaunchKernelGGL((ewise_axis_kernel<T, TK_EW_MULTIPLY>), grid, block, 0, s, (const T*)ptr(x), rt, (T*)ptr(y),
+                         n, inner, C, *a);
+      break;
+    default:
+      set_error("tk_ewise: a per-channel rhs (rhs_kind 3) takes add or multiply");
+      return TK_ERR_INVALID_ARG;
+  }
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
 template <typename T>
 static int launch_ewise(const tk_tensor* x, const tk_tensor* r, tk_tensor* y, const tk_ewise_attrs* a, hipStream_t s) {
+  if (a->rhs_kind == 3) return launch_ewise_axis<T>(x, r, y, a, s);
   const int64_t n = numel(x);
   const T* rt = a->rhs_kind == 2 ? (const T*)ptr(r) : nullptr;
   T rs;
@@ -153,8 +188,12 @@ int ewise_impl(const tk_tensor* x, const tk_tensor* r, tk_tensor* y, const tk_ew
   TK_CHECK_ARG(x->dtype.code == y->dtype.code && x->dtype.bits == y->dtype.bits, "dtype mismatch");
   if (a->rhs_kind == 2) {
     TK_CHECK_ARG(r && compact(r) && numel(r) == numel(x) && r->dtype.bits == x->dtype.bits, "rhs must match the lhs");
+  } else if (a->rhs_kind == 3) {
+    TK_CHECK_ARG(x->ndim >= 2 && x->shape[0] > 0 && x->shape[1] > 0 && r && compact(r) && numel(r) == x->shape[1] &&
+                     r->dtype.code == x->dtype.code && r->dtype.bits == x->dtype.bits,
+                 "rhs_kind 3: rhs must hold one value per channel (axis 1) of the lhs");
   } else {
-    TK_CHECK_ARG(a->rhs_kind == 0 || a->rhs_kind == 1, "rhs_kind must be 0, 1 or 2");
+    TK_CHECK_ARG(a->rhs_kind == 0 || a->rhs_kind == 1, "rhs_kind must be 0, 1, 2 or 3");
   }
   if (is_f32(x)) return launch_ewise<float>(x, r, y, a, s);
   if (is_int(x, 32)) return launch_ewise<int32_t>(x, r, y, a, s);

@@ -28,6 +28,7 @@ int max_pool_shadow_impl(const tk_tensor* x, const void* x_shadow, tk_tensor* y,
 int avg_pool_impl(const tk_tensor* x, tk_tensor* y, const tk_pool2d_attrs* a, hipStream_t s);
 int global_avg_pool_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
 int copy_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s);
+int pad_impl(const tk_tensor* x, tk_tensor* y, const tk_pad_attrs* a, hipStream_t s);
 int postops_impl(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* y, const tk_postops_attrs* a,
                  hipStream_t s);
 int digest_impl(const void* data, int64_t nbytes, uint64_t* out, hipStream_t s);
@@ -132,6 +133,8 @@ static int run_node(Node& n, hipStream_t s) {
       return conv2d_f32_impl(i0, i1, o, &d.attrs.conv2d, s);
     case TK_NODE_DENSE_F32:
       return dense_f32_impl(i0, i1, o, s);
+    case TK_NODE_PAD:
+      return pad_impl(i0, o, &d.attrs.pad, s);
   }
   set_error("tk_module: unknown node kind " + std::to_string(d.kind));
   return TK_ERR_INVALID_ARG;
@@ -246,6 +249,9 @@ int tk_global_avg_pool2d(const tk_tensor* data, tk_tensor* out, void* stream) {
 }
 int tk_copy(const tk_tensor* data, tk_tensor* out, void* stream) {
   return tk::copy_impl(data, out, tk::as_stream(stream));
+}
+int tk_pad(const tk_tensor* data, tk_tensor* out, const tk_pad_attrs* attrs, void* stream) {
+  return tk::pad_impl(data, out, attrs, tk::as_stream(stream));
 }
 int tk_tachikoma_postops(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* out,
                          const tk_postops_attrs* attrs, void* stream) {

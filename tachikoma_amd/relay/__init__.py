@@ -9,6 +9,7 @@ from . import op as _op
 from .parser import ParseError, astext, fromtext, parse  # noqa: F401  (tvm.parser.parse / fromtext)
 from . import contrib  # noqa: F401,E402  (relay.op.contrib.tachikoma analogue: contrib.tachikoma)
 from . import quantize  # noqa: F401,E402  (relay.quantize: float32 graph -> integer graph)
+from . import transform  # noqa: F401,E402  (relay.transform: SimplifyInference, FoldScaleAxis, FoldConstant)
 
 
 class _NN:
@@ -20,6 +21,8 @@ class _NN:
     batch_flatten = staticmethod(_op.batch_flatten)
     conv2d = staticmethod(_op.conv2d)
     dense = staticmethod(_op.dense)
+    batch_norm = staticmethod(_op.batch_norm)
+    pad = staticmethod(_op.pad)
 
 
 nn = _NN()

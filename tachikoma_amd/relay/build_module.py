@@ -300,8 +300,14 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
             ins = _tensor_args(call, 2, names)
             a.update(axis=1, relay_op="add")
             op = "nn.bias_add"
+        elif op == "multiply" and nd >= 2 and padded is not None and padded[1] == lhs.shape[1] and \
+                all(d == 1 for i, d in enumerate(padded) if i != 1):
+            # a per-channel multiplier (e.g. a batch norm's scale FoldScaleAxis left in place)
+            ins = _tensor_args(call, 2, names)
+            a.update(ew=op, rhs_kind=3, relay_op=op)
+            op = "ewise"
         else:
-            raise UnsupportedError(f"{op}: {lhs.shape} with {rs}: scalar, same-shape or (add) per-channel "
+            raise UnsupportedError(f"{op}: {lhs.shape} with {rs}: scalar, same-shape or per-channel "
                                    "operands only")
         if op == "ewise" and call.dtype not in ("float32", "int8", "int32", "int64"):
             raise UnsupportedError(f"{call.op} on {call.dtype}")
@@ -350,6 +356,11 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
         ins = _tensor_args(call, 1, names)
         a["lo"] = 0
         a["hi"] = int(np.iinfo(np.dtype(call.dtype)).max)
+    elif op == "nn.pad":
+        ins = _tensor_args(call, 1, names)
+        if call.dtype not in INT_DTYPES + ("float32",) or len(call.shape) > 6:
+            raise UnsupportedError(f"nn.pad on {call.dtype} / {len(call.shape)}-D")
+        a["value"] = call.args[1].data.item()
     elif op in ("cast", "nn.max_pool2d", "nn.avg_pool2d", "nn.global_avg_pool2d", "nn.batch_flatten", "reshape",
                 "annotation.stop_fusion", "annotation.cast_hint"):
         ins = _tensor_args(call, 1, names)
@@ -524,9 +535,32 @@ def build(mod, target: str = "mi355x", params=None, mod_name: str = "default", f
         params = load_param_dict(bytes(params))
     params = {k: np.ascontiguousarray(np.asarray(v.numpy() if hasattr(v, "numpy") else v))
               for k, v in (params or {}).items()}
+    mod = _simplify_batch_norms(mod, params)
     mod, params = lift_constants(mod, params)
     plan = lower(mod, params)
     return ExecutorFactory(plan, params, t, mod_name, fuse=fuse)
+
+
+def _simplify_batch_norms(mod, params: Dict[str, np.ndarray]):
+    """The reference's pass prefix runs SimplifyInference + FoldConstant on every build
+    (src/relay/backend/utils.cc:239-258): a graph with ``nn.batch_norm`` layers gets their
+    inference form (per-channel multiply + add, relay/transform.py), the scale / shift folded to
+    constants (the four statistics bound from ``params`` when they are parameters)."""
+    func = mod["main"] if isinstance(mod, IRModule) else IRModule.from_expr(mod)["main"]
+    bns = [n for n in post_order(func.body) if isinstance(n, Call) and n.op == "nn.batch_norm"]
+    if not bns:
+        return mod
+    from .fold import fold_constant, rebuild
+    from .transform import simplify_inference
+    stats = {id(v) for n in bns for v in n.args[1:] if isinstance(v, Var) and v.name_hint in params}
+
+    def bind(call: Call, args):
+        args = [Constant(params[a.name_hint]) if id(a) in stats else a for a in args]
+        return Call(call.op, args, call.attrs, call.checked_type)
+
+    body = rebuild(func.body, bind)
+    keep = [p for p in func.params if id(p) not in stats]
+    return fold_constant(simplify_inference(IRModule(Function(keep, body))))
 
 
 def lift_constants(mod, params: Dict[str, np.ndarray]):

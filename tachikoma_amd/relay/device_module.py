@@ -259,6 +259,15 @@ class DeviceModule:
                     n.kind = _lib.NODE_KINDS[kind]
                 elif kind in ("nn.batch_flatten", "reshape", "annotation.stop_fusion", "annotation.cast_hint"):
                     n.kind = _lib.NODE_KINDS["copy"]
+                elif kind == "nn.pad":
+                    n.kind = _lib.NODE_KINDS["nn.pad"]
+                    pa = n.attrs.pad
+                    for d, (b_, a_) in enumerate(a["pad_width"]):
+                        pa.before[d], pa.after[d] = b_, a_
+                    if op.out.dtype == "float32":
+                        pa.value_f = float(a["value"])
+                    else:
+                        pa.value_i = int(a["value"])
                 elif kind == "ewise":
                     n.kind = _lib.NODE_KINDS["ewise"]
                     ew = n.attrs.ewise

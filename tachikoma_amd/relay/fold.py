@@ -50,7 +50,7 @@ def _clip(x: np.ndarray, lo: float, hi: float) -> np.ndarray:
 
 def _binary(op: str, a: np.ndarray, b: np.ndarray, dtype: str) -> np.ndarray:
     if np.dtype(dtype).kind == "f":
-        r = {"add": np.add, "multiply": np.multiply, "subtract": np.subtract}[op](a, b)
+        r = {"add": np.add, "multiply": np.multiply, "subtract": np.subtract, "divide": np.divide}[op](a, b)
         return r.astype(dtype)
     a64, b64 = a.astype(np.int64), b.astype(np.int64)
     if op == "add":
@@ -70,8 +70,12 @@ def _binary(op: str, a: np.ndarray, b: np.ndarray, dtype: str) -> np.ndarray:
 
 def eval_const_call(call: Call, args) -> np.ndarray:
     op, a = call.op, call.attrs
-    if op in ("add", "multiply", "subtract", "left_shift", "right_shift"):
+    if op in ("add", "multiply", "subtract", "left_shift", "right_shift") or (op == "divide" and call.dtype == "float32"):
         return _binary(op, args[0], args[1], call.dtype)
+    if op == "sqrt" and call.dtype == "float32":  # llvm.sqrt.f32: correctly rounded, as np.sqrt
+        return np.sqrt(args[0]).astype(np.float32)
+    if op == "negative":
+        return (-args[0]).astype(args[0].dtype) if call.dtype == "float32" else _int_wrap(-args[0].astype(np.int64), call.dtype)
     if op == "round":
         return round_away(args[0])
     if op == "clip":

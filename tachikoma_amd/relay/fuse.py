@@ -45,7 +45,7 @@ _PATTERNS = {
     "round": kElemWise, "fixed_point_multiply": kElemWise,
     "nn.bias_add": kBroadcast, "qnn.add": kBroadcast, "add": kBroadcast, "multiply": kBroadcast,
     "left_shift": kBroadcast, "right_shift": kBroadcast,
-    "nn.batch_flatten": kInjective, "reshape": kInjective,
+    "nn.batch_flatten": kInjective, "reshape": kInjective, "nn.pad": kInjective,
     "annotation.stop_fusion": kOpaque, "annotation.cast_hint": kOpaque,
     "tachikoma.qnn.conv2d": kOpaque, "tachikoma.qnn.dense": kOpaque,  # external (BYOC) functions
 }

@@ -199,8 +199,10 @@ def batch_flatten(data: Expr) -> Call:
 
 
 def reshape(data: Expr, newshape) -> Call:
+    """``relay.reshape`` with Relay's special values 0 (copy the input dimension) and -1 (infer)
+    (src/relay/op/tensor/transform.cc InferNewShape)."""
     total = int(np.prod(data.shape))
-    shape = list(int(s) for s in newshape)
+    shape = [int(data.shape[i]) if int(s) == 0 else int(s) for i, s in enumerate(newshape)]
     if -1 in shape:
         k = shape.index(-1)
         rest = int(np.prod([s for i, s in enumerate(shape) if i != k]))
@@ -208,3 +210,62 @@ def reshape(data: Expr, newshape) -> Call:
     if int(np.prod(shape)) != total:
         raise TypeError(f"reshape: {data.shape} -> {newshape}")
     return Call("reshape", [data], {"newshape": tuple(shape)}, TensorType(tuple(shape), data.dtype))
+
+
+def pad(data: Expr, pad_width, pad_value=0.0, pad_mode: str = "constant") -> Call:
+    """``relay.nn.pad`` (src/relay/op/nn/pad.cc, topi/nn/pad.py), constant mode: ``pad_width`` is
+    one (before, after) pair per axis; the pad value (a scalar, or a scalar constant expression as
+    the text form writes it: ``nn.pad(%x, 0f, pad_width=...)``) is cast to the data's dtype."""
+    if pad_mode != "constant":
+        raise NotImplementedError("nn.pad: only pad_mode='constant' is supported")
+    pw = tuple((int(b), int(a)) for b, a in pad_width)
+    if len(pw) != len(data.shape) or any(b < 0 or a < 0 for b, a in pw):
+        raise TypeError(f"nn.pad: pad_width {pad_width} for a {len(data.shape)}-D tensor")
+    if isinstance(pad_value, Constant):
+        if pad_value.data.ndim != 0:
+            raise TypeError("nn.pad: the pad value must be a scalar")
+        v = pad_value.data.item()
+    elif isinstance(pad_value, Expr):
+        raise TypeError("nn.pad: the pad value must be a constant")
+    else:
+        v = pad_value
+    pv = const(np.asarray(v).astype(data.dtype), data.dtype)
+    shape = tuple(int(d) + b + a for d, (b, a) in zip(data.shape, pw))
+    return Call("nn.pad", [data, pv], {"pad_width": pw, "pad_mode": "constant"}, TensorType(shape, data.dtype))
+
+
+class TupleGetItem(Expr):
+    """A field of a multi-output op (``%0.0``).  Only ``nn.batch_norm``'s normalised output (field
+    0) exists on this path: the op's node IS that output, so field 0 resolves to it."""
+
+
+class BatchNormOutputs:
+    """What ``relay.nn.batch_norm`` returns (the reference's TupleWrapper of (out, moving_mean,
+    moving_var)); inference graphs use field 0 only."""
+
+    def __init__(self, call: Call):
+        self.call = call
+
+    def __getitem__(self, i: int) -> Call:
+        if i != 0:
+            raise NotImplementedError("nn.batch_norm: only the normalised output (field 0) is supported")
+        return self.call
+
+    def astuple(self) -> Call:
+        return self.call
+
+
+def batch_norm(data: Expr, gamma: Expr, beta: Expr, moving_mean: Expr, moving_var: Expr, axis: int = 1,
+               epsilon: float = 1e-5, center: bool = True, scale: bool = True) -> BatchNormOutputs:
+    """``relay.nn.batch_norm`` (src/relay/op/nn/nn.cc BatchNormRel): float data, four per-channel
+    vectors along ``axis``.  Graphs holding it are rewritten by ``transform.simplify_inference``
+    (``relay.build`` and ``relay.quantize`` run it first, as the reference's pass prefix and
+    prerequisite_optimize do)."""
+    ax = axis if axis >= 0 else len(data.shape) + axis
+    c = data.shape[ax]
+    for name, v in (("gamma", gamma), ("beta", beta), ("moving_mean", moving_mean), ("moving_var", moving_var)):
+        if tuple(v.shape) != (c,) or v.dtype != data.dtype:
+            raise TypeError(f"nn.batch_norm: {name} {v.shape} {v.dtype} vs {c} channels of {data.dtype}")
+    attrs = {"axis": int(axis), "epsilon": float(epsilon), "center": bool(center), "scale": bool(scale)}
+    return BatchNormOutputs(Call("nn.batch_norm", [data, gamma, beta, moving_mean, moving_var], attrs,
+                                 data.checked_type))

@@ -20,7 +20,9 @@ Accepted text is what ``mod.astext()`` prints for integer QNN graphs::
 * ``/* ... */`` (type annotations) and ``// ...`` comments are skipped.
 
 Ops map onto this package's constructors (``relay.qnn.op.*``, ``relay.nn.*``), which take the
-reference's attribute names; anything else raises ``ParseError``.
+reference's attribute names; anything else raises ``ParseError``.  Float models as the reference's
+own tests write them (``nn.batch_norm`` with its ``%k.0`` field projection, ``nn.pad`` with the
+pad value as an argument, ``reshape`` with 0 / -1) parse too: tests/golden/menangerie_*.relay.
 """
 from __future__ import annotations
 
@@ -185,6 +187,12 @@ def _call(op: str, args: List[Expr], attrs: Dict[str, Any]) -> Expr:
             return _op.batch_flatten(*args)
         if op == "reshape":
             return _op.reshape(*args, **a)
+        # float models as the reference's own tests write them (tests/python/relay/collage/
+        # menangerie.py): batch norm layers and explicit padding
+        if op == "nn.batch_norm":
+            return _op.batch_norm(*args, **a)
+        if op == "nn.pad":
+            return _op.pad(args[0], a.pop("pad_width"), *args[1:], **a)
         # float32 graphs and relay.quantize-realized graphs
         if op == "nn.conv2d":
             return _op.conv2d(*args, **a)
@@ -330,9 +338,23 @@ class _Parser:
         t = self.peek()
         if t[0] == "local":
             self.next()
-            if t[1] not in self.scope:
-                raise ParseError(f"unbound variable {t[1]}")
-            return self.scope[t[1]]
+            name = t[1]
+            if name not in self.scope:
+                # a tuple field (TupleGetItem, ``%0.0``)
+                base, dot, idx = name.rpartition(".")
+                if dot and idx.isdigit() and base in self.scope:
+                    tup = self.scope[base]
+                    if not isinstance(tup, _op.BatchNormOutputs):
+                        raise ParseError(f"{name}: {base} is not a tuple")
+                    try:
+                        return tup[int(idx)]
+                    except NotImplementedError as e:
+                        raise ParseError(f"{name}: {e}") from e
+                raise ParseError(f"unbound variable {name}")
+            v = self.scope[name]
+            if isinstance(v, _op.BatchNormOutputs):
+                raise ParseError(f"{name} is a tuple (nn.batch_norm): use a field, e.g. {name}.0")
+            return v
         if t[0] == "number":
             self.next()
             v = _number(t[1])
@@ -435,6 +457,10 @@ def astext(mod: IRModule, show_meta_data: bool = True) -> str:
         names[id(node)] = f"%{counter}"
         lines.append(f"  %{counter} = {node.op}({', '.join(args + attrs)}) /* ty={ty} */;")
         counter += 1
+        if node.op == "nn.batch_norm":  # a tuple: consumers read its field 0 (a TupleGetItem line)
+            lines.append(f"  %{counter} = %{counter - 1}.0 /* ty={ty} */;")
+            names[id(node)] = f"%{counter}"
+            counter += 1
     params = ", ".join(f"%{p.name_hint}: Tensor[({', '.join(map(str, p.shape))}{',' if len(p.shape) == 1 else ''}), "
                        f"{p.dtype}]" for p in fn.params)
     body_ref = ref(fn.body)

@@ -114,17 +114,16 @@ def _sconst(v, dtype) -> Constant:
 # ----------------------------------------------------------------------------- prerequisites
 
 def prerequisite_optimize(mod, params=None) -> IRModule:
-    """Bind params as constants, canonicalize ``nn.bias_add`` to ``add`` with an expanded
-    bias (CanonicalizeOps), FoldConstant (quantize.py:298-322).  Batch norm must already be
-    folded into the weights (SimplifyInference/FoldScaleAxis are not run here)."""
+    """quantize.py:312-322: bind params as constants, then SimplifyInference -> FoldConstant ->
+    FoldScaleAxis (relay/transform.py: batch norms become a per-channel multiply folded into the
+    producing conv / dense weights, plus a constant add) -> CanonicalizeOps (``nn.bias_add`` to
+    ``add`` with an expanded bias) -> FoldConstant."""
+    from ..transform import fold_scale_axis, simplify_inference
     func = mod["main"] if isinstance(mod, IRModule) else IRModule.from_expr(mod)["main"]
     params = {k: np.asarray(v.numpy() if hasattr(v, "numpy") else v) for k, v in (params or {}).items()}
     bound = {id(v): Constant(params[v.name_hint]) for v in func.params if v.name_hint in params}
 
     def canon(call: Call, args):
-        args = [bound.get(id(a), a) for a in args]
-        if call.op == "nn.batch_norm":
-            raise UnsupportedError("quantize: fold nn.batch_norm into the weights first")
         if call.op == "nn.bias_add":
             x, b = args
             ax = call.attrs["axis"] if call.attrs["axis"] >= 0 else len(x.shape) + call.attrs["axis"]
@@ -135,8 +134,18 @@ def prerequisite_optimize(mod, params=None) -> IRModule:
             return call
         return _forward(call, args)
 
-    body = rebuild(func.body, canon)
+    def bind(call: Call, args):
+        args = [bound.get(id(a), a) for a in args]
+        if all(x is y for x, y in zip(args, call.args)):
+            return call
+        return Call(call.op, args, call.attrs, call.checked_type)
+
+    body = rebuild(func.body, bind)
     body = bound.get(id(body), body)
+    m = IRModule(Function(_params_of(body, func.params), body))
+    m = fold_scale_axis(fold_constant(simplify_inference(m)))
+    func = m["main"]
+    body = rebuild(func.body, canon)
     return fold_constant(IRModule(Function(_params_of(body, func.params), body)))
 
 
@@ -447,9 +456,19 @@ def find_scale_by_percentile(arr: np.ndarray, percentile: float = 0.99999) -> fl
 
 
 def find_scale_by_kl(arr: np.ndarray, quantized_dtype: str = "int8", num_bins: int = 8001,
-                     num_quantized_bins: int = 255) -> float:
+                     num_quantized_bins: int = 255, edges_as: str = "reference") -> float:
     """kl_divergence.py:_find_scale_by_kl: a symmetric histogram of the values, then the native
-    MinimizeKL (tk_find_scale_by_kl, csrc/tk_calibrate.cc)."""
+    MinimizeKL (tk_find_scale_by_kl, csrc/tk_calibrate.cc).
+
+    The reference hands np.histogram's edge array to MinimizeKL through a ``c_float*`` cast of its
+    buffer (kl_divergence.py:46-51), whatever numpy built: for float32 statistics (every profile
+    graph output of a float32 model) those are float32 edges and the cast is exact; for float64
+    statistics the C side reads the first num_bins + 1 float32 words of the float64 buffer.
+    ``edges_as="reference"`` (default) passes exactly those bytes, so the threshold equals the
+    reference's for any input dtype; ``edges_as="values"`` converts the edge values to float32
+    instead (a meaningful threshold for float64 statistics, where the reference's is not)."""
+    if edges_as not in ("reference", "values"):
+        raise ValueError(f"find_scale_by_kl: edges_as must be 'reference' or 'values', not {edges_as!r}")
     import ctypes
     from ... import _lib
     arr = np.asarray(arr)
@@ -459,13 +478,22 @@ def find_scale_by_kl(arr: np.ndarray, quantized_dtype: str = "int8", num_bins: i
         num_quantized_bins = num_quantized_bins * 2 + 1
     hist, edges = np.histogram(arr, bins=num_bins, range=(-thres, thres))
     hist = np.ascontiguousarray(hist, np.int32)
-    edges = np.ascontiguousarray(edges, np.float32)
+    edges = kl_edge_buffer(edges, num_bins) if edges_as == "reference" else np.ascontiguousarray(edges, np.float32)
     out = ctypes.c_float()
     _lib.check(_lib.load().tk_find_scale_by_kl(hist.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                                                edges.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                                                num_bins, num_quantized_bins, ctypes.byref(out)),
                "tk_find_scale_by_kl")
     return float(out.value)
+
+
+def kl_edge_buffer(edges: np.ndarray, num_bins: int) -> np.ndarray:
+    """The num_bins + 1 float32 words MinimizeKL reads from np.histogram's edge array after the
+    reference's ``ctypes.cast(edges.ctypes.data_as(POINTER(c_float)), c_void_p)``
+    (kl_divergence.py:42-48; calibrate.cc:214-218 copies ``hist_edges_ptr[0 .. num_bins]``): the
+    array's own bytes reinterpreted, not its values converted."""
+    raw = np.ascontiguousarray(edges).view(np.uint8)
+    return np.frombuffer(raw.tobytes()[:4 * (num_bins + 1)], np.float32).copy()
 
 
 def _dataset_scales(mod, dataset, finder) -> List[float]:

@@ -68,3 +68,30 @@ def test_parsed_realized_graph_trace(device, tmp_path):
         if name not in exp:
             records.pop(name)
     _compare(records, exp)
+
+
+@pytest.mark.parametrize("name", ["mnist", "mobilenet", "resnet50"])
+def test_reference_relay_text_quantized_trace(device, tmp_path, name):
+    """The reference's own float models as Relay text (tests/python/relay/collage/menangerie.py,
+    extracted to tests/golden/menangerie_*.relay; batch norms, explicit padding), parsed,
+    quantized (SimplifyInference / FoldScaleAxis folding the batch norms first), built and traced
+    on the MI355X: every record bit-exact against the oracle run of the same quantized graph."""
+    from tachikoma_amd.relay.quantize import quantize
+    from .golden_util import menangerie
+    mod, iname, shape = menangerie(name)
+    q = quantize(mod, {})
+    x = np.random.default_rng(7).standard_normal(shape).astype(np.float32)
+    lib = relay.build(q, target="mi355x")
+    m = graph_executor.GraphModule(lib["default"]())
+    m.set_input(iname, x)
+    path = str(tmp_path / f"{name}.tkt")
+    m.dump_trace(path)
+    records = read_trace(path).records
+    exp = graph_ref.calibrate(q, {}, {iname: x})
+    assert set(exp) <= set(records)
+    for k, v in exp.items():
+        got = records[k]
+        assert got.shape == v.shape and got.dtype == v.dtype, k
+        if not np.array_equal(got, v):
+            idx = tuple(np.argwhere(got != v)[0])
+            raise AssertionError(f"{name} record {k}: first mismatch at {idx}: {got[idx]} vs {v[idx]}")

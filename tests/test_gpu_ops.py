@@ -263,9 +263,9 @@ BLOCK_CASES = [
 ]
 
 
-# stride-1 3x3 blocks with 64-channel multiples take the halo-tile kernel (conv3x3_halo_kernel):
-# whole-image tiles (several images per tile on small planes, last tile partial) and row-band
-# tiles (28x28: 7-row bands, 56x56: 4-row bands), both 4-column fragment counts
+# stride-1 3x3 blocks of ResNet stage shapes: whole-image tiles of the image-tile kernel on planes of
+# up to 256 pixels (several images per workgroup, the last one partial), the im2col kernel's tiles
+# on the 28x28 / 56x56 / 20x20 planes
 HALO_CASES = [
     # N, C, H, O, dx, za, out_dtype, clip
     (3, 64, 28, 128, "int8", -3, "int8", (0, 127)),
@@ -299,9 +299,8 @@ def test_conv3x3_halo_block(tk, case):
     np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
 
 
-# 1x1 / 3x3 blocks of every ResNet stage shape on the patch kernel: strided 1x1 (downsample) and
-# strided 3x3, residual joins on whole-image and row-band patches, several sub-tiles per
-# workgroup (the 1x1 expand layers), 32-row sub-tiles (96 channels), uint8
+# 1x1 / 3x3 blocks of every ResNet stage shape: strided 1x1 (downsample) and strided 3x3,
+# residual joins, expand layers (1x1 to 4x the channels), 32-channel output multiples (96), uint8
 PATCH_CASES = [
     # N, C, H, O, K, stride, dx, za, residual add params or None, clip
     (3, 256, 28, 512, 1, 2, "int8", -2, None, None),
@@ -345,6 +344,86 @@ def test_conv_patch_block(tk, case):
     for got, e in zip(outs, exp):
         np.testing.assert_array_equal(got, e)
     np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
+
+
+# image-tile kernel (tk_conv_img.hip): 1x1 (128-channel stages) and 3x3 (32-channel stages, chunked
+# weights) blocks on planes of up to 256 pixels, R = 64 / 32 output channels x whole images per
+# workgroup; several images per workgroup with the last one ragged, planes whose pixel count is
+# not a multiple of 4 (groups crossing channel rows), strided 3x3 (halo of a strided patch) and
+# strided 1x1 (strided patch loader), residual joins on either side, uint8, no clip
+IMG_CASES = [
+    # N, C, H, O, K, stride, dtype, za, residual add params or None, clip, block_is_rhs
+    (5, 256, 14, 256, 3, 1, "int8", -3, None, (0, 127), False),
+    (3, 512, 7, 512, 3, 1, "int8", 2, None, (0, 127), False),
+    (7, 64, 7, 96, 3, 1, "uint8", 130, None, (128, 255), False),
+    (3, 96, 9, 64, 3, 1, "int8", 1, (0.05, -3, 0.06, 4, 0.08, -1), (-1, 127), False),
+    (4, 128, 16, 128, 3, 1, "int8", 0, None, None, False),
+    (3, 256, 14, 128, 3, 2, "int8", 4, None, (0, 127), False),
+    (2, 128, 28, 64, 3, 2, "uint8", 129, None, None, False),
+    (2, 128, 12, 64, 3, 1, "int8", 2, (0.05, 3, 0.07, -2, 0.09, 1), (1, 127), True),
+    (6, 1024, 14, 256, 1, 1, "int8", 2, None, (0, 127), False),
+    (5, 256, 14, 1024, 1, 1, "int8", -1, (0.04, 0, 0.04, 0, 0.04, 0), (0, 127), False),
+    (3, 512, 7, 2048, 1, 1, "uint8", 130, (0.1, 130, 0.2, 120, 0.15, 128), (128, 255), True),
+    (4, 512, 28, 1024, 1, 2, "int8", 3, None, None, False),
+    (3, 2048, 7, 512, 1, 1, "int8", -2, None, (0, 127), False),
+    (9, 128, 5, 64, 1, 1, "int8", 5, (0.05, -3, 0.06, 4, 0.08, -1), None, False),
+]
+
+
+@pytest.mark.parametrize("case", IMG_CASES, ids=[f"img{i}" for i in range(len(IMG_CASES))])
+def test_conv_img_block(tk, case):
+    """Every record (and the shadow of the last one) of a block on the image-tile kernel against
+    the unfused oracle ops."""
+    n, c, h, o, k, st, dt, za, ap, clip, rhs = case
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
+    x = _rand(rng, (n, c, h, h), dt)
+    wt = _rand(rng, (o, c, k, k), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_in = rng.uniform(1e-5, 1e-3, size=o).astype(np.float32)
+    s_out = np.float32(0.01)
+    p = k // 2
+    pad = (p, p, p, p)
+    oh = (h + 2 * p - k) // st + 1
+    kw = dict(clip=clip, strides=(st, st), padding=pad, out_dtype=dt, want_shadow=True)
+    residual = None
+    if ap is not None:
+        residual = _rand(rng, (n, o, oh, oh), dt)
+        kw.update(residual=residual, add_params=ap, block_is_rhs=rhs)
+    outs = tk.conv2d_block(x, wt, bias, za, 0, s_in, s_out, 3, **kw)
+    conv = ref.qnn_conv2d(x, wt, za, 0, strides=(st, st), padding=pad)
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(3), axis=1, out_dtype=dt)
+    exp = [conv, badd, rq]
+    if ap is not None:
+        exp.append(ref.qnn_add(residual, rq, *ap) if rhs else ref.qnn_add(rq, residual, *ap))
+    if clip is not None:
+        exp.append(ref.clip(exp[-1], *clip))
+    for got, e in zip(outs, exp):
+        np.testing.assert_array_equal(got, e)
+    np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
+
+
+@pytest.mark.parametrize("k", [1, 3])
+@pytest.mark.parametrize("rounding", ["UPWARD", "TONEAREST"])
+def test_conv_img_shift_regimes(tk, rounding, k):
+    """The image-tile kernel's general requantize path (per-channel right shifts 0..8 and left
+    shifts) and TONEAREST, against the oracle."""
+    rng = np.random.default_rng(79 + k)
+    n, c, h, o = 3, 128, 14, 64
+    x = _rand(rng, (n, c, h, h), "int8")
+    wt = _rand(rng, (o, c, k, k), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_out = np.float32(0.5)
+    s_in = (np.geomspace(2.0 ** -8, 3.5, o) * s_out).astype(np.float32)
+    pad = (k // 2,) * 4
+    outs = tk.conv2d_block(x, wt, bias, 3, 0, s_in, s_out, -4, clip=(-128, 127), padding=pad, rounding=rounding,
+                           want_shadow=True)
+    conv = ref.qnn_conv2d(x, wt, 3, 0, padding=pad)
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(-4), axis=1, out_dtype="int8", rounding=rounding)
+    for got, e in zip(outs, [conv, badd, rq, rq]):
+        np.testing.assert_array_equal(got, e)
+    np.testing.assert_array_equal(outs[-1], blocked_shadow(rq))
 
 
 @pytest.mark.parametrize("rounding", ["UPWARD", "TONEAREST"])
@@ -527,3 +606,25 @@ def test_conv_block_matches_unfused_ops(tk, case):
         np.testing.assert_array_equal(got, e)
     # the shadow of the last output (what the next MFMA conv reads)
     np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
+
+
+@pytest.mark.parametrize("dt,value", [("int8", -5), ("uint8", 200), ("int32", -70000), ("float32", 1.5)])
+def test_pad(tk, dt, value):
+    """tk_pad (nn.pad, constant mode) against the oracle's np.pad restatement."""
+    from tachikoma_amd import _lib
+    rng = np.random.default_rng(31)
+    x = _rand(rng, (2, 3, 5, 7), dt) if dt != "float32" else rng.standard_normal((2, 3, 5, 7)).astype(np.float32)
+    pw = ((0, 1), (1, 2), (3, 0), (2, 2))
+    exp = ref.pad(x, pw, np.asarray(value).astype(dt))
+    out = tk.empty(exp.shape, dt)
+    a = _lib.tk_pad_attrs()
+    for d, (b, e) in enumerate(pw):
+        a.before[d], a.after[d] = b, e
+    if dt == "float32":
+        a.value_f = value
+    else:
+        a.value_i = int(np.asarray(value).astype(dt).astype(np.int64))
+    xd = tk.dev(x)
+    rc = _lib.load().tk_pad(tk.ref(xd).ptr, tk.ref(out).ptr, a, tk.stream())
+    tk._sync_check(rc, "tk_pad")
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)

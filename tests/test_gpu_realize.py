@@ -43,11 +43,11 @@ def test_realized_resnet_trace_bit_exact(device, tmp_path, depth, cfg):
     _compare(tr.records, exp)
 
 
-def _ew(x, op, rhs=None, scalar=None, **kw):
+def _ew(x, op, rhs=None, scalar=None, per_channel=False, **kw):
     out = G.empty(x.shape, str(x.dtype))
     a = _lib.tk_ewise_attrs()
     a.op = _lib.TK_EW[op]
-    a.rhs_kind = 2 if rhs is not None else (1 if scalar is not None else 0)
+    a.rhs_kind = (3 if per_channel else 2) if rhs is not None else (1 if scalar is not None else 0)
     if scalar is not None:
         if x.dtype == np.float32:
             a.scalar_f = float(scalar)
@@ -154,3 +154,19 @@ def test_conv2d_f32_bit_exact(device, shape):
                   "tk_conv2d_f32")
     exp = realize_ref.conv2d_f32(x, wt, (s, s), (p, p, p, p), (1, 1), groups)
     assert np.array_equal(out.cpu().numpy(), exp)
+
+
+def test_ewise_per_channel_operand(device):
+    """tk_ewise rhs_kind 3: one value per channel (axis 1) -- a batch norm's scale left unfolded
+    by FoldScaleAxis -- for float32 multiply / add and the int32 wrap-around forms."""
+    rng = np.random.default_rng(12)
+    f = rng.standard_normal((2, 5, 7, 3)).astype(np.float32)
+    s = rng.standard_normal(5).astype(np.float32)
+    for op in ("multiply", "add"):
+        exp = realize_ref.binary(op, f, s.reshape(5, 1, 1), "float32")
+        assert np.array_equal(_ew(f, op, rhs=s, per_channel=True), exp), op
+    i = rng.integers(-2**31, 2**31, (3, 4, 5, 5)).astype(np.int32)
+    v = rng.integers(-2**31, 2**31, 4).astype(np.int32)
+    for op in ("multiply", "add"):
+        exp = realize_ref.binary(op, i, v.reshape(4, 1, 1), "int32")
+        assert np.array_equal(_ew(i, op, rhs=v, per_channel=True), exp), op

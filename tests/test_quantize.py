@@ -304,3 +304,34 @@ def test_kl_histogram_edges_are_float32():
     thres = max(abs(np.min(arr)), abs(np.max(arr)))
     _, edges = np.histogram(arr, bins=8001, range=(-thres, thres))
     assert edges.dtype == np.float32
+
+
+def test_kl_edges_reference_byte_buffer():
+    """find_scale_by_kl hands MinimizeKL the bytes the reference's c_float* cast of np.histogram's
+    edges would (kl_divergence.py:46-51): identical to the values for float32 statistics, the
+    first num_bins + 1 float32 words of the float64 buffer for float64 statistics; edges_as="values"
+    converts the float64 edges instead."""
+    import ctypes
+    from tachikoma_amd import _lib
+    from tachikoma_amd.relay.quantize.passes import find_scale_by_kl, kl_edge_buffer
+    rng = np.random.default_rng(9)
+    nb, nq = 201, 21
+    for dt in (np.float32, np.float64):
+        arr = (rng.standard_normal(20000) * 2.5).astype(dt)
+        thres = max(abs(np.min(arr)), abs(np.max(arr)))
+        hist, edges = np.histogram(arr, bins=nb, range=(-thres, thres))
+        assert edges.dtype == dt
+        buf = kl_edge_buffer(edges, nb)
+        # the reference's buffer, built the way its ctypes cast builds it
+        cbuf = ctypes.cast(edges.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.POINTER(ctypes.c_float))
+        assert np.array_equal(buf.view(np.uint32), np.array([cbuf[i] for i in range(nb + 1)], np.float32).view(np.uint32))
+        if dt == np.float32:
+            assert np.array_equal(buf, edges)
+        exp = np.float32(realize_ref.minimize_kl(hist, buf, nb, nq))
+        assert np.float32(find_scale_by_kl(arr, num_bins=nb, num_quantized_bins=nq)) == exp
+        got_v = np.float32(find_scale_by_kl(arr, num_bins=nb, num_quantized_bins=nq, edges_as="values"))
+        assert got_v == np.float32(realize_ref.minimize_kl(hist, edges.astype(np.float32), nb, nq))
+        if dt == np.float32:
+            assert got_v == exp
+    with pytest.raises(ValueError):
+        find_scale_by_kl(np.ones(10, np.float32), edges_as="bogus")
