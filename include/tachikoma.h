@@ -310,13 +310,15 @@ enum {
 typedef struct {
   int32_t op;                   /* TK_EW_* */
   int32_t rhs_kind;             /* 0: unary, 1: scalar (scalar_f / scalar_i), 2: tensor of x's shape,
-                                   3: one value per channel (axis 1) of x, add / multiply only */
+                                   3: one value per channel (axis 1) of x, add / multiply; for an int32
+                                   fixed_point_multiply: int32[2C], the multipliers then the shifts
+                                   (fixed_point_multiply_per_axis, no power-of-two special case) */
   double scalar_f;              /* float32 tensors */
   int64_t scalar_i;             /* integer tensors */
   double lo, hi;                /* TK_EW_CLIP */
   int32_t multiplier, shift;    /* TK_EW_FIXED_POINT_MULTIPLY */
 } tk_ewise_attrs;
-/* Elementwise op of a float32 / int8 / int32 / int64 tensor (topi broadcast ops with a scalar or
+/* Elementwise op of a float32 / int8 / int16 / int32 / int64 tensor (topi broadcast ops with a scalar or
  * same-shape rhs; relay.round; relay.fixed_point_multiply, topi/math.py:644-673). */
 int tk_ewise(const tk_tensor* x, const tk_tensor* rhs, tk_tensor* out, const tk_ewise_attrs* attrs, void* stream);
 /* float32 nn.conv2d NCHW/OIHW (the conv the quantizer skips, skip_conv_layers) and nn.dense. */

@@ -24,6 +24,12 @@ Granularity (``create(..., granularity=)``):
     ``tvmgen_default_fused_qnn_conv2d_nn_bias_add_qnn_requantize_clip_3``); its output is the
     value of the group's last op, and params appear as ``null`` nodes before their first
     consumer, as the graph codegen emits bound constants;
+  * ``"canonical"``: the fused functions of the graph the reference's executor actually runs --
+    QNN legalized / canonicalized to int16 shifts, int16 contractions and the integer requantize
+    chain, simplified (relay/canonical.py) -- so node names are the reference's own
+    (``tvmgen_default_fused_nn_conv2d_add_fixed_point_multiply_per_axis_add_clip_cast``) and
+    node values are the canonical tensors: plan records where one holds the value, the rest
+    (int16 operand shifts, int32 partial sums) computed on the device (canonical_values.py);
   * ``"op"``: one graph node per Relay op (MRT names ``%N``), finer than the reference.
 Device time of a node is the time of the device kernels that write its records (a device
 block's time goes to the node holding its first op).
@@ -85,8 +91,11 @@ def executor_graph_json(plan, granularity: str = "op", mod_name: str = "default"
             null(t)
         for op in plan.ops:
             call(op.name, "tachikoma_" + op.op.replace(".", "_"), op.inputs, op.out)
-    elif granularity == "fused":
+    elif granularity in ("fused", "canonical"):
         from ...relay.fuse import fused_nodes
+        if granularity == "canonical":
+            from ...relay.canonical import canonicalize
+            plan = canonicalize(plan)
         params = {t.name: t for t in plan.params}
         for t in plan.inputs:
             null(t)
@@ -96,7 +105,7 @@ def executor_graph_json(plan, granularity: str = "op", mod_name: str = "default"
                     null(params[x])
             call(fn.node_name, fn.func_name, fn.inputs, fn.ops[-1].out)
     else:
-        raise ValueError(f"granularity must be 'fused' or 'op', not {granularity!r}")
+        raise ValueError(f"granularity must be 'fused', 'canonical' or 'op', not {granularity!r}")
     return {
         "nodes": nodes,
         "arg_nodes": arg_nodes,
@@ -136,6 +145,11 @@ class GraphModuleDebug(GraphModule):
         self._dump_path = os.path.join(self._dump_root, folder)
         os.makedirs(self._dump_path, 0o700, exist_ok=True)
         self.granularity = granularity
+        self.mod_name = mod_name
+        self.canon = None
+        if granularity == "canonical":
+            from ...relay.canonical import canonicalize
+            self.canon = canonicalize(self.plan)
         graph = executor_graph_json(self.plan, granularity, mod_name)
         self._node_outputs: List[str] = graph.pop("outputs")
         self._graph = graph
@@ -156,9 +170,17 @@ class GraphModuleDebug(GraphModule):
         if self.granularity == "fused":
             from ...relay.fuse import fused_nodes
             op_nodes = [i for i, n in enumerate(self._nodes) if n["op"] != "param"]
-            for gi, fn in zip(op_nodes, fused_nodes(self.plan)):
+            for gi, fn in zip(op_nodes, fused_nodes(self.plan, self.mod_name)):
                 for op in fn.ops:
                     node_of[op.name] = gi
+        elif self.granularity == "canonical":
+            # a device node's time goes to the fused function holding the first canonical op
+            # lowered from its first record's plan op
+            from ...relay.fuse import fused_nodes
+            op_nodes = [i for i, n in enumerate(self._nodes) if n["op"] != "param"]
+            for gi, fn in zip(op_nodes, fused_nodes(self.canon, self.mod_name)):
+                for op in fn.ops:
+                    node_of.setdefault(op.origin, gi)
         else:
             for i, n in enumerate(self._nodes):
                 node_of[n["name"]] = i
@@ -171,7 +193,13 @@ class GraphModuleDebug(GraphModule):
                 if key.startswith("<"):
                     carry += ms  # shadow nodes carry no op: charged to the consumer
                     continue
-                acc[node_of[key.split("+")[0]]] += (ms + carry) * 1e-3
+                # the first of its records that has a graph node (a canonical graph can simplify
+                # a plan op away entirely, e.g. a cast back to the clip's own type)
+                gi = next((node_of[r] for r in key.split("+") if r in node_of), None)
+                if gi is None:
+                    carry += ms
+                    continue
+                acc[gi] += (ms + carry) * 1e-3
                 carry = 0.0
             for i, t in enumerate(acc):
                 per_node[i].append(t)
@@ -182,8 +210,14 @@ class GraphModuleDebug(GraphModule):
         if inputs:
             self.set_input(**inputs)
         self._times_s = self._node_times(repeat)
-        self._outputs = {i: self.module.buffers[name].detach().cpu().numpy()
-                         for i, name in enumerate(self._node_outputs)}
+        if self.canon is not None:
+            from .canonical_values import CanonicalValues
+            vals = CanonicalValues(self.module, self.canon)
+            dev = [vals.value(name) for name in self._node_outputs]
+            self._outputs = {i: t.detach().cpu().numpy() for i, t in enumerate(dev)}
+        else:
+            self._outputs = {i: self.module.buffers[name].detach().cpu().numpy()
+                             for i, name in enumerate(self._node_outputs)}
         self.dump_output_tensor()
         self.dump_chrome_trace()
         self.display_debug_result(sort_by_time)
@@ -194,7 +228,8 @@ class GraphModuleDebug(GraphModule):
                 for i, n in enumerate(self._nodes)}
 
     def node_outputs(self) -> List[str]:
-        """Plan tensor holding each graph node's value (a fused node: its group's last op)."""
+        """Plan tensor holding each graph node's value (a fused node: its group's last op; with
+        granularity "canonical", the canonical tensor)."""
         return list(self._node_outputs)
 
     def dump_output_tensor(self) -> None:

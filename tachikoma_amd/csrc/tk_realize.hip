@@ -32,6 +32,7 @@ static inline int ew_grid(int64_t items) {
 // One kernel per (type, op): x op rhs with rhs a scalar or a same-shape tensor.
 template <typename T> struct Wide { using U = T; };
 template <> struct Wide<int8_t> { using U = uint8_t; };
+template <> struct Wide<int16_t> { using U = uint16_t; };
 template <> struct Wide<int32_t> { using U = uint32_t; };
 template <> struct Wide<int64_t> { using U = uint64_t; };
 
@@ -105,12 +106,40 @@ __global__ __launch_bounds__(kEwBlock) void ewise_axis_kernel(const T* __restric
     y[i] = ew_apply<T, OP>(x[i], rt[(i / inner) % C], a);
 }
 
+// fixed_point_multiply_per_axis (topi/math.py fixed_point_multiply_per_axis, the per-channel
+// requantize of FixedPointMultiplyPerChannel, src/relay/qnn/utils.cc:111-135): element i of
+// channel c = (i / inner) % C takes multiplier rhs[c] and shift rhs[C + c], always in
+// q_multiply_shift's general int64 form (intrin_rule.cc:166-195, :252-267: no power-of-two case)
+__global__ __launch_bounds__(kEwBlock) void fpm_axis_kernel(const int32_t* __restrict__ x,
+                                                            const int32_t* __restrict__ ms,
+                                                            int32_t* __restrict__ y, int64_t n, int64_t inner,
+                                                            int64_t C) {
+  const int64_t stride = (int64_t)gridDim.x * kEwBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kEwBlock + threadIdx.x; i < n; i += stride) {
+    const int64_t c = (i / inner) % C;
+    const int32_t m = ms[c], sh = ms[C + c];
+    const int ls = sh > 0 ? sh : 0, rs = sh > 0 ? 0 : -sh;
+    uint64_t v = (uint64_t)(int64_t)x[i] << ls;
+    v *= (uint64_t)(int64_t)m;
+    const int total = 31 + rs;
+    v += 1ull << (total - 1);
+    y[i] = (int32_t)((int64_t)v >> total);
+  }
+}
+
 template <typename T>
 static int launch_ewise_axis(const tk_tensor* x, const tk_tensor* r, tk_tensor* y, const tk_ewise_attrs* a,
                              hipStream_t s) {
   const int64_t n = numel(x), C = x->shape[1], inner = n / (x->shape[0] * C);
   const dim3 grid(ew_grid(n)), block(kEwBlock);
   const T* rt = (const T*)ptr(r);
+  if constexpr (std::is_same<T, int32_t>::value) {
+    if (a->op == TK_EW_FIXED_POINT_MULTIPLY) {
+      hipLaunchKernelGGL(fpm_axis_kernel, grid, block, 0, s, (const int32_t*)ptr(x), rt, (int32_t*)ptr(y), n, inner, C);
+      TK_LAUNCH_CHECK();
+      return TK_OK;
+    }
+  }
   switch (a->op) {
     case TK_EW_ADD:
       hipLaunchKernelGGL((ewise_axis_kernel<T, TK_EW_ADD>), grid, block, 0, s, (const T*)ptr(x), rt, (T*)ptr(y), n,
@@ -121,7 +150,7 @@ static int launch_ewise_axis(const tk_tensor* x, const tk_tensor* r, tk_tensor* 
                          n, inner, C, *a);
       break;
     default:
-      set_error("tk_ewise: a per-channel rhs (rhs_kind 3) takes add or multiply");
+      set_error("tk_ewise: a per-channel rhs (rhs_kind 3) takes add, multiply or (int32) fixed_point_multiply");
       return TK_ERR_INVALID_ARG;
   }
   TK_LAUNCH_CHECK();
@@ -189,9 +218,12 @@ int ewise_impl(const tk_tensor* x, const tk_tensor* r, tk_tensor* y, const tk_ew
   if (a->rhs_kind == 2) {
     TK_CHECK_ARG(r && compact(r) && numel(r) == numel(x) && r->dtype.bits == x->dtype.bits, "rhs must match the lhs");
   } else if (a->rhs_kind == 3) {
-    TK_CHECK_ARG(x->ndim >= 2 && x->shape[0] > 0 && x->shape[1] > 0 && r && compact(r) && numel(r) == x->shape[1] &&
-                     r->dtype.code == x->dtype.code && r->dtype.bits == x->dtype.bits,
-                 "rhs_kind 3: rhs must hold one value per channel (axis 1) of the lhs");
+    // fixed_point_multiply: multipliers then shifts, two int32 per channel
+    const int64_t per = a->op == TK_EW_FIXED_POINT_MULTIPLY ? 2 : 1;
+    TK_CHECK_ARG(x->ndim >= 2 && x->shape[0] > 0 && x->shape[1] > 0 && r && compact(r) &&
+                     numel(r) == per * x->shape[1] && r->dtype.code == x->dtype.code && r->dtype.bits == x->dtype.bits,
+                 "rhs_kind 3: rhs must hold one value per channel (axis 1) of the lhs (fixed_point_multiply: "
+                 "the multipliers, then the shifts)");
   } else {
     TK_CHECK_ARG(a->rhs_kind == 0 || a->rhs_kind == 1, "rhs_kind must be 0, 1, 2 or 3");
   }
@@ -199,7 +231,8 @@ int ewise_impl(const tk_tensor* x, const tk_tensor* r, tk_tensor* y, const tk_ew
   if (is_int(x, 32)) return launch_ewise<int32_t>(x, r, y, a, s);
   if (is_int(x, 64)) return launch_ewise<int64_t>(x, r, y, a, s);
   if (is_int(x, 8)) return launch_ewise<int8_t>(x, r, y, a, s);
-  set_error("tk_ewise: float32, int8, int32 or int64 tensors only");
+  if (is_int(x, 16)) return launch_ewise<int16_t>(x, r, y, a, s);
+  set_error("tk_ewise: float32, int8, int16, int32 or int64 tensors only");
   return TK_ERR_DTYPE;
 }
 

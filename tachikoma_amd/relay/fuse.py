@@ -44,7 +44,8 @@ _PATTERNS = {
     "qnn.requantize": kElemWise, "clip": kElemWise, "cast": kElemWise, "nn.relu": kElemWise,
     "round": kElemWise, "fixed_point_multiply": kElemWise,
     "nn.bias_add": kBroadcast, "qnn.add": kBroadcast, "add": kBroadcast, "multiply": kBroadcast,
-    "left_shift": kBroadcast, "right_shift": kBroadcast,
+    "left_shift": kBroadcast, "right_shift": kBroadcast, "subtract": kBroadcast,
+    "fixed_point_multiply_per_axis": kBroadcast,  # transform.cc:4421-4432
     "nn.batch_flatten": kInjective, "reshape": kInjective, "nn.pad": kInjective,
     "annotation.stop_fusion": kOpaque, "annotation.cast_hint": kOpaque,
     "tachikoma.qnn.conv2d": kOpaque, "tachikoma.qnn.dense": kOpaque,  # external (BYOC) functions

@@ -138,3 +138,58 @@ def test_debug_dump_matches_oracle(device, tmp_path):
     assert lines[-1].startswith("Total_time")
     mod.exit()
     assert not os.path.exists(directory)
+
+
+def test_canonical_graph_json_layout():
+    """granularity="canonical": the fused functions of the canonicalized graph, with the
+    reference's names (cast_subtract operand shifts, nn_conv2d_add_fixed_point_multiply_* blocks)."""
+    from tachikoma_amd.relay.canonical import canonicalize
+    from tachikoma_amd.relay.fuse import fused_nodes
+    m = zoo.resnet18(batch=1)
+    plan = lower(m.mod, m.params)
+    g = executor_graph_json(plan, "canonical")
+    outputs = g.pop("outputs")
+    ops = [n for n in g["nodes"] if n["op"] == "tvm_op"]
+    fns = fused_nodes(canonicalize(plan))
+    assert [n["name"] for n in ops] == [f.node_name for f in fns]
+    names = {n["attrs"]["func_name"] for n in ops}
+    assert any(f.startswith("tvmgen_default_fused_cast_subtract") for f in names)
+    assert any(f.startswith("tvmgen_default_fused_nn_conv2d_add_fixed_point_multiply_per_axis") for f in names)
+    assert not any("qnn_" in f for f in names)
+    for i, n in enumerate(g["nodes"]):
+        assert all(src[0] < i for src in n["inputs"])
+    assert len(outputs) == len(g["nodes"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,batch", [("resnet18", 2), ("mobilenet_v2", 1)])
+def test_canonical_debug_dump_matches_oracle(device, tmp_path, name, batch):
+    """Every canonical fused node's dumped tensor -- plan records and the device-computed
+    intermediates (int16 operand shifts, int32 partial requantize / add results) -- equals the
+    CPU evaluation of the canonical ops (oracle/canonical_ref.py)."""
+    import tachikoma_amd
+    from oracle import canonical_ref
+    from tachikoma_amd import relay, trace_format as tf
+    from tachikoma_amd.contrib.debugger import debug_executor
+
+    model = zoo.MODELS[name](batch=batch)
+    x = model.random_input()
+    lib = relay.build(model.mod, target="mi355x", params=model.params)
+    mod = debug_executor.create(lib, tachikoma_amd.rocm(0), dump_root=str(tmp_path / "dbg"), granularity="canonical")
+    mod.set_input("data", x)
+    mod.run()
+    with open(os.path.join(mod.dump_path, "output_tensors.params"), "rb") as f:
+        tensors = tf.parse_ndarray_list(f.read(), copy=True)
+    exp = canonical_ref.evaluate(mod.canon, {"data": x, **{k: np.asarray(v) for k, v in model.params.items()}})
+    pattern = re.compile(r"^(.+)____topo-index:(\d+)____output-num:0$")
+    outs = mod.node_outputs()
+    computed = 0
+    ops = {o.name: o for o in mod.canon.ops}
+    for i, (key, arr) in enumerate(tensors.items()):
+        mt = pattern.match(key)
+        assert mt and int(mt.group(2)) == i
+        np.testing.assert_array_equal(arr, exp[outs[i]], err_msg=key)
+        computed += outs[i] in ops and ops[outs[i]].record is None
+    assert computed > 0  # the int16 shifts at least were evaluated on the device
+    assert mod.get_debug_result().split("\n")[-1].startswith("Total_time")
+    mod.exit()

@@ -16,14 +16,26 @@ def main(path, model="resnet50", batch=64):
     plan = lower(m.mod, m.params)
     groups = exec_groups(plan)
     blocks = [g for g in groups if g.kind in ("conv_block", "dense_block")]
-    g_rows = [r for r in rows if r["Kernel_Name"].startswith("gemm_i8_kernel") or
-              r["Kernel_Name"].startswith("direct_conv_kernel")]
+    fams = ("gemm_i8_kernel", "direct_conv_kernel", "conv_img_kernel")
+    g_rows = [r for r in rows if any(f in r["Kernel_Name"] for f in fams)]
+    # idle time before each launch: end of the previous kernel (any) to this start
+    prev_end = {}
+    last = None
+    for r in rows:
+        if last is not None:
+            prev_end[id(r)] = int(last["End_Timestamp"])
+        last = r
+    gap = defaultdict(list)
+    kname = {}
     n = len(blocks)
     dur = defaultdict(list)
     for i, r in enumerate(g_rows[-(len(g_rows) // n) * n:]):
         dur[i % n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    print(f"{'layer':34s} {'us':>8s} {'GB/s':>8s} {'TOPS':>7s}  VGPR/AGPR")
-    tot = 0
+        if id(r) in prev_end:
+            gap[i % n].append((int(r["Start_Timestamp"]) - prev_end[id(r)]) / 1e3)
+        kname[i % n] = r["Kernel_Name"].split("(")[0].replace("void tk::", "")
+    print(f"{'layer':34s} {'us':>8s} {'GB/s':>8s} {'TOPS':>7s} {'gap us':>7s}  kernel")
+    tot = tgap = 0
     for i, g in enumerate(blocks):
         head = g.ops[0]
         w = plan.tensor(head.inputs[1]).shape
@@ -38,9 +50,11 @@ def main(path, model="resnet50", batch=64):
             desc = f"dense {w[1]}->{w[0]}"
         b = x.nbytes + int(w[0] * w[1] * w[2] * w[3] if len(w) == 4 else w[0] * w[1]) + outb
         d = sorted(dur[i])[len(dur[i]) // 2]
+        gp = sorted(gap[i])[len(gap[i]) // 2] if gap[i] else 0.0
         tot += d
-        print(f"{desc:34s} {d:8.1f} {b / d / 1e3:8.0f} {2 * macs / d / 1e6:7.1f}")
-    print("total us", round(tot, 1))
+        tgap += gp
+        print(f"{desc:34s} {d:8.1f} {b / d / 1e3:8.0f} {2 * macs / d / 1e6:7.1f} {gp:7.1f}  {kname.get(i, '')}")
+    print("total us", round(tot, 1), "idle before block launches us", round(tgap, 1))
 
 
 if __name__ == "__main__":
