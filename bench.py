@@ -59,6 +59,7 @@ def parse(argv=None):
                         "to trace.rank<r>.tkt, overlapped with the next step (two pinned images, writer thread)")
     p.add_argument("--out-dir", default="/tmp")
     p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
+    p.add_argument("--tune-report", default=None, help="write the find step's per-node kernel timings (JSON) here")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse N>1 on one GPU")
     p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
@@ -296,6 +297,11 @@ def main(argv=None) -> int:
          f"(numa node {placement['numa_node']}, {placement['cpus']} cpus)")
     lib = relay.build(model.mod, target="mi355x", params=model.params)
     m = graph_executor.GraphModule(lib["default"](device.index))
+    # the module's find step (tk_module_tune) picked each conv block's kernel on this GPU
+    tuning = m.module.tuning
+    if args.tune_report and rank == 0:
+        with open(args.tune_report, "w") as f:
+            json.dump(tuning, f, indent=1)
     # weak scaling: B samples per GPU; this rank traces samples [offset, offset + B) of the global batch
     offset, count = shard.shard_range(B * world, world, rank)
     x = model.sample_inputs(offset, count)
@@ -610,6 +616,10 @@ def main(argv=None) -> int:
                 "compute_only_traces_per_s": round(B * world / (compute_ms * 1e-3), 1),
                 "compute_step_device_ms": round(total_ms, 3),
                 "block_segments": len(blk_segs),
+                "find_step": {"tuned_nodes": len(tuning),
+                              "image_tile_nodes": sum(1 for t in tuning if t["algo"] >= 16),
+                              "im2col_nodes": sum(1 for t in tuning if t["algo"] == 1),
+                              "best_us_sum": round(sum(t["us"] for t in tuning), 1)},
                 "trace_bytes_per_step": trace_bytes,
                 "trace_GBps_per_gpu": round(trace_bytes / (elapsed_max / args.steps) / 1e9, 2),
                 "macs_per_sample": macs_per_sample,

@@ -164,7 +164,18 @@ typedef struct {
   int32_t block_is_rhs;         /* 1: the requantize output is qnn.add's rhs operand */
   const tk_tensor* residual;    /* the other qnn.add operand (same shape and dtype, NCHW) */
   tk_qnn_add_attrs add;
+  int32_t algo;                 /* MFMA conv blocks: the kernel (tk_conv2d_block_algos): 0 = the
+                                   library's choice, 1 = im2col tiles, 16 + i = image-tile plan i.
+                                   Every algo gives bit-identical records; only time differs. */
 } tk_block_attrs;
+
+/* The kernels an MFMA conv block can run on, as tk_block_attrs.algo values: 1 (im2col tiles,
+ * always) then 16 + i for each image-tile plan that applies, in the planner's estimated-time
+ * order.  Writes at most max_algos entries; returns how many exist (0: not an MFMA conv, the
+ * block has a single kernel) or a negative tk_status.  The reference has one CPU kernel per op
+ * (its TOPI schedules are chosen at compile time); this is the MI355X find step's search space. */
+int tk_conv2d_block_algos(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
+                          int32_t* algos, int max_algos);
 
 /* A fused residual join: qnn.add [→ clip].  One kernel writes both records and,
  * optionally, the int8 shadow (tk_conv2d_make_shadow layout) of the last output for the next MFMA conv. */
@@ -415,6 +426,14 @@ int tk_module_run_profiled(tk_module* mod, void* stream, float* node_ms);
  * event after every node on the compute stream; tk_module_node_times reads the last run. */
 int tk_module_set_profiling(tk_module* mod, int enable);
 int tk_module_node_times(tk_module* mod, float* node_ms);
+/* Find step (MIOpen-style, replacing the reference's compile-time schedule choice): for every
+ * MFMA conv-block node, times its first max_candidates kernels (tk_conv2d_block_algos; one
+ * warm-up + `reps` back-to-back launches each, HIP events on `stream`) and keeps the fastest in
+ * the node (block.algo).  Nodes with equal shapes and attributes share one measurement.
+ * Overwrites node outputs (run afterwards); synchronises `stream`.  Optional reports, n_nodes x
+ * (max_candidates + 1) each: algo_out[i][0] = the chosen algo (-1: node not tuned), [i][1 + c]
+ * = candidate c (-1 past the last); us_out likewise in microseconds per launch. */
+int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, int32_t* algo_out, float* us_out);
 
 /* ---------------------------------------------------------------- trace format
  * NDArray-list blob (src/runtime/file_utils.cc:184-236, include/tvm/runtime/ndarray.h:447-494):

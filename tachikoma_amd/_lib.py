@@ -97,6 +97,7 @@ class tk_block_attrs(ctypes.Structure):
         ("block_is_rhs", ctypes.c_int32),
         ("residual", ctypes.POINTER(tk_tensor)),
         ("add", tk_qnn_add_attrs),
+        ("algo", ctypes.c_int32),
     ]
 
 
@@ -274,6 +275,10 @@ SIGNATURES = {
     "tk_module_run_profiled": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_F32)]),
     "tk_module_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
     "tk_module_node_times": (ctypes.c_int, [_VP, ctypes.POINTER(_F32)]),
+    "tk_module_tune": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
+                                      ctypes.POINTER(_F32)]),
+    "tk_conv2d_block_algos": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_block_attrs), ctypes.POINTER(ctypes.c_int32),
+                                             ctypes.c_int]),
     "tk_ndlist_layout": (_I64, [ctypes.POINTER(tk_array_meta), ctypes.c_int, ctypes.POINTER(_I64)]),
     "tk_ndlist_write_headers": (ctypes.c_int, [ctypes.POINTER(tk_array_meta), ctypes.c_int, _VP, _I64]),
     "tk_ndlist_parse": (ctypes.c_int, [_VP, _I64, ctypes.c_int, ctypes.POINTER(tk_array_meta), ctypes.POINTER(_I64),

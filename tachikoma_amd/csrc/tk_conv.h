@@ -81,6 +81,8 @@ struct GemmArgs {
                        // 32768 flat epilogue without the lean groups, 65536 skip the flat groups,
                        // 131072 flat epilogue without the lean row-crossing groups (hw % 4 != 0),
                        // 8192 residual join without the LUTs, 16384 skip the add record,
+                       // (image-tile kernel: 32768 residual words not read from LDS, 65536 residual
+                       // words not loaded),
                        // 8/16/32/64 skip the conv / bias_add / requantize / clip record,
                        // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs, 1024 main-loop
                        // barrier without the lgkmcnt(0) drain, 2048 skip the fragment reads, 4096 skip
@@ -252,10 +254,16 @@ static int env_int(const char* name, int dflt) {
 int64_t conv_img_chunked_bytes(int rows_pad, int cin_pad, int taps);
 // Writes that image from the OIHW weight (int8, or uint8 stored xor 0x80).
 int conv_img_pack(const tk_tensor* weight, int8_t* dst, int rows_pad, int cin_pad, hipStream_t s);
-// Runs the conv block on the image-tile kernel when its plan applies (returns 1 and sets *rc),
-// else returns 0 and the caller takes the im2col kernel.  `chunked`: the chunked weight image
-// (NULL for 1x1 convs, whose packed weight already has that layout).
-int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked,
+// tk_block_attrs.algo values (tk_conv2d_block_algos): 0 the library's choice, 1 im2col tiles
+// (gemm_i8_kernel), 2 image tiles with the planner's plan, 16 + i image-tile plan i.
+constexpr int kAlgoIm2col = 1, kAlgoImg = 2, kAlgoImg0 = 16;
+// Runs the conv block on the image-tile kernel when its plan applies (returns 1 and sets *rc;
+// algo 0: the cheapest plan by the planner's estimate), else returns 0 (im2col path).
+// `chunked`: the chunked weight image (NULL for 1x1 convs, whose packed weight has that layout).
+int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked, int algo,
                  hipStream_t s, int* rc);
+// The image-tile plans as algo values (16 + i), cheapest estimate first; returns how many exist.
+int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked,
+                   int32_t* algos, int max_algos);
 
 }  // namespace tk

@@ -23,7 +23,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <string>
 #include <type_traits>
+#include <vector>
 
 #include "tk_conv.h"
 
@@ -46,19 +48,22 @@ struct ImgArgs {
   int32_t pstep;               // patch source bytes per stage (CC/16 shadow channel groups)
   int32_t tstride;             // int32 pitch of the epilogue staging rows
   int32_t rowc_off, lut_off, res_off;  // LDS byte offsets (the staging tile aliases the ring at 0)
-  uint64_t mg_pl, mg_img, mg_hc, mg_ws, mg_hw, mg_ow, mg_runq, mg_pe;  // (x * mg) >> 40 == x / d
-  int32_t runq;                // 4-element epilogue groups per image run (R * hw / 4)
+  uint64_t mg_pl, mg_img, mg_hc, mg_ws, mg_hw, mg_ow, mg_runq, mg_cw;  // (x * mg) >> 40 == x / d
+  int32_t runq;                // 4-element epilogue groups per image run and pass (R * cw / 4)
+  int32_t npass, cw;           // epilogue passes over the tile's columns (npass > 1: one image per
+                               // workgroup, cw = hw / npass pixels per pass), or 1 pass of cw = hw
 };
 
 // KT: 1 or 3 taps per axis; WM: 32-row wave groups (R = 32 * WM); CT: 32-column tiles per wave
-// (the waves of a row group take columns wn, wn + WN, ...).
-template <int KT, int WM, int CT>
+// (the waves of a row group take columns wn, wn + WN, ...); CC: input channels per K stage (32
+// for 3x3; 32, 64 or 128 for 1x1: smaller stages for larger planes or two workgroups per CU).
+template <int KT, int WM, int CT, int CC>
 __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, ImgArgs h) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   __shared__ int s_fast;
   constexpr int R = 32 * WM;
   constexpr int WN = 4 / WM;
-  constexpr int CC = KT == 3 ? 32 : 128;  // input channels per stage
+  static_assert(CC % 32 == 0 && (KT == 1 || CC == 32), "3x3 stages hold 32 channels");
   constexpr int TAPS = KT * KT;
   constexpr int SUB = CC / 32;             // K = 32 MFMA steps per tap and stage
   constexpr int KS = TAPS * SUB;           // K = 32 MFMA steps per stage
@@ -83,20 +88,22 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   const int8_t* fill_src = reinterpret_cast<const int8_t*>(tk_fill_rows.v + 16 * (g.fill & 0xFFu));
   const bool has_add = g.has_add;
   const int runq = h.runq;
-  const int total = nimg * runq;  // epilogue groups
+  const int npass = h.npass, W = h.cw;  // epilogue passes; pixels of a channel row per pass
+  const int total = (npass > 1 ? 1 : nimg) * runq;  // epilogue groups per pass
   if (tid == 0) s_fast = 1;       // visible after the first barrier; only cleared at the epilogue
 
   // ---- residual words of every epilogue group (qnn.add joins), LDS-DMA'd in group order during
   // the last K step (after its barrier: no counted ring wait follows, the epilogue's full wait
   // covers them), so that they neither delay the first stages nor expose their latency
-  auto issue_residual = [&]() __attribute__((always_inline)) {
+  auto issue_residual = [&](int c0) __attribute__((always_inline)) {
     for (int q0 = wave * 64; q0 < total; q0 += kGemmThreads) {
       const int gi = q0 + lane;
       const int8_t* src = reinterpret_cast<const int8_t*>(tk_zero_words);
       if (gi < total) {
         const int kk = (int)fdiv40((uint32_t)gi, h.mg_runq);
         const int f = (gi - kk * runq) * 4;
-        src = reinterpret_cast<const int8_t*>(g.add_res) + (uint32_t)(((img0 + kk) * g.M + m0) * hw + f);
+        const int r = (int)fdiv40((uint32_t)f, h.mg_cw), pp = f - r * W;  // row, pixel of the pass
+        src = reinterpret_cast<const int8_t*>(g.add_res) + (uint32_t)(((img0 + kk) * g.M + m0 + r) * hw + c0 + pp);
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (void*)(resw + q0), 4, 0, 0);
     }
@@ -210,7 +217,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       issue(nxt);
       nxt = nxt == ns - 1 ? 0 : nxt + 1;
     }
-    if (has_add && it == nst - 1) issue_residual();
+    if (has_add && it == nst - 1 && !TK_ABL(65536)) issue_residual(0);
     compute(smem + cur * h.stage_bytes);
     cur = cur == ns - 1 ? 0 : cur + 1;
   }
@@ -235,21 +242,26 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     lut[256 + tid] = g.add_up_r ? x : rq_tensor(x, g.add_pr);
   }
   const int ts = h.tstride;
+  // columns of the tile staged per pass: [c0, c0 + span)
+  const int span = npass > 1 ? W : h.p;
+  auto stage = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
-  for (int j = 0; j < CT; ++j)
-    if (j < jn) {
-      const int lc = (wn + WN * j) * 32 + (lane & 31);
+    for (int j = 0; j < CT; ++j)
+      if (j < jn) {
+        const int lc = (wn + WN * j) * 32 + (lane & 31) - c0;
+        if ((unsigned)lc < (unsigned)span) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) tileI[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * ts + lc] = acc[j][r];
-    }
-  lds_barrier();
+          for (int r = 0; r < 16; ++r) tileI[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * ts + lc] = acc[j][r];
+        }
+      }
+  };
 
-  // group gi = 4 consecutive elements of image run kk = gi / runq (channels m0 .. m0 + R, all hw
-  // pixels: contiguous NCHW memory), element f = 4 (gi % runq) = row r0 (channel m0 + r0), pixel p0.
-  // A thread's groups are 256 apart: the walk advances (kk, r0, p0) by 1024 elements per step
-  // without divisions.  hw % 4 == 0: a group lies in one channel row (one b128 read of the tile,
-  // one row of constants); else (7x7) it may cross into the next row, whose elements take that
-  // row's constants.
+  // group gi = 4 consecutive elements of image run kk = gi / runq (channels m0 .. m0 + R, the W
+  // pixels [c0, c0 + W) of each channel row: contiguous NCHW memory when W = hw), element
+  // f = 4 (gi % runq) = row r0 (channel m0 + r0), pixel p0.  A thread's groups are 256 apart: the
+  // walk advances (kk, r0, p0) by 1024 elements per step without divisions.  W % 4 == 0: a group
+  // lies in one channel row (one b128 read of the tile, one row of constants); else (7x7, one pass)
+  // it may cross into the next row, whose elements take that row's constants.
   const uint32_t n4 = g.out_elems * 4u;
   const auto r_conv = rec_rsrc(g.C, n4), r_bias = rec_rsrc(g.bias_out, n4);
   const auto r_rq = rec_rsrc(g.rq_out, g.out_elems);
@@ -258,15 +270,16 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
   const int32_t clip_lo = g.clip_lo, clip_hi = g.clip_hi, add_zp = g.add_zp;
   const int mode = g.rq.mode, Mrows = g.M;
-  const int dr = 1024 / hw, dp = 1024 - dr * hw;
+  const int dr = 1024 / W, dp = 1024 - dr * W;
+  int c0 = 0;  // first pixel of the current pass
   auto walk = [&](auto fast_c, auto add_c, auto clip_c, auto rowu_c) __attribute__((always_inline)) {
     constexpr bool FAST = decltype(fast_c)::value, ADD = decltype(add_c)::value, CLIP = decltype(clip_c)::value;
     constexpr bool ROWU = decltype(rowu_c)::value;
-    int kk = 0, r0 = (4 * tid) / hw, p0 = 4 * tid - r0 * hw;
+    int kk = 0, r0 = (4 * tid) / W, p0 = 4 * tid - r0 * W;
     while (r0 >= R) r0 -= R, ++kk;
     for (int gi = tid; gi < total; gi += kGemmThreads) {
-      const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0) * hw + r0 * hw + p0);
-      const int base = r0 * ts + kk * hw + p0;
+      const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0 + r0) * hw + c0 + p0);
+      const int base = r0 * ts + kk * W + p0;
       v4u v;
       EpiRow ra, rb;
       ra = rowc[r0];
@@ -276,13 +289,13 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       } else {
         rb = rowc[min(r0 + 1, R - 1)];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (uint32_t)tileI[base + e + (p0 + e >= hw ? ts - hw : 0)];
+        for (int e = 0; e < 4; ++e) v[e] = (uint32_t)tileI[base + e + (p0 + e >= W ? ts - W : 0)];
       }
       uint32_t fold[4], zp[4];
       int32_t bias[4], m[4], sh[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const bool nx = !ROWU && p0 + e >= hw;
+        const bool nx = !ROWU && p0 + e >= W;
         fold[e] = nx ? rb.fold : ra.fold;
         bias[e] = nx ? rb.bias : ra.bias;
         zp[e] = nx ? (uint32_t)rb.zp : (uint32_t)ra.zp;
@@ -312,11 +325,13 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
       if constexpr (ADD) {
         // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
-        const uint32_t res = resw[gi];
+        const uint32_t res = TK_ABL(32768) ? 0x01010101u : resw[gi];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          q[e] = clamp_i32(lut[q[e] & 0xFF] + lut[256 + ((res >> (8 * e)) & 0xFFu)] - add_zp, qmin, qmax);
-        if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
+          q[e] = clamp_i32(TK_ABL(8192) ? q[e] + (int32_t)((res >> (8 * e)) & 0xFFu) - add_zp
+                                        : lut[q[e] & 0xFF] + lut[256 + ((res >> (8 * e)) & 0xFFu)] - add_zp,
+                           qmin, qmax);
+        if (!TK_ABL(16384 | 2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
       }
       if constexpr (CLIP) {
 #pragma unroll
@@ -327,19 +342,19 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
         *reinterpret_cast<v4i*>(tileI + base) = v4i{q[0], q[1], q[2], q[3]};
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) tileI[base + e + (p0 + e >= hw ? ts - hw : 0)] = q[e];
+        for (int e = 0; e < 4; ++e) tileI[base + e + (p0 + e >= W ? ts - W : 0)] = q[e];
       }
       // next group: 1024 elements on
       r0 += dr;
       p0 += dp;
-      if (p0 >= hw) p0 -= hw, ++r0;
+      if (p0 >= W) p0 -= W, ++r0;
       while (r0 >= R) r0 -= R, ++kk;
     }
   };
   using T = std::true_type;
   using F = std::false_type;
   auto by_rowu = [&](auto fast_c, auto add_c, auto clip_c) __attribute__((always_inline)) {
-    if (hw % 4 == 0) walk(fast_c, add_c, clip_c, T{});
+    if (W % 4 == 0) walk(fast_c, add_c, clip_c, T{});
     else walk(fast_c, add_c, clip_c, F{});
   };
   auto by_clip = [&](auto fast_c, auto add_c) __attribute__((always_inline)) {
@@ -350,29 +365,42 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     if (has_add) by_clip(fast_c, T{});
     else by_clip(fast_c, F{});
   };
-  if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) by_add(T{});
-  else by_add(F{});
+  for (int pass = 0; pass < npass; ++pass) {
+    c0 = pass * W;
+    if (pass) {
+      lds_barrier();  // the previous pass is done with the staging tile and the residual words
+      if (has_add && !TK_ABL(65536)) issue_residual(c0);
+    }
+    stage(c0);
+    if (pass && has_add) {
+      wait_vm(0);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+    lds_barrier();  // (also publishes s_fast and the row constants)
+    if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) by_add(T{});
+    else by_add(F{});
 
-  // ---- the next conv's shadow: 16 channels of one pixel per 16-byte store; the tile's columns are
-  // the images' pixels in order, so column c is shadow pixel img0 * hw + c
-  if (g.shadow_out && !TK_ABL(1)) {
-    lds_barrier();
-    const int pe = nimg * hw;
-    const int items = (R / 16) * pe;
-    for (int it = tid; it < items; it += kGemmThreads) {
-      const int grp = (int)fdiv40((uint32_t)it, h.mg_pe);
-      const int col = it - grp * pe;
-      uint32_t wd[4];
+    // ---- the next conv's shadow: 16 channels of one pixel per 16-byte store; the pass's columns
+    // are the images' pixels in order, so column col is shadow pixel img0 * hw + c0 + col
+    if (g.shadow_out && !TK_ABL(1)) {
+      lds_barrier();
+      const int pe = npass > 1 ? W : nimg * hw;  // this pass's pixels (the last workgroup may hold fewer images)
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        uint32_t word = 0;
+      for (int grp = 0; grp < R / 16; ++grp)
+        for (int col = tid; col < pe; col += kGemmThreads) {
+          uint32_t wd[4];
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq)
-          word |= (((uint32_t)tileI[(grp * 16 + d * 4 + qq) * ts + col] ^ g.shadow_xor) & 0xFFu) << (8 * qq);
-        wd[d] = word;
-      }
-      *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)((m0 >> 4) + grp) * g.N + (int64_t)img0 * hw + col) * 16) =
-          v4i{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+          for (int d = 0; d < 4; ++d) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq)
+              word |= (((uint32_t)tileI[(grp * 16 + d * 4 + qq) * ts + col] ^ g.shadow_xor) & 0xFFu) << (8 * qq);
+            wd[d] = word;
+          }
+          *reinterpret_cast<v4i*>(g.shadow_out +
+                                  ((int64_t)((m0 >> 4) + grp) * g.N + (int64_t)img0 * hw + c0 + col) * 16) =
+              v4i{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+        }
     }
   }
 }
@@ -415,29 +443,44 @@ namespace {
 
 using ImgKernel = void (*)(GemmArgs, ImgArgs);
 
+template <int KT, int WM, int CC>
+ImgKernel img_kernel_cc(int ct) {
+  if constexpr (WM == 1) {
+    if (ct == 7) return conv_img_kernel<KT, WM, 7, CC>;
+  }
+  return ct == 2 ? conv_img_kernel<KT, WM, 2, CC> : conv_img_kernel<KT, WM, 4, CC>;
+}
+
 template <int KT, int WM>
-ImgKernel img_kernel(int ct) {
-  switch (ct) {
-    case 2: return conv_img_kernel<KT, WM, 2>;
-    case 4: return conv_img_kernel<KT, WM, 4>;
-    default: return conv_img_kernel<KT, WM, 7>;
+ImgKernel img_kernel(int ct, int cc) {
+  if constexpr (KT == 3) {
+    return img_kernel_cc<3, WM, 32>(ct);
+  } else {
+    return cc == 32 ? img_kernel_cc<1, WM, 32>(ct) : cc == 64 ? img_kernel_cc<1, WM, 64>(ct) : img_kernel_cc<1, WM, 128>(ct);
   }
 }
 
 struct ImgPlan {
   ImgArgs a;
   size_t lds;
-  int kt, wm, ct;
+  int kt, wm, ct, cc, occ;
   double cost;
 };
 
 uint64_t magic40(uint64_t d) { return ((1ull << 40) + d - 1) / d; }
 
-// One candidate tiling (R rows, ipt images per workgroup); false if it does not fit.
-bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R, int ipt, ImgPlan* out) {
-  const int CC = kt == 3 ? 32 : 128;
+// Most output columns a workgroup holds: 4 waves x 7 column tiles (R = 32), 2 x 4 (R = 64).
+constexpr int kImgMaxCols = 4 * 7 * 32;
+
+// One candidate tiling (R rows, ipt images per workgroup, CC channels per stage, one or two
+// workgroups per CU, the epilogue in npass column passes); false if it does not fit.
+bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R, int ipt, int CC, bool two,
+                   int npass, ImgPlan* out) {
   const int taps = kt * kt;
   const int hw = g.OH * g.OW;
+  // several passes: one image per workgroup, each pass a whole number of 4-pixel groups per row
+  if (npass > 1 && (ipt != 1 || hw % (4 * npass))) return false;
+  const int cw = hw / npass;
   const int p = ipt * hw;
   const int nct = (p + 31) / 32;
   const int wm = R / 32, wn = 4 / wm;
@@ -470,28 +513,30 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   const int64_t pstep = (int64_t)(CC / 16) * ga.in_pix * 16;
   if (pstep >= (1ll << 31)) return false;
   x.pstep = (int32_t)pstep;
-  x.tstride = nct * 32 + 4;
-  // ring depth: every slot the LDS holds (up to 8, no more than the stages need), at least 3 where
-  // there are more than 2 stages.  Grids of several rounds keep two workgroups per CU (80 KB each)
-  // when that still gives 3 slots: one workgroup's epilogue stores then overlap the other's K loop.
-  const size_t extra = (size_t)R * sizeof(EpiRow) + 2048 + (ga.has_add ? ((size_t)p * R + 255) / 256 * 256 : 0);
+  x.npass = npass;
+  x.cw = cw;
+  x.tstride = npass > 1 ? cw + 4 : nct * 32 + 4;
+  // ring depth: every slot the LDS budget holds (up to 8, no more than the stages need), at least
+  // 3 where there are more than 2 stages and one workgroup per CU.  The budget is the CU's 160 KB, or half of it for two
+  // resident workgroups (one's epilogue stores then overlap the other's K loop).
+  const size_t res_bytes = ga.has_add ? ((size_t)(npass > 1 ? cw : p) * R + 255) / 256 * 256 : 0;
+  const size_t extra = (size_t)R * sizeof(EpiRow) + 2048 + res_bytes;
   const size_t tile = (size_t)R * x.tstride * 4;
   const int cap = env_int("TK_IMG_NS", 8);
-  auto slots = [&](size_t budget) -> int {
-    if (tile > budget) return 0;
-    return (int)std::min<size_t>({(size_t)cap, budget / x.stage_bytes, (size_t)x.stages + 1});
-  };
-  const int need = x.stages > 2 ? 3 : 2;
-  const size_t half = 80 * 1024 - 64 - extra, full = 160 * 1024 - 64 - extra;
-  x.ns = x.wgs > 256 && slots(half) >= need && env_int("TK_IMG_TWO", 1) ? slots(half) : slots(full);
-  if (x.ns < need) return false;
+  const size_t budget = (two ? 80 : 160) * 1024 - 64 - extra;
+  if (tile > budget) return false;
+  x.ns = (int)std::min<size_t>({(size_t)cap, budget / x.stage_bytes, (size_t)x.stages + 1});
+  // one workgroup per CU needs a stage in flight while it computes; two may double-buffer (the
+  // other workgroup computes while this one waits)
+  if (x.ns < (x.stages > 2 && !two ? 3 : 2)) return false;
   const size_t ring = (size_t)x.ns * x.stage_bytes;
   x.rowc_off = (int32_t)std::max(ring, tile);
   x.lut_off = x.rowc_off + R * (int)sizeof(EpiRow);
   x.res_off = x.lut_off + 2048;
-  const size_t lds = (size_t)x.res_off + (ga.has_add ? ((size_t)p * R + 255) / 256 * 256 : 0);
-  if (lds > 160 * 1024 - 64) return false;
-  x.runq = R * hw / 4;
+  const size_t lds = (size_t)x.res_off + res_bytes;
+  if (lds > (two ? 80 : 160) * 1024 - 64) return false;
+  x.runq = R * cw / 4;
+  x.mg_cw = magic40(cw);
   x.mg_pl = magic40(x.pl);
   x.mg_img = magic40((uint64_t)x.hr * x.hc);
   x.mg_hc = magic40(x.hc);
@@ -499,59 +544,111 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   x.mg_hw = magic40(hw);
   x.mg_ow = magic40(g.OW);
   x.mg_runq = magic40(x.runq);
-  x.mg_pe = magic40(p);
   out->a = x;
   out->lds = lds;
   out->kt = kt;
   out->wm = wm;
   out->ct = ct;
-  // estimated time: rounds of one workgroup per CU x max(L2 -> LDS bytes at ~55 GB/s per CU, the
-  // busiest wave's MFMA cycles at ~2.1 GHz); the record stores are the same for every candidate
+  out->cc = CC;
+  out->occ = two ? 2 : 1;
+  // estimated time per CU (ns): each workgroup's K loop = max(L2 -> LDS bytes at ~55 GB/s per CU,
+  // the busiest wave's MFMA cycles at ~2.1 GHz) and epilogue = its record bytes at ~22 GB/s per CU
+  // (~5.6 TB/s over 256 CUs), plus ~2 us of load latency per round.  One workgroup per CU runs
+  // them back to back; two overlap one's epilogue with the other's K loop.
   const double K = (double)taps * g.cin_pad;
   const double bytes = R * K + (double)x.pl * g.cin_pad;
-  const double mfma_ns = ct_need * K / 2.1;
-  const double rounds = std::ceil(x.wgs / 256.0);
-  out->cost = rounds * std::max(bytes / 55.0, mfma_ns);
+  const double main_ns = std::max(bytes / 55.0, ct_need * K / 2.1);
+  const double epi_ns = (double)R * p * (ga.has_add ? 12.0 : 10.0) / 22.0;
+  const double per_cu = std::ceil(x.wgs / 256.0);
+  const double lat = 2000.0;
+  out->cost = two && per_cu >= 2 ? per_cu * std::max(main_ns, epi_ns) + lat + std::min(main_ns, epi_ns)
+                                 : per_cu * (lat + main_ns + epi_ns);
+  out->cost += per_cu * (npass - 1) * 1000.0;  // a store drain + barrier per extra pass
   return true;
 }
 
 }  // namespace
 
-int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked,
-                 hipStream_t s, int* rc) {
-  if (!env_int("TK_IMG", 1) || !ga.bias_out) return 0;  // conv blocks only
-  if (ga.RB || ga.zA_vec || ga.zA != 0) return 0;       // the weights' zero point must be 0
-  if (a->dilation[0] != 1 || a->dilation[1] != 1) return 0;
+namespace {
+
+// Every image-tile plan that applies to the conv block, in enumeration order (R, stage width,
+// images per tile, one or two workgroups per CU); empty when the kernel does not apply.
+std::vector<ImgPlan> img_plans(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked) {
+  std::vector<ImgPlan> out;
+  if (!env_int("TK_IMG", 1) || !ga.bias_out) return out;  // conv blocks only
+  if (ga.RB || ga.zA_vec || ga.zA != 0) return out;       // the weights' zero point must be 0
+  if (a->dilation[0] != 1 || a->dilation[1] != 1) return out;
   const int st = a->strides[0];
-  if (a->strides[1] != st || (st != 1 && st != 2)) return 0;
+  if (a->strides[1] != st || (st != 1 && st != 2)) return out;
   int kt = 0;
   if (g.KH == 3 && g.KW == 3 && a->padding[0] == 1 && a->padding[1] == 1 && a->padding[2] == 1 && a->padding[3] == 1)
     kt = 3;
   else if (g.KH == 1 && g.KW == 1 && !a->padding[0] && !a->padding[1] && !a->padding[2] && !a->padding[3])
     kt = 1;
-  if (!kt || (kt == 3 && !chunked)) return 0;
-  if (kt == 3 && !env_int("TK_IMG3", 1)) return 0;
-  if (kt == 1 && !env_int("TK_IMG1", 1)) return 0;
-  const int CC = kt == 3 ? 32 : 128;
+  if (!kt || (kt == 3 && !have_chunked)) return out;
+  if (kt == 3 && !env_int("TK_IMG3", 1)) return out;
+  if (kt == 1 && !env_int("TK_IMG1", 1)) return out;
   const int hw = g.OH * g.OW;
-  if (g.cin_pad % CC || g.O % 32 || hw > env_int("TK_IMG_MAXHW", 256) || hw < 4 ||
+  if (g.cin_pad % 32 || g.O % 32 || hw > env_int("TK_IMG_MAXHW", kImgMaxCols) || hw < 4 ||
       (int64_t)g.N * hw * g.O * 4 >= 0xFFFFFFC0ll)
-    return 0;
-  ImgPlan best{}, c{};
-  bool have = false;
+    return out;
   const int force_r = env_int("TK_IMG_R", 0), force_ipt = env_int("TK_IMG_IPT", 0);
+  const int force_cc = env_int("TK_IMG_CC", 0), two_mode = env_int("TK_IMG_TWO", 1);  // 0 never, 2 only
+  ImgPlan c{};
   for (int R : {64, 32}) {
     if (g.O % R || (force_r && R != force_r)) continue;
-    for (int ipt = std::min(256 / hw, g.N); ipt >= 1; --ipt) {
-      if (force_ipt && ipt != force_ipt) continue;
-      if (img_candidate(g, ga, kt, st, R, ipt, &c) && (!have || c.cost < best.cost)) best = c, have = true;
+    const int maxcols = R == 32 ? kImgMaxCols : 256;
+    for (int CC : {128, 64, 32}) {
+      if ((kt == 3 && CC != 32) || g.cin_pad % CC || (force_cc && CC != force_cc)) continue;
+      for (int ipt = std::min(maxcols / hw, g.N); ipt >= 1; --ipt) {
+        if (force_ipt && ipt != force_ipt) continue;
+        for (int two = 0; two < 2; ++two) {
+          if ((two && !two_mode) || (!two && two_mode == 2)) continue;
+          for (int npass : {1, 2, 4})
+            if (img_candidate(g, ga, kt, st, R, ipt, CC, two, npass, &c)) out.push_back(c);
+        }
+      }
     }
   }
-  if (!have) return 0;
+  return out;
+}
+
+}  // namespace
+
+int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked,
+                   int32_t* algos, int max_algos) {
+  const std::vector<ImgPlan> plans = img_plans(g, a, ga, have_chunked);
+  std::vector<int> order(plans.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return plans[x].cost < plans[y].cost; });
+  for (int k = 0; k < (int)order.size() && k < max_algos; ++k) algos[k] = kAlgoImg0 + order[k];
+  return (int)plans.size();
+}
+
+int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked, int algo,
+                 hipStream_t s, int* rc) {
+  if (algo == kAlgoIm2col) return 0;
+  const std::vector<ImgPlan> plans = img_plans(g, a, ga, chunked != nullptr);
+  if (plans.empty() && algo == 0) return 0;
+  if (plans.empty() || (algo >= kAlgoImg0 && algo - kAlgoImg0 >= (int)plans.size()) ||
+      (algo != 0 && algo != kAlgoImg && algo < kAlgoImg0)) {
+    set_error("tk_qnn_conv2d_block: algo " + std::to_string(algo) + " does not apply to this conv (" +
+              std::to_string(plans.size()) + " image-tile plans; see tk_conv2d_block_algos)");
+    *rc = TK_ERR_INVALID_ARG;
+    return 1;
+  }
+  ImgPlan best = plans[0];
+  if (algo >= kAlgoImg0) {
+    best = plans[algo - kAlgoImg0];
+  } else {
+    for (const ImgPlan& p : plans)
+      if (p.cost < best.cost) best = p;
+  }
+  const int kt = best.kt;
   best.a.wimg = kt == 3 ? chunked : ga.A;
   best.a.ldw = kt == 3 ? 9 * g.cin_pad : ga.lda;
-  ImgKernel kern = kt == 3 ? (best.wm == 2 ? img_kernel<3, 2>(best.ct) : img_kernel<3, 1>(best.ct))
-                           : (best.wm == 2 ? img_kernel<1, 2>(best.ct) : img_kernel<1, 1>(best.ct));
+  ImgKernel kern = kt == 3 ? (best.wm == 2 ? img_kernel<3, 2>(best.ct, 32) : img_kernel<3, 1>(best.ct, 32))
+                           : (best.wm == 2 ? img_kernel<1, 2>(best.ct, best.cc) : img_kernel<1, 1>(best.ct, best.cc));
   if (best.lds > 64 * 1024) {
     // dynamic LDS beyond 64 KiB must be allowed per kernel (the static s_fast word counts too)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,

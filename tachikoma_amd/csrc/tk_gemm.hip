@@ -1844,7 +1844,7 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
                                 ? (const int8_t*)packed + (int64_t)g.rows_pad * g.k_pad
                                 : nullptr;
     int irc = TK_OK;
-    if (conv_img_try(g, a, ga, chunked, s, &irc)) return irc;
+    if (conv_img_try(g, a, ga, chunked, blk->attrs->algo, s, &irc)) return irc;
   }
   const bool mt1 = conv_mt1(g, blk != nullptr);
   const int ipt = mt1 ? conv_image_tiles(g, blk != nullptr, conv_needs_patch(weight, a)) : 0;
@@ -1915,6 +1915,32 @@ int conv2d_block_impl(const tk_tensor* data, const void* shadow, const tk_tensor
   TK_CHECK_ARG(outs && n_outs >= 3 && outs[0], "block needs outputs");
   BlockIO b{bias, outs, n_outs, attrs, shadow_out};
   return conv2d_run(data, shadow, weight, packed, sums, outs[0], attrs ? &attrs->conv : nullptr, patch, &b, s);
+}
+
+int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
+                            int32_t* algos, int max_algos) {
+  TK_CHECK_ARG(data && weight && attrs && (algos || max_algos <= 0), "null argument");
+  ConvGeom g;
+  if (conv_geom(data, weight, &attrs->conv, &g) != TK_OK) {
+    set_error("tk_conv2d_block_algos: bad shapes");
+    return TK_ERR_SHAPE;
+  }
+  if (!use_mfma_conv(g, attrs->conv.groups) || !is_int8ish(data) || !is_int8ish(weight)) return 0;
+  // what the image-tile planner reads of the launch arguments (see conv2d_run)
+  static int32_t marker;
+  GemmArgs ga{};
+  ga.bias_out = &marker;
+  ga.has_add = attrs->has_add;
+  ga.in_pix = (int64_t)g.N * g.H * g.W;
+  ga.zA = attrs->conv.kernel_zero_point - (is_uint(weight, 8) ? 128 : 0);
+  ga.zA_vec = attrs->conv.kernel_zero_points;
+  ga.RB = conv_needs_patch(weight, &attrs->conv) ? &marker : nullptr;
+  int n = 0;
+  if (max_algos > 0) algos[0] = kAlgoIm2col;
+  ++n;
+  n += conv_img_algos(g, &attrs->conv, ga, g.KH * g.KW == 1 || conv_img_chunked_bytes(g.rows_pad, g.cin_pad, g.KH * g.KW),
+                      algos ? algos + 1 : nullptr, max_algos - 1);
+  return n;
 }
 
 int64_t conv2d_workspace_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* a) {

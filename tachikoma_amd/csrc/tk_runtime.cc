@@ -8,6 +8,7 @@
 // host memory on a second stream, each copy gated by an event recorded right
 // after the node, so the PCIe transfer of node i overlaps the kernels of nodes > i.
 #include <cstring>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -53,6 +54,8 @@ int conv2d_block_impl(const tk_tensor* data, const void* shadow, const tk_tensor
                       const tk_block_attrs* attrs, void* scratch, void* shadow_out, hipStream_t s);
 int dense_block_impl(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,
                      int n_outs, const tk_block_attrs* attrs, void* workspace, hipStream_t s);
+int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
+                            int32_t* algos, int max_algos);
 
 // A tensor descriptor owned by the module (shape copied).
 struct OwnedTensor {
@@ -209,6 +212,10 @@ int tk_qnn_conv2d_block(const tk_tensor* data, const void* shadow, const tk_tens
                         const tk_block_attrs* attrs, void* scratch, void* shadow_out, void* stream) {
   return tk::conv2d_block_impl(data, shadow, weight, packed, weight_sums, bias, outs, n_outs, attrs, scratch,
                                shadow_out, tk::as_stream(stream));
+}
+int tk_conv2d_block_algos(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
+                          int32_t* algos, int max_algos) {
+  return tk::conv2d_block_algos_impl(data, weight, attrs, algos, max_algos);
 }
 int tk_qnn_dense_block(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,
                        int n_outs, const tk_block_attrs* attrs, void* workspace, void* stream) {
@@ -456,6 +463,109 @@ int tk_module_run_profiled(tk_module* mod, void* stream, float* node_ms) {
   TK_HIP(hipEventSynchronize(mod->prof[n]));
   for (size_t i = 0; i < n; ++i) TK_HIP(hipEventElapsedTime(&node_ms[i], mod->prof[i], mod->prof[i + 1]));
   return TK_OK;
+}
+
+// Shape + attribute key of a conv-block node: nodes with equal keys run the same kernels on the
+// same amount of work, so one measurement serves all of them.
+static std::string tune_key(const tk::Node& n) {
+  const tk_node& d = n.desc;
+  const tk_block_attrs& b = d.attrs.block;
+  std::string k;
+  auto add = [&](int64_t v) { k += std::to_string(v) + ","; };
+  for (int i = 0; i < 2; ++i) {
+    const tk_tensor& t = n.in[i].t;
+    add(t.dtype.code), add(t.dtype.bits);
+    for (int j = 0; j < t.ndim; ++j) add(t.shape[j]);
+    k += "|";
+  }
+  for (int v : b.conv.strides) add(v);
+  for (int v : b.conv.padding) add(v);
+  for (int v : b.conv.dilation) add(v);
+  add(b.conv.groups), add(b.conv.input_zero_point), add(b.conv.kernel_zero_point), add(b.conv.kernel_zero_points != nullptr);
+  add(b.requantize.mode), add(b.has_clip), add(b.has_add), add(d.n_outputs), add(d.ext[4] != nullptr);
+  return k;
+}
+
+int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, int32_t* algo_out, float* us_out) {
+  if (!mod || max_candidates < 1 || reps < 1) {
+    tk::set_error("tk_module_tune: invalid argument");
+    return TK_ERR_INVALID_ARG;
+  }
+  hipStream_t s = tk::as_stream(stream);
+  const int W = max_candidates + 1;
+  const size_t n = mod->nodes.size();
+  if (algo_out)
+    for (size_t i = 0; i < n * W; ++i) algo_out[i] = -1;
+  if (us_out)
+    for (size_t i = 0; i < n * W; ++i) us_out[i] = -1.0f;
+  int rc0 = wait_capture(mod, s);
+  if (rc0) return rc0;
+  hipEvent_t e0, e1;
+  TK_HIP(hipEventCreate(&e0));
+  if (hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    tk::set_error("tk_module_tune: hipEventCreate failed");
+    return TK_ERR_HIP;
+  }
+  struct Result {
+    int best;
+    std::vector<int32_t> algos;
+    std::vector<float> us;
+  };
+  std::map<std::string, Result> seen;
+  int rc = TK_OK;
+  for (size_t i = 0; i < n && rc == TK_OK; ++i) {
+    tk::Node& node = mod->nodes[i];
+    if (node.desc.kind != TK_NODE_CONV_BLOCK) continue;
+    const std::string key = tune_key(node);
+    auto it = seen.find(key);
+    if (it == seen.end()) {
+      Result r{0, std::vector<int32_t>(max_candidates, -1), std::vector<float>(max_candidates, -1.0f)};
+      int total = tk_conv2d_block_algos(&node.in[0].t, &node.in[1].t, &node.desc.attrs.block, r.algos.data(),
+                                        max_candidates);
+      if (total < 0) {
+        rc = total;
+        break;
+      }
+      float best_us = 0.0f;
+      for (int c = 0; c < std::min(total, max_candidates) && rc == TK_OK; ++c) {
+        node.desc.attrs.block.algo = r.algos[c];
+        rc = tk::run_node(node, s);  // warm-up (and the image-tile kernel's LDS attribute)
+        if (rc) break;
+        if (hipEventRecord(e0, s) != hipSuccess) rc = TK_ERR_HIP;
+        for (int k = 0; k < reps && rc == TK_OK; ++k) rc = tk::run_node(node, s);
+        if (rc == TK_OK && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess)) rc = TK_ERR_HIP;
+        float ms = 0.0f;
+        if (rc == TK_OK && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = TK_ERR_HIP;
+        if (rc) break;
+        r.us[c] = ms * 1e3f / (float)reps;
+        if (c == 0 || r.us[c] < best_us) best_us = r.us[c], r.best = r.algos[c];
+      }
+      if (rc) {
+        node.desc.attrs.block.algo = 0;
+        if (rc == TK_ERR_HIP) tk::set_error("tk_module_tune: node " + std::to_string(i) + ": HIP timing failed");
+        else tk::set_error("tk_module_tune: node " + std::to_string(i) + ": " + tk_last_error());
+        break;
+      }
+      it = seen.emplace(key, std::move(r)).first;
+    }
+    const Result& r = it->second;
+    node.desc.attrs.block.algo = r.best;
+    if (algo_out) {
+      algo_out[i * W] = r.best;
+      for (int c = 0; c < max_candidates; ++c) algo_out[i * W + 1 + c] = r.algos[c];
+    }
+    if (us_out) {
+      float b = -1.0f;
+      for (int c = 0; c < max_candidates; ++c)
+        if (r.algos[c] == r.best) b = r.us[c];
+      us_out[i * W] = b;
+      for (int c = 0; c < max_candidates; ++c) us_out[i * W + 1 + c] = r.us[c];
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return rc;
 }
 
 }  // extern "C"

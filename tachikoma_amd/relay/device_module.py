@@ -38,7 +38,7 @@ def torch_dtype(name: str):
 
 
 class DeviceModule:
-    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], dev=None, fuse: bool = True):
+    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], dev=None, fuse: bool = True, tune: bool = True):
         torch = _torch()
         if not torch.cuda.is_available():
             raise _lib.TachikomaError("no MI355X visible: the engine runs on the GPU only (no CPU fallback)")
@@ -53,9 +53,12 @@ class DeviceModule:
         # weights + weight sums), re-run whenever the param's device copy is rewritten
         self._derived: Dict[str, List[Callable[[int], None]]] = {}
         self.groups = exec_groups(plan, fuse=fuse)
+        self.tuning: List[dict] = []
         with torch.cuda.device(self.device):
             self._alloc(params)
             self._build_nodes()
+            if tune:
+                self.tune()
 
     # ------------------------------------------------------------ setup
     def _alloc(self, params):
@@ -526,6 +529,27 @@ class DeviceModule:
         for i, recs in enumerate(self.node_records):
             key = "+".join(recs) if recs else f"<shadow:{i}>"
             out[key] = float(ms[i])
+        return out
+
+    def tune(self, max_candidates: int = 8, reps: int = 5, stream=None) -> List[dict]:
+        """Find step (tk_module_tune): every MFMA conv-block node keeps the fastest of its first
+        ``max_candidates`` kernels, timed on this GPU.  All kernels give bit-identical records.
+        Returns (and keeps in ``self.tuning``) per tuned node: records, chosen algo, its time and
+        every candidate's."""
+        w = max_candidates + 1
+        algos = (ctypes.c_int32 * (self.n_nodes * w))()
+        us = (ctypes.c_float * (self.n_nodes * w))()
+        _lib.check(self.lib.tk_module_tune(self.handle, ctypes.c_void_p(_lib.stream_handle(stream)), max_candidates, reps,
+                                           algos, us), "tk_module_tune")
+        out = []
+        for i in range(self.n_nodes):
+            if algos[i * w] < 0:
+                continue
+            cands = [(int(algos[i * w + 1 + c]), round(float(us[i * w + 1 + c]), 2)) for c in range(max_candidates)
+                     if algos[i * w + 1 + c] >= 0]
+            out.append({"node": i, "records": list(self.node_records[i]), "algo": int(algos[i * w]),
+                        "us": round(float(us[i * w]), 2), "candidates": cands})
+        self.tuning = out
         return out
 
     def set_profiling(self, enable: bool) -> None:

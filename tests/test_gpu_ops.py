@@ -403,6 +403,73 @@ def test_conv_img_block(tk, case):
     np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
 
 
+# every kernel a block can run on (tk_conv2d_block_algos: im2col tiles and each image-tile plan --
+# R = 32 / 64 rows, 32 / 64 / 128-channel stages, 1..28 images per workgroup, one or two workgroups
+# per CU), incl. the 28x28 planes that only R = 32 x 7 column tiles per wave cover
+ALGO_CASES = [
+    # N, C, H, O, K, stride, dtype, za, residual add params or None, clip
+    (3, 128, 28, 128, 3, 1, "int8", -2, None, (0, 127)),
+    (2, 128, 28, 512, 1, 1, "int8", 3, (0.05, 3, 0.07, -2, 0.09, 1), (1, 127)),
+    (3, 256, 14, 1024, 1, 1, "uint8", 131, (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
+    (4, 256, 14, 256, 3, 1, "int8", 1, None, (0, 127)),
+    (5, 512, 7, 512, 3, 1, "int8", -1, None, (0, 127)),
+    (3, 256, 56, 512, 1, 2, "int8", 2, None, None),
+    (2, 64, 28, 96, 1, 1, "int8", 0, None, (0, 127)),
+]
+
+
+@pytest.mark.parametrize("case", ALGO_CASES, ids=[f"algo{i}" for i in range(len(ALGO_CASES))])
+def test_conv_block_every_algo(tk, case):
+    """Each algo tk_conv2d_block_algos lists gives the oracle's records bit for bit."""
+    n, c, h, o, k, st, dt, za, ap, clip = case
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
+    x = _rand(rng, (n, c, h, h), dt)
+    wt = _rand(rng, (o, c, k, k), "int8")
+    bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
+    s_in = rng.uniform(1e-5, 1e-3, size=o).astype(np.float32)
+    s_out = np.float32(0.01)
+    p = k // 2
+    pad = (p, p, p, p)
+    oh = (h + 2 * p - k) // st + 1
+    kw = dict(clip=clip, strides=(st, st), padding=pad, out_dtype=dt, want_shadow=True)
+    residual = None
+    if ap is not None:
+        residual = _rand(rng, (n, o, oh, oh), dt)
+        kw.update(residual=residual, add_params=ap)
+    algos = tk.conv2d_block(x, wt, bias, za, 0, s_in, s_out, 3, algos_only=True, **kw)
+    assert algos[0] == 1 and len(algos) >= 2, algos
+    conv = ref.qnn_conv2d(x, wt, za, 0, strides=(st, st), padding=pad)
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(3), axis=1, out_dtype=dt)
+    exp = [conv, badd, rq]
+    if ap is not None:
+        exp.append(ref.qnn_add(rq, residual, *ap))
+    if clip is not None:
+        exp.append(ref.clip(exp[-1], *clip))
+    exp.append(blocked_shadow(exp[-1]))
+    bad = []
+    for algo in [0] + algos:
+        outs = tk.conv2d_block(x, wt, bias, za, 0, s_in, s_out, 3, algo=algo, **kw)
+        for i, (got, e) in enumerate(zip(outs, exp)):
+            if not np.array_equal(got, e):
+                where = np.argwhere(got != e)
+                bad.append(f"algo {algo} output {i}: {len(where)} of {e.size} differ, first at {where[0].tolist()}, "
+                           f"index ranges {where.min(0).tolist()}..{where.max(0).tolist()}")
+    assert not bad, "\n".join(bad)
+
+
+def test_conv_block_bad_algo(tk):
+    """An algo the block does not have fails loudly (no silent fallback)."""
+    rng = np.random.default_rng(5)
+    x = _rand(rng, (2, 64, 14, 14), "int8")
+    wt = _rand(rng, (64, 64, 1, 1), "int8")
+    bias = np.zeros(64, np.int32)
+    s_in = np.full(64, 1e-4, np.float32)
+    n_algos = len(tk.conv2d_block(x, wt, bias, 1, 0, s_in, np.float32(0.01), 3, algos_only=True))
+    with pytest.raises(Exception, match="does not apply"):
+        tk.conv2d_block(x, wt, bias, 1, 0, s_in, np.float32(0.01), 3, algo=16 + n_algos)
+
+
 @pytest.mark.parametrize("k", [1, 3])
 @pytest.mark.parametrize("rounding", ["UPWARD", "TONEAREST"])
 def test_conv_img_shift_regimes(tk, rounding, k):

@@ -251,10 +251,11 @@ def _rq_attrs(r, keep, input_scale, output_scale, output_zero_point, rounding="U
 
 def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1, 1), padding=(0, 0, 0, 0),
                  dilation=(1, 1), groups=1, out_dtype="int8", want_shadow=False, residual=None, add_params=None,
-                 block_is_rhs=False, rounding="UPWARD"):
+                 block_is_rhs=False, rounding="UPWARD", algo=0, algos_only=False):
     """Fused conv -> bias_add -> requantize(axis 1) [-> qnn.add(., residual)] [-> clip] through
     tk_qnn_conv2d_block.  add_params = (ls, lz, rs, rz, os, oz) of the qnn.add (lhs = the block's
-    requantize output unless block_is_rhs)."""
+    requantize output unless block_is_rhs).  algo: tk_block_attrs.algo; algos_only: return the
+    block's kernel list (tk_conv2d_block_algos) instead of running it."""
     lib = _lib.load()
     n, c, h, wd = x.shape
     o = w.shape[0]
@@ -288,7 +289,14 @@ def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1,
         a.block_is_rhs = int(block_is_rhs)
         a.residual = res_ref.ptr
         _add_attrs(a.add, *add_params)
+    a.algo = int(algo)
     rx, rw, rb = ref(xd), ref(wdv), ref(bd)
+    if algos_only:
+        buf = (ctypes.c_int32 * 256)()
+        cnt = lib.tk_conv2d_block_algos(rx.ptr, rw.ptr, ctypes.byref(a), buf, 256)
+        _lib.check(min(cnt, 0), "tk_conv2d_block_algos")
+        assert cnt <= 256
+        return [int(buf[i]) for i in range(cnt)]
     ws_bytes = lib.tk_qnn_conv2d_workspace_bytes(rx.ptr, rw.ptr, ctypes.byref(a.conv))
     shadow = packed = sums = patch = shadow_out = None
     st = stream()

@@ -28,12 +28,27 @@ def main(path, model="resnet50", batch=64):
     gap = defaultdict(list)
     kname = {}
     n = len(blocks)
+    # launches per step: the smallest period >= n of the kernel-name sequence (a split-K block
+    # launches its partial tiles, then the reduce that runs the epilogue)
+    names = [r["Kernel_Name"] for r in g_rows]
+    L = next(p for p in range(n, n + 8)
+             if len(names) % p == 0 and all(names[i] == names[i % p] for i in range(len(names))))
     dur = defaultdict(list)
-    for i, r in enumerate(g_rows[-(len(g_rows) // n) * n:]):
-        dur[i % n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-        if id(r) in prev_end:
-            gap[i % n].append((int(r["Start_Timestamp"]) - prev_end[id(r)]) / 1e3)
-        kname[i % n] = r["Kernel_Name"].split("(")[0].replace("void tk::", "")
+    for st in range(len(g_rows) // L):
+        step = g_rows[st * L:(st + 1) * L]
+        i = 0
+        pending = 0.0
+        for r in step:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            if "true, false, 1," in r["Kernel_Name"] and L > n:  # split-K partials: + the reduce
+                pending += d
+                continue
+            dur[i].append(d + pending)
+            pending = 0.0
+            if id(r) in prev_end:
+                gap[i].append((int(r["Start_Timestamp"]) - prev_end[id(r)]) / 1e3)
+            kname[i] = r["Kernel_Name"].split("(")[0].replace("void tk::", "")
+            i += 1
     print(f"{'layer':34s} {'us':>8s} {'GB/s':>8s} {'TOPS':>7s} {'gap us':>7s}  kernel")
     tot = tgap = 0
     for i, g in enumerate(blocks):
