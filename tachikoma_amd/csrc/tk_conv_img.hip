@@ -52,6 +52,7 @@ struct ImgArgs {
   int32_t runq;                // 4-element epilogue groups per image run and pass (R * cw / 4)
   int32_t npass, cw;           // epilogue passes over the tile's columns (npass > 1: one image per
                                // workgroup, cw = hw / npass pixels per pass), or 1 pass of cw = hw
+  int32_t skew;                // profiling: odd waves start the epilogue walk this many s_sleep units late
 };
 
 // KT: 1 or 3 taps per axis; WM: 32-row wave groups (R = 32 * WM); CT: 32-column tiles per wave
@@ -272,30 +273,59 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   const int mode = g.rq.mode, Mrows = g.M;
   const int dr = 1024 / W, dp = 1024 - dr * W;
   int c0 = 0;  // first pixel of the current pass
+  // nontemporal record stores (plain ones measured no faster, also on multi-pass epilogues:
+  // profiles/r03k_img_epilogue_ablations.txt)
+  auto st128 = [&](v4u v, __amdgpu_buffer_rsrc_t rsrc, uint32_t off) __attribute__((always_inline)) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), rsrc, off, 0, kAuxNT);
+  };
+  auto st32 = [&](uint32_t v, __amdgpu_buffer_rsrc_t rsrc, uint32_t off) __attribute__((always_inline)) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, rsrc, off, 0, kAuxNT);
+  };
   auto walk = [&](auto fast_c, auto add_c, auto clip_c, auto rowu_c) __attribute__((always_inline)) {
     constexpr bool FAST = decltype(fast_c)::value, ADD = decltype(add_c)::value, CLIP = decltype(clip_c)::value;
     constexpr bool ROWU = decltype(rowu_c)::value;
     int kk = 0, r0 = (4 * tid) / W, p0 = 4 * tid - r0 * W;
     while (r0 >= R) r0 -= R, ++kk;
-    for (int gi = tid; gi < total; gi += kGemmThreads) {
-      const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0 + r0) * hw + c0 + p0);
-      const int base = r0 * ts + kk * W + p0;
-      v4u v;
-      EpiRow ra, rb;
-      ra = rowc[r0];
+    // software pipeline by one group: the next group's tile values, row constants and residual
+    // word are read from LDS before this group's arithmetic and stores (at one or two waves per
+    // SIMD nothing else hides the LDS latency); slots are read unconditionally (in bounds: the
+    // walk position of a group past the end still lies inside the staging tile)
+    auto load = [&](int r, int base, int p, int gi, v4u& v, EpiRow& ra, EpiRow& rb, uint32_t& res)
+        __attribute__((always_inline)) {
+      ra = rowc[min(r, R - 1)];
       if constexpr (ROWU) {
         v = *reinterpret_cast<const v4u*>(tileI + base);
         rb = ra;
       } else {
-        rb = rowc[min(r0 + 1, R - 1)];
+        rb = rowc[min(r + 1, R - 1)];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (uint32_t)tileI[base + e + (p0 + e >= W ? ts - W : 0)];
+        for (int e = 0; e < 4; ++e) v[e] = (uint32_t)tileI[base + e + (p + e >= W ? ts - W : 0)];
       }
+      if constexpr (ADD) res = TK_ABL(32768) ? 0x01010101u : resw[min(gi, total - 1)];
+    };
+    v4u vn;
+    EpiRow ran, rbn;
+    uint32_t resn = 0;
+    int basen = r0 * ts + kk * W + p0;
+    load(r0, basen, p0, tid, vn, ran, rbn, resn);
+    for (int gi = tid; gi < total; gi += kGemmThreads) {
+      const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0 + r0) * hw + c0 + p0);
+      const int base = basen, pc = p0;
+      v4u v = vn;
+      const EpiRow ra = ran, rb = rbn;
+      const uint32_t res = resn;
+      // next group: 1024 elements on
+      r0 += dr;
+      p0 += dp;
+      if (p0 >= W) p0 -= W, ++r0;
+      while (r0 >= R) r0 -= R, ++kk;
+      basen = r0 * ts + kk * W + p0;
+      if (gi + kGemmThreads < total) load(r0, basen, p0, gi + kGemmThreads, vn, ran, rbn, resn);
       uint32_t fold[4], zp[4];
       int32_t bias[4], m[4], sh[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const bool nx = !ROWU && p0 + e >= W;
+        const bool nx = !ROWU && pc + e >= W;
         fold[e] = nx ? rb.fold : ra.fold;
         bias[e] = nx ? rb.bias : ra.bias;
         zp[e] = nx ? (uint32_t)rb.zp : (uint32_t)ra.zp;
@@ -304,10 +334,10 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += fold[e];
-      if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, kAuxNT);
+      if (!TK_ABL(2)) st128(v, r_conv, o * 4u);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += (uint32_t)bias[e];
-      if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, kAuxNT);
+      if (!TK_ABL(2)) st128(v, r_bias, o * 4u);
       int32_t q[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -322,33 +352,27 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
         }
         q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
       }
-      if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, kAuxNT);
+      if (!TK_ABL(2)) st32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o);
       if constexpr (ADD) {
         // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
-        const uint32_t res = TK_ABL(32768) ? 0x01010101u : resw[gi];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           q[e] = clamp_i32(TK_ABL(8192) ? q[e] + (int32_t)((res >> (8 * e)) & 0xFFu) - add_zp
                                         : lut[q[e] & 0xFF] + lut[256 + ((res >> (8 * e)) & 0xFFu)] - add_zp,
                            qmin, qmax);
-        if (!TK_ABL(16384 | 2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, kAuxNT);
+        if (!TK_ABL(16384 | 2)) st32(pack4u(q[0], q[1], q[2], q[3]), r_add, o);
       }
       if constexpr (CLIP) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
-        if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, kAuxNT);
+        if (!TK_ABL(2)) st32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o);
       }
       if constexpr (ROWU) {
         *reinterpret_cast<v4i*>(tileI + base) = v4i{q[0], q[1], q[2], q[3]};
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) tileI[base + e + (p0 + e >= W ? ts - W : 0)] = q[e];
+        for (int e = 0; e < 4; ++e) tileI[base + e + (pc + e >= W ? ts - W : 0)] = q[e];
       }
-      // next group: 1024 elements on
-      r0 += dr;
-      p0 += dp;
-      if (p0 >= W) p0 -= W, ++r0;
-      while (r0 >= R) r0 -= R, ++kk;
     }
   };
   using T = std::true_type;
@@ -377,6 +401,10 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     lds_barrier();  // (also publishes s_fast and the row constants)
+#ifdef TK_ABLATION_BUILD
+    if (h.skew && (wave & 1))
+      for (int k = 0; k < h.skew; ++k) __builtin_amdgcn_s_sleep(1);
+#endif
     if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) by_add(T{});
     else by_add(F{});
 
@@ -515,6 +543,7 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   x.pstep = (int32_t)pstep;
   x.npass = npass;
   x.cw = cw;
+  x.skew = env_int("TK_IMG_SKEW", 0);
   x.tstride = npass > 1 ? cw + 4 : nct * 32 + 4;
   // ring depth: every slot the LDS budget holds (up to 8, no more than the stages need), at least
   // 3 where there are more than 2 stages and one workgroup per CU.  The budget is the CU's 160 KB, or half of it for two

@@ -25,6 +25,7 @@ SHAPES = [  # name, C, H, O, K, stride, pad
     ("1x1 512->2048 7", 512, 7, 2048, 1, 1, 0),
     ("1x1 2048->512 7", 2048, 7, 512, 1, 1, 0),
     # expand layers with the fused residual join (qnn.add -> clip), as in every bottleneck
+    ("1x1 128->512 28", 128, 28, 512, 1, 1, 0),
     ("res 1x1 64->256 56", 64, 56, 256, 1, 1, 0),
     ("res 1x1 128->512 28", 128, 28, 512, 1, 1, 0),
     ("res 1x1 256->1024 14", 256, 14, 1024, 1, 1, 0),

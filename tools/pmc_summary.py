@@ -34,14 +34,28 @@ def load(d):
     return per, meta
 
 
+def step_period(names, lo=8):
+    """Block-kernel dispatches per step: the smallest p >= lo whose last two p-long runs of kernel
+    names are equal (the module's find step launches candidate kernels before the steps, so the
+    dispatch count is not a multiple of the step)."""
+    for p in range(lo, len(names) // 2 + 1):
+        if names[-p:] == names[-2 * p:-p]:
+            return p
+    return None
+
+
 def summarise(d, launches=None, runs=None):
-    """launches: block-kernel dispatches per step; or runs: how many steps the traced command
-    executed (launches = dispatches per pass / runs)."""
+    """launches: block-kernel dispatches per step (default: the period of the dispatch sequence,
+    step_period); runs: only used when no period is found (launches = dispatches / runs)."""
     per, meta = load(d)
     passes = sorted({k[0] for k in per})
     if launches is None:
-        counts = {p: sum(1 for k in per if k[0] == p) for p in passes}
-        launches = min(counts.values()) // runs
+        p0 = passes[0]
+        names = [meta[k]["kernel"] for k in sorted(k for k in per if k[0] == p0)]
+        launches = step_period(names)
+        if launches is None:
+            counts = {p: sum(1 for k in per if k[0] == p) for p in passes}
+            launches = min(counts.values()) // runs
     steps = defaultdict(dict)
     for p in passes:
         keys = sorted(k for k in per if k[0] == p)[-launches:]

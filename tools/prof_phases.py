@@ -20,8 +20,17 @@ from collections import defaultdict
 def main(d, runs=18):
     path = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    gemm = [r for r in rows if "gemm_i8_kernel" in r["Kernel_Name"]]
-    launches = len(gemm) // runs
+    fams = ("gemm_i8_kernel", "conv_img_kernel", "direct_conv_kernel")
+    gemm = [r for r in rows if any(f in r["Kernel_Name"] for f in fams)]
+    # launches per step = the period of the kernel-name sequence (the module's find step launches
+    # candidate kernels first: drop everything before the first whole period from the end)
+    names = [r["Kernel_Name"] for r in gemm]
+    launches = next((p for p in range(8, len(names) // 2 + 1) if names[-p:] == names[-2 * p:-p]), len(gemm) // runs)
+    n_steps = 1
+    while (n_steps + 1) * launches <= len(names) and \
+            names[-(n_steps + 1) * launches:-n_steps * launches] == names[-launches:]:
+        n_steps += 1
+    gemm = gemm[len(gemm) - n_steps * launches:]
     copies = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if "copyBuffer" in r["Kernel_Name"]]
     phases = defaultdict(lambda: defaultdict(list))
     steps = defaultdict(int)
