@@ -60,6 +60,11 @@ def parse(argv=None):
     p.add_argument("--out-dir", default="/tmp")
     p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
     p.add_argument("--tune-report", default=None, help="write the find step's per-node kernel timings (JSON) here")
+    p.add_argument("--no-graph", action="store_true",
+                   help="issue every kernel and copy from the host each step (tk_module_run) instead of "
+                        "replaying one HIP graph per step (tk_module_run_graph)")
+    p.add_argument("--graph-memcpy", action="store_true",
+                   help="graph runs copy records with memcpy nodes instead of copy kernels")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse N>1 on one GPU")
     p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
@@ -297,6 +302,9 @@ def main(argv=None) -> int:
          f"(numa node {placement['numa_node']}, {placement['cpus']} cpus)")
     lib = relay.build(model.mod, target="mi355x", params=model.params)
     m = graph_executor.GraphModule(lib["default"](device.index))
+    m.module.use_graph = not args.no_graph
+    if args.graph_memcpy:
+        _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, 0), "tk_module_set_graph_copies")
     # the module's find step (tk_module_tune) picked each conv block's kernel on this GPU
     tuning = m.module.tuning
     if args.tune_report and rank == 0:
@@ -616,6 +624,8 @@ def main(argv=None) -> int:
                 "compute_only_traces_per_s": round(B * world / (compute_ms * 1e-3), 1),
                 "compute_step_device_ms": round(total_ms, 3),
                 "block_segments": len(blk_segs),
+                "run_mode": "hip graph per step (tk_module_run_graph)" if m.module.use_graph else
+                            "host-issued kernels and copies (tk_module_run)",
                 "find_step": {"tuned_nodes": len(tuning),
                               "image_tile_nodes": sum(1 for t in tuning if t["algo"] >= 16),
                               "im2col_nodes": sum(1 for t in tuning if t["algo"] == 1),

@@ -413,6 +413,18 @@ int tk_module_num_nodes(const tk_module* mod);
  * (the call returns as soon as the work is enqueued, like GraphExecutor::Run on an
  * asynchronous device). */
 int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst);
+/* tk_module_run as one HIP graph: the first call captures the node loop (and the copies, forked
+ * onto capture_stream and joined back) into a graph and instantiates it; later calls with the
+ * same streams and host destinations replay it with a single launch on `stream`, so a run costs
+ * one host API call instead of one per kernel and copy (the host side of a traced step no longer
+ * depends on how fast the host issues ~300 calls).  Anything already queued on capture_stream
+ * runs first, and capture_stream waits for the launch, so the copies are complete for anything
+ * queued on it afterwards (as with tk_module_run).  Up to four graphs (streams / destinations)
+ * are kept; tk_module_tune drops them; profiling mode runs tk_module_run. */
+int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst);
+/* How tk_module_run_graph copies records to host memory: 1 (default) one copy kernel per node
+ * (kernel nodes writing pinned memory with 16-byte stores), 0 one memcpy node per record. */
+int tk_module_set_graph_copies(tk_module* mod, int copy_kernels);
 /* Makes `stream` wait for the copies of the last traced run: call before writing any
  * tensor the module reads (GraphModule.set_input / load_params,
  * graph_executor.cc:158-166 SetInput) on a stream of your own. */

@@ -275,6 +275,8 @@ SIGNATURES = {
     "tk_module_run_profiled": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_F32)]),
     "tk_module_set_profiling": (ctypes.c_int, [_VP, ctypes.c_int]),
     "tk_module_node_times": (ctypes.c_int, [_VP, ctypes.POINTER(_F32)]),
+    "tk_module_run_graph": (ctypes.c_int, [_VP, _VP, _VP, ctypes.POINTER(_VP)]),
+    "tk_module_set_graph_copies": (ctypes.c_int, [_VP, ctypes.c_int]),
     "tk_module_tune": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
                                       ctypes.POINTER(_F32)]),
     "tk_conv2d_block_algos": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_block_attrs), ctypes.POINTER(ctypes.c_int32),

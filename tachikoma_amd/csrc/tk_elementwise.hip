@@ -560,6 +560,67 @@ int copy_impl(const tk_tensor* x, tk_tensor* y, hipStream_t s) {
   return TK_OK;
 }
 
+// ---------------------------------------------------------------- records to host memory
+// One launch copies up to kHostCopyMax device buffers into pinned host memory (a node's trace
+// records; tk_module_run_graph's copies).  Host destinations are 8-byte aligned (NDArray-list
+// payloads); each buffer is copied as an 8-byte head (to reach 16-byte destination alignment),
+// 16-byte nontemporal stores from two 8-byte loads, and a byte tail.  64-128 workgroups of such a
+// kernel write pinned memory at ~55 GB/s (profiles/r03b_probe_d2h.jsonl, kernel_wg128), about the
+// SDMA engines' rate, and as a graph kernel node it needs no per-copy host call.
+constexpr int kHostCopyMax = 6;
+struct HostCopies {
+  const uint8_t* src[kHostCopyMax];
+  uint8_t* dst[kHostCopyMax];
+  int64_t bytes[kHostCopyMax];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void host_copy_kernel(HostCopies c) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int b = 0; b < c.n; ++b) {
+    const uint8_t* src = c.src[b];
+    uint8_t* dst = c.dst[b];
+    int64_t n = c.bytes[b];
+    const int64_t head = (int64_t)((16 - ((uintptr_t)dst & 15)) & 15) < n ? (int64_t)((16 - ((uintptr_t)dst & 15)) & 15) : n;
+    for (int64_t i = t; i < head; i += stride) dst[i] = src[i];
+    const int64_t n16 = (n - head) / 16;
+    const uint64_t* s8 = reinterpret_cast<const uint64_t*>(src + head);
+    tk_v4i* d16 = reinterpret_cast<tk_v4i*>(dst + head);
+    if (((uintptr_t)(src + head) & 7) == 0) {
+      for (int64_t i = t; i < n16; i += stride) {
+        const uint64_t a = __builtin_nontemporal_load(s8 + 2 * i), bb = __builtin_nontemporal_load(s8 + 2 * i + 1);
+        __builtin_nontemporal_store(tk_v4i{(int)(uint32_t)a, (int)(uint32_t)(a >> 32), (int)(uint32_t)bb, (int)(uint32_t)(bb >> 32)},
+                                    d16 + i);
+      }
+    } else {
+      for (int64_t i = t; i < n16 * 16; i += stride) dst[head + i] = src[head + i];
+    }
+    for (int64_t i = head + n16 * 16 + t; i < n; i += stride) dst[i] = src[i];
+  }
+}
+
+int host_copy_impl(const void* const* src, void* const* dst, const int64_t* bytes, int n, hipStream_t s) {
+  TK_CHECK_ARG(n >= 0 && n <= kHostCopyMax, "host copy: too many buffers");
+  HostCopies c{};
+  int64_t total = 0;
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!dst[i] || bytes[i] <= 0) continue;
+    c.src[k] = (const uint8_t*)src[i];
+    c.dst[k] = (uint8_t*)dst[i];
+    c.bytes[k] = bytes[i];
+    total += bytes[i];
+    ++k;
+  }
+  c.n = k;
+  if (!k) return TK_OK;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(128, (total / 16 + 255) / 256));
+  hipLaunchKernelGGL(host_copy_kernel, dim3(grid), dim3(256), 0, s, c);
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
 // ---------------------------------------------------------------- nn.pad
 // One thread per output element (its index decomposed over up to 6 dimensions, innermost first):
 // inside the data's range it copies data[i - before], else writes the pad value.

@@ -33,6 +33,7 @@ int pad_impl(const tk_tensor* x, tk_tensor* y, const tk_pad_attrs* a, hipStream_
 int postops_impl(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* y, const tk_postops_attrs* a,
                  hipStream_t s);
 int digest_impl(const void* data, int64_t nbytes, uint64_t* out, hipStream_t s);
+int host_copy_impl(const void* const* src, void* const* dst, const int64_t* bytes, int n, hipStream_t s);
 int ewise_impl(const tk_tensor* x, const tk_tensor* r, tk_tensor* y, const tk_ewise_attrs* a, hipStream_t s);
 int conv2d_f32_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, const tk_conv2d_attrs* a, hipStream_t s);
 int dense_f32_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, hipStream_t s);
@@ -157,10 +158,37 @@ struct tk_module {
   bool capture_recorded = false;
   bool profiling = false;
   bool have_times = false;
+  // tk_module_run_graph: the whole run (every node, and the copies when capturing) as one HIP
+  // graph per (stream, capture stream, host destinations), instantiated once and replayed; a few
+  // are kept (a file sink alternates two trace images)
+  struct Graph {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    hipStream_t s = nullptr, cs = nullptr;
+    std::vector<void*> dst;
+  };
+  std::vector<Graph> graphs;
+  hipEvent_t graph_join = nullptr, graph_pre = nullptr;
+  // the graphs are captured on two streams of the module's own (the caller's may be the legacy
+  // default stream, which cannot capture) and launched on the caller's
+  hipStream_t cap_s = nullptr, cap_cs = nullptr;
+  bool graph_copy_kernels = true;  // graph copies as copy kernels (else memcpy nodes)
+  void drop_graph() {
+    for (Graph& x : graphs) {
+      if (x.ge) (void)hipGraphExecDestroy(x.ge);
+      if (x.g) (void)hipGraphDestroy(x.g);
+    }
+    graphs.clear();
+  }
   ~tk_module() {
+    drop_graph();
     for (auto e : done) (void)hipEventDestroy(e);
     for (auto e : prof) (void)hipEventDestroy(e);
     if (capture_done) (void)hipEventDestroy(capture_done);
+    if (graph_join) (void)hipEventDestroy(graph_join);
+    if (graph_pre) (void)hipEventDestroy(graph_pre);
+    if (cap_s) (void)hipStreamDestroy(cap_s);
+    if (cap_cs) (void)hipStreamDestroy(cap_cs);
   }
 };
 
@@ -379,6 +407,44 @@ int tk_module_node_times(tk_module* mod, float* node_ms) {
   return TK_OK;
 }
 
+// Enqueues every node on s and, when capturing, node i's output copies on cs gated by an event
+// recorded after node i (shared by tk_module_run and the graph capture of tk_module_run_graph).
+static int enqueue_nodes(tk_module* mod, hipStream_t s, hipStream_t cs, void* const* host_dst, bool capture,
+                         bool profiling, bool copy_kernels = false) {
+  if (profiling) TK_HIP(hipEventRecord(mod->prof[0], s));
+  for (size_t i = 0; i < mod->nodes.size(); ++i) {
+    tk::Node& n = mod->nodes[i];
+    int rc = tk::run_node(n, s);
+    if (rc) {
+      tk::set_error("node " + std::to_string(i) + ": " + tk_last_error());
+      return rc;
+    }
+    if (profiling) TK_HIP(hipEventRecord(mod->prof[i + 1], s));
+    if (capture && n.desc.n_outputs > 0) {
+      void* const* dst = host_dst + i * TK_MAX_NODE_OUTPUTS;
+      bool any = false;
+      for (int k = 0; k < n.desc.n_outputs; ++k) any |= dst[k] != nullptr;
+      if (any) {
+        TK_HIP(hipEventRecord(mod->done[i], s));
+        TK_HIP(hipStreamWaitEvent(cs, mod->done[i], 0));
+        if (copy_kernels) {
+          // one copy kernel for the node's records (graph runs: a kernel node, no host call)
+          const void* src[TK_MAX_NODE_OUTPUTS];
+          int64_t nb[TK_MAX_NODE_OUTPUTS];
+          for (int k = 0; k < n.desc.n_outputs; ++k) src[k] = tk::ptr(&n.out[k].t), nb[k] = tk::nbytes(&n.out[k].t);
+          int rc = tk::host_copy_impl(src, dst, nb, n.desc.n_outputs, cs);
+          if (rc) return rc;
+        } else {
+          for (int k = 0; k < n.desc.n_outputs; ++k)
+            if (dst[k])
+              TK_HIP(hipMemcpyAsync(dst[k], tk::ptr(&n.out[k].t), tk::nbytes(&n.out[k].t), hipMemcpyDeviceToHost, cs));
+        }
+      }
+    }
+  }
+  return TK_OK;
+}
+
 int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst) {
   if (!mod) {
     tk::set_error("tk_module_run: null module");
@@ -389,34 +455,109 @@ int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* cons
   bool capture = capture_stream && host_dst;
   int rc0 = wait_capture(mod, s);
   if (rc0) return rc0;
-  if (mod->profiling) TK_HIP(hipEventRecord(mod->prof[0], s));
-  for (size_t i = 0; i < mod->nodes.size(); ++i) {
-    tk::Node& n = mod->nodes[i];
-    int rc = tk::run_node(n, s);
-    if (rc) {
-      tk::set_error("node " + std::to_string(i) + ": " + tk_last_error());
-      return rc;
-    }
-    if (mod->profiling) TK_HIP(hipEventRecord(mod->prof[i + 1], s));
-    if (capture && n.desc.n_outputs > 0) {
-      void* const* dst = host_dst + i * TK_MAX_NODE_OUTPUTS;
-      bool any = false;
-      for (int k = 0; k < n.desc.n_outputs; ++k) any |= dst[k] != nullptr;
-      if (any) {
-        TK_HIP(hipEventRecord(mod->done[i], s));
-        TK_HIP(hipStreamWaitEvent(cs, mod->done[i], 0));
-        for (int k = 0; k < n.desc.n_outputs; ++k)
-          if (dst[k])
-            TK_HIP(hipMemcpyAsync(dst[k], tk::ptr(&n.out[k].t), tk::nbytes(&n.out[k].t), hipMemcpyDeviceToHost, cs));
-      }
-    }
-  }
+  rc0 = enqueue_nodes(mod, s, cs, host_dst, capture, mod->profiling);
+  if (rc0) return rc0;
   if (capture) {
     // the next run / input write waits for these copies (wait_capture)
     TK_HIP(hipEventRecord(mod->capture_done, cs));
     mod->capture_recorded = true;
   }
   mod->have_times = mod->profiling;
+  return TK_OK;
+}
+
+int tk_module_set_graph_copies(tk_module* mod, int copy_kernels) {
+  if (!mod) {
+    tk::set_error("tk_module_set_graph_copies: null module");
+    return TK_ERR_INVALID_ARG;
+  }
+  if (mod->graph_copy_kernels != (copy_kernels != 0)) mod->drop_graph();
+  mod->graph_copy_kernels = copy_kernels != 0;
+  return TK_OK;
+}
+
+int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst) {
+  if (!mod) {
+    tk::set_error("tk_module_run_graph: null module");
+    return TK_ERR_INVALID_ARG;
+  }
+  if (mod->profiling) return tk_module_run(mod, stream, capture_stream, host_dst);  // per-node events
+  hipStream_t s = tk::as_stream(stream);
+  hipStream_t cs = tk::as_stream(capture_stream);
+  const bool capture = capture_stream && host_dst;
+  const size_t nd = capture ? mod->nodes.size() * TK_MAX_NODE_OUTPUTS : 0;
+  std::vector<void*> dst(nd);
+  for (size_t i = 0; i < nd; ++i) dst[i] = host_dst[i];
+  int gi = -1;
+  for (size_t i = 0; i < mod->graphs.size(); ++i)
+    if (mod->graphs[i].dst == dst && (mod->graphs[i].cs != nullptr) == capture) gi = (int)i;
+  int rc0 = wait_capture(mod, s);
+  if (rc0) return rc0;
+  if (gi < 0) {
+    if (mod->graphs.size() >= 4) {  // keep the newest few
+      tk_module::Graph& old = mod->graphs.front();
+      if (old.ge) (void)hipGraphExecDestroy(old.ge);
+      if (old.g) (void)hipGraphDestroy(old.g);
+      mod->graphs.erase(mod->graphs.begin());
+    }
+    if (!mod->graph_join) TK_HIP(hipEventCreateWithFlags(&mod->graph_join, hipEventDisableTiming));
+    if (!mod->cap_s) TK_HIP(hipStreamCreateWithFlags(&mod->cap_s, hipStreamNonBlocking));
+    if (!mod->cap_cs) TK_HIP(hipStreamCreateWithFlags(&mod->cap_cs, hipStreamNonBlocking));
+    hipStream_t qs = mod->cap_s, qcs = mod->cap_cs;
+    // capture: the node loop on qs, the copies forked onto qcs through the per-node events and
+    // joined back into qs at the end, so that one launch covers the run and its copies
+    TK_HIP(hipStreamBeginCapture(qs, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_nodes(mod, qs, qcs, host_dst, capture, false, mod->graph_copy_kernels);
+    if (rc == TK_OK && capture) {
+      if (hipEventRecord(mod->graph_join, qcs) != hipSuccess || hipStreamWaitEvent(qs, mod->graph_join, 0) != hipSuccess) {
+        tk::set_error("tk_module_run_graph: joining the capture stream failed");
+        rc = TK_ERR_HIP;
+      }
+    }
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(qs, &g);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    if (e != hipSuccess || !g) {
+      (void)hipGetLastError();
+      tk::set_error(std::string("tk_module_run_graph: stream capture failed: ") + hipGetErrorString(e));
+      return TK_ERR_HIP;
+    }
+    hipGraphExec_t ge = nullptr;
+    e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+      (void)hipGraphDestroy(g);
+      tk::set_error(std::string("tk_module_run_graph: instantiate failed: ") + hipGetErrorString(e));
+      return TK_ERR_HIP;
+    }
+    tk_module::Graph x;
+    x.g = g;
+    x.ge = ge;
+    x.s = qs;
+    x.cs = capture ? qcs : nullptr;
+    x.dst = std::move(dst);
+    mod->graphs.push_back(std::move(x));
+    gi = (int)mod->graphs.size() - 1;
+  }
+  if (capture) {
+    // whatever the caller queued on the capture stream before this run (the graph-input copies)
+    // completes before the launch, so that capture_done covers it as in tk_module_run
+    if (!mod->graph_pre) TK_HIP(hipEventCreateWithFlags(&mod->graph_pre, hipEventDisableTiming));
+    TK_HIP(hipEventRecord(mod->graph_pre, cs));
+    TK_HIP(hipStreamWaitEvent(s, mod->graph_pre, 0));
+  }
+  TK_HIP(hipGraphLaunch(mod->graphs[gi].ge, s));
+  if (capture) {
+    // the next run / input write waits for this run's copies (they are part of the launch on s),
+    // and so does the capture stream: as after tk_module_run, work queued on it later (or its
+    // synchronisation) sees the copies complete
+    TK_HIP(hipEventRecord(mod->capture_done, s));
+    mod->capture_recorded = true;
+    TK_HIP(hipStreamWaitEvent(cs, mod->capture_done, 0));
+  }
+  mod->have_times = false;
   return TK_OK;
 }
 
@@ -492,6 +633,7 @@ int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, i
     return TK_ERR_INVALID_ARG;
   }
   hipStream_t s = tk::as_stream(stream);
+  mod->drop_graph();  // the kernels it captured may change
   const int W = max_candidates + 1;
   const size_t n = mod->nodes.size();
   if (algo_out)

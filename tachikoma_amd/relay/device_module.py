@@ -54,6 +54,7 @@ class DeviceModule:
         self._derived: Dict[str, List[Callable[[int], None]]] = {}
         self.groups = exec_groups(plan, fuse=fuse)
         self.tuning: List[dict] = []
+        self.use_graph = True  # runs replay one HIP graph (tk_module_run_graph)
         with torch.cuda.device(self.device):
             self._alloc(params)
             self._build_nodes()
@@ -508,13 +509,17 @@ class DeviceModule:
         return arr
 
     def run(self, stream=None, capture_stream=None, host_dst=None) -> None:
+        """One run of every node on ``stream`` (+ the record copies on ``capture_stream`` into
+        ``host_dst``).  With ``use_graph`` (default) the run is one replayed HIP graph
+        (tk_module_run_graph): the copies then execute inside the launch on ``stream``."""
         s = _lib.stream_handle(stream)
+        fn = self.lib.tk_module_run_graph if self.use_graph else self.lib.tk_module_run
+        what = "tk_module_run_graph" if self.use_graph else "tk_module_run"
         if host_dst is not None:
-            _lib.check(self.lib.tk_module_run(self.handle, ctypes.c_void_p(s),
-                                              ctypes.c_void_p(_lib.stream_handle(capture_stream)), host_dst),
-                       "tk_module_run")
+            _lib.check(fn(self.handle, ctypes.c_void_p(s), ctypes.c_void_p(_lib.stream_handle(capture_stream)),
+                          host_dst), what)
         else:
-            _lib.check(self.lib.tk_module_run(self.handle, ctypes.c_void_p(s), None, None), "tk_module_run")
+            _lib.check(fn(self.handle, ctypes.c_void_p(s), None, None), what)
 
     def run_range(self, begin: int, end: int, stream=None) -> None:
         """Nodes [begin, end) only, on ``stream`` (tk_module_run_range; no capture)."""

@@ -59,6 +59,39 @@ def test_traced_run_then_immediate_rewrite(device):
     np.testing.assert_array_equal(out[[3]], exp_b[m.plan.outputs[0]])
 
 
+def test_graph_replay_equals_plain_run(device):
+    """tk_module_run_graph (one replayed HIP graph per run, the default) and tk_module_run give
+    the same trace image byte for byte; the graph is re-used across runs with new inputs and a
+    second pinned image (a second graph) holds its own run."""
+    import torch
+    model = zoo.lenet5(batch=8)
+    lib = relay.build(model.mod, target="mi355x", params=model.params)
+    m = graph_executor.GraphModule(lib["default"]())
+    xs = [model.sample_inputs(8 * i, 8) for i in range(3)]
+    images = []
+    for use_graph in (False, True):
+        m.module.use_graph = use_graph
+        for x in xs:
+            m.set_input("data", x)
+            m.run(trace=True)
+            m.trace_capture().synchronize()
+            images.append(bytes(m.trace_capture().bytes()))
+    assert images[:3] == images[3:]
+    assert images[0] != images[1]
+    # a second image: its own graph; both images hold their own run
+    cap2 = graph_executor.TraceCapture(m.module, m._meta)
+    stream = torch.cuda.current_stream()
+    m.set_input("data", xs[0])
+    cap2.capture_inputs(stream)
+    m.module.run(stream, cap2.capture_stream, cap2.host_dst)
+    m.set_input("data", xs[2])
+    m.run(trace=True)
+    cap2.synchronize()
+    m.trace_capture().synchronize()
+    assert bytes(cap2.bytes()) == images[0]
+    assert bytes(m.trace_capture().bytes()) == images[2]
+
+
 def _reversed(params):
     """Same shapes, dtypes and value ranges, different values: each array reversed along axis 0."""
     return {k: np.ascontiguousarray(np.asarray(v)[::-1]) for k, v in params.items()}
