@@ -60,11 +60,12 @@ def parse(argv=None):
     p.add_argument("--out-dir", default="/tmp")
     p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
     p.add_argument("--tune-report", default=None, help="write the find step's per-node kernel timings (JSON) here")
-    p.add_argument("--no-graph", action="store_true",
-                   help="issue every kernel and copy from the host each step (tk_module_run) instead of "
-                        "replaying one HIP graph per step (tk_module_run_graph)")
-    p.add_argument("--graph-memcpy", action="store_true",
-                   help="graph runs copy records with memcpy nodes instead of copy kernels")
+    p.add_argument("--run-mode", choices=["auto", "graph", "host"], default="auto",
+                   help="traced-step submission: one replayed HIP graph (tk_module_run_graph), every kernel "
+                        "and copy issued from the host (tk_module_run), or auto = the faster of the two "
+                        "timed on this host before the warm-up (GraphModule.pick_run_mode)")
+    p.add_argument("--graph-copy-kernels", action="store_true",
+                   help="graph runs copy records with copy kernels instead of memcpy nodes")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse N>1 on one GPU")
     p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
@@ -302,9 +303,9 @@ def main(argv=None) -> int:
          f"(numa node {placement['numa_node']}, {placement['cpus']} cpus)")
     lib = relay.build(model.mod, target="mi355x", params=model.params)
     m = graph_executor.GraphModule(lib["default"](device.index))
-    m.module.use_graph = not args.no_graph
-    if args.graph_memcpy:
-        _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, 0), "tk_module_set_graph_copies")
+    m.module.use_graph = args.run_mode == "graph"
+    if args.graph_copy_kernels:
+        _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, 1), "tk_module_set_graph_copies")
     # the module's find step (tk_module_tune) picked each conv block's kernel on this GPU
     tuning = m.module.tuning
     if args.tune_report and rank == 0:
@@ -370,6 +371,11 @@ def main(argv=None) -> int:
         if world > 1:
             dist.barrier()
 
+    # submission find step (untimed): host-issued vs one replayed HIP graph per traced step
+    mode_pick = None
+    if args.run_mode == "auto" and not args.no_trace:
+        mode_pick = m.pick_run_mode(steps=2)
+        torch.cuda.synchronize(device)
     for i in range(args.warmup):
         step(i)
     drain()
@@ -626,6 +632,7 @@ def main(argv=None) -> int:
                 "block_segments": len(blk_segs),
                 "run_mode": "hip graph per step (tk_module_run_graph)" if m.module.use_graph else
                             "host-issued kernels and copies (tk_module_run)",
+                "run_mode_pick": mode_pick,
                 "find_step": {"tuned_nodes": len(tuning),
                               "image_tile_nodes": sum(1 for t in tuning if t["algo"] >= 16),
                               "im2col_nodes": sum(1 for t in tuning if t["algo"] == 1),

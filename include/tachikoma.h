@@ -422,8 +422,9 @@ int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* cons
  * queued on it afterwards (as with tk_module_run).  Up to four graphs (streams / destinations)
  * are kept; tk_module_tune drops them; profiling mode runs tk_module_run. */
 int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst);
-/* How tk_module_run_graph copies records to host memory: 1 (default) one copy kernel per node
- * (kernel nodes writing pinned memory with 16-byte stores), 0 one memcpy node per record. */
+/* How tk_module_run_graph copies records to host memory: 0 (default) one memcpy node per record,
+ * 1 one copy kernel per node (kernel nodes writing pinned memory with 16-byte stores; measured
+ * slower on ResNet-50 traces). */
 int tk_module_set_graph_copies(tk_module* mod, int copy_kernels);
 /* Makes `stream` wait for the copies of the last traced run: call before writing any
  * tensor the module reads (GraphModule.set_input / load_params,

@@ -148,6 +148,31 @@ class GraphModule:
         else:
             self.module.run(stream)
 
+    def pick_run_mode(self, steps: int = 2) -> Dict[str, Any]:
+        """Submission find step for traced runs on this host: times ``steps`` traced runs issued
+        node by node from the host (tk_module_run) and as one replayed HIP graph
+        (tk_module_run_graph), and keeps the faster.  On a healthy host the host-issued copies
+        reach the SDMA rate and win by ~5 % (profiles/r03n_run_modes.txt); on a host that issues
+        the ~300 calls of a step slowly, the graph's single launch does.  Results are identical
+        either way."""
+        import time
+        import torch
+        times = {}
+        for use_graph in (False, True):
+            self.module.use_graph = use_graph
+            self.run(trace=True)  # warm-up (a graph run captures and instantiates here)
+            self.trace_capture().synchronize()
+            torch.cuda.synchronize(self.module.device)
+            t0 = time.perf_counter()
+            for _ in range(max(1, steps)):
+                self.run(trace=True)
+            self.trace_capture().synchronize()
+            torch.cuda.synchronize(self.module.device)
+            times[use_graph] = (time.perf_counter() - t0) / max(1, steps)
+        self.module.use_graph = times[True] < times[False]
+        return {"host_issued_ms": round(times[False] * 1e3, 2), "graph_ms": round(times[True] * 1e3, 2),
+                "chosen": "graph" if self.module.use_graph else "host-issued"}
+
     def get_num_outputs(self) -> int:
         return len(self.plan.outputs)
 

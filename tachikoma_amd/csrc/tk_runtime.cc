@@ -172,7 +172,9 @@ struct tk_module {
   // the graphs are captured on two streams of the module's own (the caller's may be the legacy
   // default stream, which cannot capture) and launched on the caller's
   hipStream_t cap_s = nullptr, cap_cs = nullptr;
-  bool graph_copy_kernels = true;  // graph copies as copy kernels (else memcpy nodes)
+  // graph copies as copy kernels instead of memcpy nodes: measured slower (41.7 vs 52.7 GB/s per
+  // traced ResNet-50 step, profiles/r03n_run_modes.txt), so off by default
+  bool graph_copy_kernels = false;
   void drop_graph() {
     for (Graph& x : graphs) {
       if (x.ge) (void)hipGraphExecDestroy(x.ge);

@@ -54,7 +54,9 @@ class DeviceModule:
         self._derived: Dict[str, List[Callable[[int], None]]] = {}
         self.groups = exec_groups(plan, fuse=fuse)
         self.tuning: List[dict] = []
-        self.use_graph = True  # runs replay one HIP graph (tk_module_run_graph)
+        # runs as one replayed HIP graph (tk_module_run_graph) instead of host-issued nodes and
+        # copies; GraphModule.pick_run_mode chooses by timing both on this host
+        self.use_graph = False
         with torch.cuda.device(self.device):
             self._alloc(params)
             self._build_nodes()
@@ -510,7 +512,7 @@ class DeviceModule:
 
     def run(self, stream=None, capture_stream=None, host_dst=None) -> None:
         """One run of every node on ``stream`` (+ the record copies on ``capture_stream`` into
-        ``host_dst``).  With ``use_graph`` (default) the run is one replayed HIP graph
+        ``host_dst``).  With ``use_graph`` the run is one replayed HIP graph
         (tk_module_run_graph): the copies then execute inside the launch on ``stream``."""
         s = _lib.stream_handle(stream)
         fn = self.lib.tk_module_run_graph if self.use_graph else self.lib.tk_module_run

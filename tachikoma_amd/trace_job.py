@@ -207,6 +207,8 @@ class GraphModuleTracer:
         if n not in self.modules:
             from .contrib.graph_executor import TraceCapture
             m = self.build_module(n)
+            # host-issued vs replayed-graph traced runs: the faster on this host (before any chunk)
+            self.run_mode = m.pick_run_mode(steps=1)
             caps = [m.trace_capture(), TraceCapture(m.module, m._meta)]
             self.modules[n] = [m, caps, 0]
         return self.modules[n]
