@@ -82,7 +82,7 @@ struct GemmArgs {
                        // 131072 flat epilogue without the lean row-crossing groups (hw % 4 != 0),
                        // 8192 residual join without the LUTs, 16384 skip the add record,
                        // (image-tile kernel: 32768 residual words not read from LDS, 65536 residual
-                       // words not loaded),
+                       // words not loaded, 262144 records stored with no epilogue arithmetic),
                        // 8/16/32/64 skip the conv / bias_add / requantize / clip record,
                        // 128/256 skip the A / B LDS-DMA loads, 512 skip the MFMAs, 1024 main-loop
                        // barrier without the lgkmcnt(0) drain, 2048 skip the fragment reads, 4096 skip

@@ -52,7 +52,7 @@ struct ImgArgs {
   int32_t runq;                // 4-element epilogue groups per image run and pass (R * cw / 4)
   int32_t npass, cw;           // epilogue passes over the tile's columns (npass > 1: one image per
                                // workgroup, cw = hw / npass pixels per pass), or 1 pass of cw = hw
-  int32_t skew;                // profiling: odd waves start the epilogue walk this many s_sleep units late
+  int32_t skew;                // profiling: first-round workgroups start up to 3 x skew x s_sleep(8) late
 };
 
 // KT: 1 or 3 taps per axis; WM: 32-row wave groups (R = 32 * WM); CT: 32-column tiles per wave
@@ -77,6 +77,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   const int L = blockIdx.x;
   const int w = (L & 7) * (h.wgs8 >> 3) + (L >> 3);
   if (w >= h.wgs) return;
+#ifdef TK_ABLATION_BUILD
+  // profiling: stagger the first round's workgroups ((L >> 3) % 4 quarters of h.skew x s_sleep(8))
+  // so that CUs are in different phases (K loop / epilogue stores)
+  if (h.skew && L < 8 * 256)
+    for (int k = 0; k < ((L >> 3) & 3) * h.skew; ++k) __builtin_amdgcn_s_sleep(8);
+#endif
   const int mt = w % h.mtiles;
   const int img0 = (w / h.mtiles) * h.ipt;
   const int nimg = min(h.ipt, h.nimg - img0);
@@ -332,6 +338,17 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
         m[e] = nx ? rb.m : ra.m;
         sh[e] = nx ? rb.s : ra.s;
       }
+      if (TK_ABL(262144)) {
+        // profiling: every record stored with no epilogue arithmetic (raw accumulators / their low
+        // bytes): the store side of the epilogue alone, at the kernel's own occupancy and order
+        st128(v, r_conv, o * 4u);
+        st128(v, r_bias, o * 4u);
+        const uint32_t b8 = pack4u((int32_t)v[0], (int32_t)v[1], (int32_t)v[2], (int32_t)v[3]);
+        st32(b8, r_rq, o);
+        if constexpr (ADD) st32(b8 ^ res, r_add, o);
+        if constexpr (CLIP) st32(b8, r_clip, o);
+        continue;
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += fold[e];
       if (!TK_ABL(2)) st128(v, r_conv, o * 4u);
@@ -401,10 +418,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     lds_barrier();  // (also publishes s_fast and the row constants)
-#ifdef TK_ABLATION_BUILD
-    if (h.skew && (wave & 1))
-      for (int k = 0; k < h.skew; ++k) __builtin_amdgcn_s_sleep(1);
-#endif
     if (s_fast && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)) by_add(T{});
     else by_add(F{});
 

@@ -947,6 +947,16 @@ gemm_i8_kernel(GemmArgs g) {
           int32_t* slot = tileI + lr * kStr + c4;
           const v4i t = *reinterpret_cast<const v4i*>(slot);
           const uint32_t o = offs[k];
+          if (TK_ABL(262144)) {
+            // profiling: every record stored with no epilogue arithmetic (store side alone)
+            const uint32_t b8 = pack4u(t.x, t.y, t.z, t.w);
+            __builtin_amdgcn_raw_buffer_store_b128(t, r_conv, o * 4u, 0, AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(t, r_bias, o * 4u, 0, AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(b8, r_rq, o, 0, AUX);
+            if constexpr (ADD) __builtin_amdgcn_raw_buffer_store_b32(b8 ^ resid_pre[k], r_add, o, 0, AUX);
+            if constexpr (CLIP) __builtin_amdgcn_raw_buffer_store_b32(b8, r_clip, o, 0, AUX);
+            continue;
+          }
           // int32 wrap-around arithmetic in unsigned lanes (the reference accumulates mod 2^32)
           v4u v = __builtin_bit_cast(v4u, t) + r.fold;
           if (!TK_ABL(2)) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, AUX);
