@@ -60,10 +60,11 @@ def parse(argv=None):
     p.add_argument("--out-dir", default="/tmp")
     p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
     p.add_argument("--tune-report", default=None, help="write the find step's per-node kernel timings (JSON) here")
-    p.add_argument("--run-mode", choices=["auto", "graph", "host"], default="auto",
-                   help="traced-step submission: one replayed HIP graph (tk_module_run_graph), every kernel "
-                        "and copy issued from the host (tk_module_run), or auto = the faster of the two "
-                        "timed on this host before the warm-up (GraphModule.pick_run_mode)")
+    p.add_argument("--run-mode", choices=["graph", "host", "auto"], default="graph",
+                   help="traced-step submission: one replayed HIP graph per step (tk_module_run_graph, the "
+                        "default: immune to a host that issues calls late, profiles/r03r_run_modes_slow_host.txt), "
+                        "every kernel and copy issued from the host (tk_module_run), or auto = the faster of the "
+                        "two over two steps before the warm-up (GraphModule.pick_run_mode)")
     p.add_argument("--graph-copy-kernels", action="store_true",
                    help="graph runs copy records with copy kernels instead of memcpy nodes")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],

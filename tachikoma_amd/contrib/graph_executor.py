@@ -153,8 +153,10 @@ class GraphModule:
         node by node from the host (tk_module_run) and as one replayed HIP graph
         (tk_module_run_graph), and keeps the faster.  On a healthy host the host-issued copies
         reach the SDMA rate and win by ~5 % (profiles/r03n_run_modes.txt); on a host that issues
-        the ~300 calls of a step slowly, the graph's single launch does.  Results are identical
-        either way."""
+        the ~300 calls of a step slowly, the graph's single launch does — but such hosts can be
+        slow only intermittently (profiles/r03r_run_modes_slow_host.txt: 454 vs 186 op-traces/s
+        on one box), which two timed steps may not catch, so bench.py and trace jobs default to the
+        graph.  Results are identical either way."""
         import time
         import torch
         times = {}

@@ -207,8 +207,9 @@ class GraphModuleTracer:
         if n not in self.modules:
             from .contrib.graph_executor import TraceCapture
             m = self.build_module(n)
-            # host-issued vs replayed-graph traced runs: the faster on this host (before any chunk)
-            self.run_mode = m.pick_run_mode(steps=1)
+            # traced runs as one replayed HIP graph: one host call per chunk, so a host that issues
+            # calls late cannot starve the copies (profiles/r03r_run_modes_slow_host.txt)
+            m.module.use_graph = True
             caps = [m.trace_capture(), TraceCapture(m.module, m._meta)]
             self.modules[n] = [m, caps, 0]
         return self.modules[n]

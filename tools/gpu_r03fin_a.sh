@@ -1,6 +1,6 @@
 set -o pipefail
-# round-3 final evidence, part 1: smoke() and the whole -m gpu suite (the driver's commands)
+# round-3 final evidence (at HEAD after the graph / find-step changes), part 1: smoke() and the whole -m gpu suite (the driver's commands)
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r03fin
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03fin/smoke.log 2>&1 &&
-timeout -k 10 1050 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r03fin/gputest.log 2>&1
+mkdir -p gpurun_out/r03fin2
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03fin2/smoke.log 2>&1 &&
+timeout -k 10 1050 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r03fin2/gputest.log 2>&1
