@@ -65,8 +65,9 @@ def parse(argv=None):
                         "default: immune to a host that issues calls late, profiles/r03r_run_modes_slow_host.txt), "
                         "every kernel and copy issued from the host (tk_module_run), or auto = the faster of the "
                         "two over two steps before the warm-up (GraphModule.pick_run_mode)")
-    p.add_argument("--graph-copy-kernels", action="store_true",
-                   help="graph runs copy records with copy kernels instead of memcpy nodes")
+    p.add_argument("--graph-copies", type=int, default=0,
+                   help="graph runs' record copies (tk_module_set_graph_copies): 0 memcpy nodes in 4 parallel chains, "
+                        "1 copy kernels, 2-4 memcpy nodes in that many chains, 5 one chain")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse N>1 on one GPU")
     p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
@@ -305,8 +306,9 @@ def main(argv=None) -> int:
     lib = relay.build(model.mod, target="mi355x", params=model.params)
     m = graph_executor.GraphModule(lib["default"](device.index))
     m.module.use_graph = args.run_mode == "graph"
-    if args.graph_copy_kernels:
-        _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, 1), "tk_module_set_graph_copies")
+    if args.graph_copies:
+        _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, args.graph_copies),
+                   "tk_module_set_graph_copies")
     # the module's find step (tk_module_tune) picked each conv block's kernel on this GPU
     tuning = m.module.tuning
     if args.tune_report and rank == 0:

@@ -423,8 +423,9 @@ int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* cons
  * are kept; tk_module_tune drops them; profiling mode runs tk_module_run. */
 int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst);
 /* How tk_module_run_graph copies records to host memory: 0 (default) one memcpy node per record,
- * 1 one copy kernel per node (kernel nodes writing pinned memory with 16-byte stores; measured
- * slower on ResNet-50 traces). */
+ * the nodes' copies spread over 4 parallel chains; 2..4 the same over that many chains (1 chain:
+ * pass 5); 1 one copy kernel per node (kernel nodes writing pinned memory with 16-byte stores;
+ * measured slower on ResNet-50 traces). */
 int tk_module_set_graph_copies(tk_module* mod, int copy_kernels);
 /* Makes `stream` wait for the copies of the last traced run: call before writing any
  * tensor the module reads (GraphModule.set_input / load_params,

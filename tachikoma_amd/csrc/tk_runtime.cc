@@ -171,10 +171,13 @@ struct tk_module {
   hipEvent_t graph_join = nullptr, graph_pre = nullptr;
   // the graphs are captured on two streams of the module's own (the caller's may be the legacy
   // default stream, which cannot capture) and launched on the caller's
-  hipStream_t cap_s = nullptr, cap_cs = nullptr;
+  hipStream_t cap_s = nullptr, cap_cs = nullptr, cap_cx[3] = {nullptr, nullptr, nullptr};
   // graph copies as copy kernels instead of memcpy nodes: measured slower (41.7 vs 52.7 GB/s per
   // traced ResNet-50 step, profiles/r03n_run_modes.txt), so off by default
   bool graph_copy_kernels = false;
+  // memcpy nodes in this many parallel chains (1..4): 4 measured 53.4 GB/s per traced ResNet-50
+  // step against 52.7 for one chain (profiles/r03s_graph_copy_chains.txt)
+  int graph_copy_chains = 4;
   void drop_graph() {
     for (Graph& x : graphs) {
       if (x.ge) (void)hipGraphExecDestroy(x.ge);
@@ -191,6 +194,8 @@ struct tk_module {
     if (graph_pre) (void)hipEventDestroy(graph_pre);
     if (cap_s) (void)hipStreamDestroy(cap_s);
     if (cap_cs) (void)hipStreamDestroy(cap_cs);
+    for (hipStream_t x : cap_cx)
+      if (x) (void)hipStreamDestroy(x);
   }
 };
 
@@ -412,8 +417,10 @@ int tk_module_node_times(tk_module* mod, float* node_ms) {
 // Enqueues every node on s and, when capturing, node i's output copies on cs gated by an event
 // recorded after node i (shared by tk_module_run and the graph capture of tk_module_run_graph).
 static int enqueue_nodes(tk_module* mod, hipStream_t s, hipStream_t cs, void* const* host_dst, bool capture,
-                         bool profiling, bool copy_kernels = false) {
+                         bool profiling, bool copy_kernels = false, hipStream_t const* chains = nullptr,
+                         int n_chains = 1) {
   if (profiling) TK_HIP(hipEventRecord(mod->prof[0], s));
+  int copied = 0;  // captured nodes so far: node copies rotate over the chains
   for (size_t i = 0; i < mod->nodes.size(); ++i) {
     tk::Node& n = mod->nodes[i];
     int rc = tk::run_node(n, s);
@@ -427,6 +434,7 @@ static int enqueue_nodes(tk_module* mod, hipStream_t s, hipStream_t cs, void* co
       bool any = false;
       for (int k = 0; k < n.desc.n_outputs; ++k) any |= dst[k] != nullptr;
       if (any) {
+        if (chains) cs = chains[copied++ % n_chains];
         TK_HIP(hipEventRecord(mod->done[i], s));
         TK_HIP(hipStreamWaitEvent(cs, mod->done[i], 0));
         if (copy_kernels) {
@@ -473,8 +481,11 @@ int tk_module_set_graph_copies(tk_module* mod, int copy_kernels) {
     tk::set_error("tk_module_set_graph_copies: null module");
     return TK_ERR_INVALID_ARG;
   }
-  if (mod->graph_copy_kernels != (copy_kernels != 0)) mod->drop_graph();
-  mod->graph_copy_kernels = copy_kernels != 0;
+  const bool kern = copy_kernels == 1;
+  const int chains = copy_kernels == 5 ? 1 : copy_kernels >= 2 ? std::min(copy_kernels, 4) : copy_kernels == 0 ? 4 : 1;
+  if (mod->graph_copy_kernels != kern || mod->graph_copy_chains != chains) mod->drop_graph();
+  mod->graph_copy_kernels = kern;
+  mod->graph_copy_chains = chains;
   return TK_OK;
 }
 
@@ -506,13 +517,20 @@ int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void
     if (!mod->cap_s) TK_HIP(hipStreamCreateWithFlags(&mod->cap_s, hipStreamNonBlocking));
     if (!mod->cap_cs) TK_HIP(hipStreamCreateWithFlags(&mod->cap_cs, hipStreamNonBlocking));
     hipStream_t qs = mod->cap_s, qcs = mod->cap_cs;
+    hipStream_t chains[4] = {qcs, nullptr, nullptr, nullptr};
+    const int nch = capture ? mod->graph_copy_chains : 1;
+    for (int c = 1; c < nch; ++c) {
+      if (!mod->cap_cx[c - 1]) TK_HIP(hipStreamCreateWithFlags(&mod->cap_cx[c - 1], hipStreamNonBlocking));
+      chains[c] = mod->cap_cx[c - 1];
+    }
     // capture: the node loop on qs, the copies forked onto qcs through the per-node events and
     // joined back into qs at the end, so that one launch covers the run and its copies
     TK_HIP(hipStreamBeginCapture(qs, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_nodes(mod, qs, qcs, host_dst, capture, false, mod->graph_copy_kernels);
-    if (rc == TK_OK && capture) {
-      if (hipEventRecord(mod->graph_join, qcs) != hipSuccess || hipStreamWaitEvent(qs, mod->graph_join, 0) != hipSuccess) {
-        tk::set_error("tk_module_run_graph: joining the capture stream failed");
+    int rc = enqueue_nodes(mod, qs, qcs, host_dst, capture, false, mod->graph_copy_kernels, chains, nch);
+    for (int c = 0; c < nch && rc == TK_OK && capture; ++c) {
+      // every copy chain joins back into qs (one event per join: record, then wait, in order)
+      if (hipEventRecord(mod->graph_join, chains[c]) != hipSuccess || hipStreamWaitEvent(qs, mod->graph_join, 0) != hipSuccess) {
+        tk::set_error("tk_module_run_graph: joining the capture streams failed");
         rc = TK_ERR_HIP;
       }
     }

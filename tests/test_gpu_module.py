@@ -78,6 +78,14 @@ def test_graph_replay_equals_plain_run(device):
             images.append(bytes(m.trace_capture().bytes()))
     assert images[:3] == images[3:]
     assert images[0] != images[1]
+    # copy kernels, and memcpy nodes over 2 chains / 1 chain (the default spreads them over 4)
+    for mode in (1, 2, 5):
+        _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, mode), "tk_module_set_graph_copies")
+        m.set_input("data", xs[1])
+        m.run(trace=True)
+        m.trace_capture().synchronize()
+        assert bytes(m.trace_capture().bytes()) == images[1], mode
+    _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, 0), "tk_module_set_graph_copies")
     # a second image: its own graph; both images hold their own run
     cap2 = graph_executor.TraceCapture(m.module, m._meta)
     stream = torch.cuda.current_stream()
