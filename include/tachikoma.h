@@ -165,13 +165,16 @@ typedef struct {
   const tk_tensor* residual;    /* the other qnn.add operand (same shape and dtype, NCHW) */
   tk_qnn_add_attrs add;
   int32_t algo;                 /* MFMA conv blocks: the kernel (tk_conv2d_block_algos): 0 = the
-                                   library's choice, 1 = im2col tiles, 16 + i = image-tile plan i.
+                                   library's choice, 1 = im2col tiles, 3 / 4 = persistent im2col
+                                   tiles with cross-tile prefetch (2- / 3-slot ring), 16 + i =
+                                   image-tile plan i.
                                    Every algo gives bit-identical records; only time differs. */
 } tk_block_attrs;
 
 /* The kernels an MFMA conv block can run on, as tk_block_attrs.algo values: 1 (im2col tiles,
- * always) then 16 + i for each image-tile plan that applies, in the planner's estimated-time
- * order.  Writes at most max_algos entries; returns how many exist (0: not an MFMA conv, the
+ * always), then 16 + i for each image-tile plan that applies, in the planner's estimated-time
+ * order, then 3 and 4 where the persistent im2col kernel applies (planes of more than 64 pixels,
+ * pixel count a multiple of 4, UPWARD requantize, no kernel zero point).  Writes at most max_algos entries; returns how many exist (0: not an MFMA conv, the
  * block has a single kernel) or a negative tk_status.  The reference has one CPU kernel per op
  * (its TOPI schedules are chosen at compile time); this is the MI355X find step's search space. */
 int tk_conv2d_block_algos(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,

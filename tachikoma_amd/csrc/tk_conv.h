@@ -255,8 +255,9 @@ int64_t conv_img_chunked_bytes(int rows_pad, int cin_pad, int taps);
 // Writes that image from the OIHW weight (int8, or uint8 stored xor 0x80).
 int conv_img_pack(const tk_tensor* weight, int8_t* dst, int rows_pad, int cin_pad, hipStream_t s);
 // tk_block_attrs.algo values (tk_conv2d_block_algos): 0 the library's choice, 1 im2col tiles
-// (gemm_i8_kernel), 2 image tiles with the planner's plan, 16 + i image-tile plan i.
-constexpr int kAlgoIm2col = 1, kAlgoImg = 2, kAlgoImg0 = 16;
+// (gemm_i8_kernel), 2 image tiles with the planner's plan, 3 / 4 persistent im2col tiles with
+// cross-tile prefetch and a 2- / 3-slot ring (conv_pf_kernel), 16 + i image-tile plan i.
+constexpr int kAlgoIm2col = 1, kAlgoImg = 2, kAlgoPf2 = 3, kAlgoPf3 = 4, kAlgoImg0 = 16;
 // Runs the conv block on the image-tile kernel when its plan applies (returns 1 and sets *rc;
 // algo 0: the cheapest plan by the planner's estimate), else returns 0 (im2col path).
 // `chunked`: the chunked weight image (NULL for 1x1 convs, whose packed weight has that layout).
@@ -265,5 +266,11 @@ int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga
 // The image-tile plans as algo values (16 + i), cheapest estimate first; returns how many exist.
 int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked,
                    int32_t* algos, int max_algos);
+
+// ---------------------------------------------------------------- persistent im2col conv blocks
+// (tk_conv_pf.hip) whether the launch arguments (conv2d_run's, before the tile grid) suit the
+// persistent kernel, and its launch (ring: 2 or 3 slots).
+bool conv_pf_applies(const ConvGeom& g, const GemmArgs& ga);
+int conv_pf_run(const ConvGeom& g, GemmArgs ga, int ring, hipStream_t s);
 
 }  // namespace tk

@@ -669,7 +669,7 @@ int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& 
 
 int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked, int algo,
                  hipStream_t s, int* rc) {
-  if (algo == kAlgoIm2col) return 0;
+  if (algo == kAlgoIm2col || algo == kAlgoPf2 || algo == kAlgoPf3) return 0;
   const std::vector<ImgPlan> plans = img_plans(g, a, ga, chunked != nullptr);
   if (plans.empty() && algo == 0) return 0;
   if (plans.empty() || (algo >= kAlgoImg0 && algo - kAlgoImg0 >= (int)plans.size()) ||

@@ -1855,6 +1855,15 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
                                 : nullptr;
     int irc = TK_OK;
     if (conv_img_try(g, a, ga, chunked, blk->attrs->algo, s, &irc)) return irc;
+    const int algo = blk->attrs->algo;
+    if (algo == kAlgoPf2 || algo == kAlgoPf3) {
+      if (!conv_pf_applies(g, ga)) {
+        set_error("tk_qnn_conv2d_block: algo " + std::to_string(algo) +
+                  " (persistent im2col) does not apply to this conv; see tk_conv2d_block_algos");
+        return TK_ERR_INVALID_ARG;
+      }
+      return conv_pf_run(g, ga, algo == kAlgoPf2 ? 2 : 3, s);
+    }
   }
   const bool mt1 = conv_mt1(g, blk != nullptr);
   const int ipt = mt1 ? conv_image_tiles(g, blk != nullptr, conv_needs_patch(weight, a)) : 0;
@@ -1949,7 +1958,27 @@ int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, cons
   if (max_algos > 0) algos[0] = kAlgoIm2col;
   ++n;
   n += conv_img_algos(g, &attrs->conv, ga, g.KH * g.KW == 1 || conv_img_chunked_bytes(g.rows_pad, g.cin_pad, g.KH * g.KW),
-                      algos ? algos + 1 : nullptr, max_algos - 1);
+                      algos && max_algos > 1 ? algos + 1 : nullptr, max_algos - 1);
+  // the persistent im2col kernel, last: it measured slower than the im2col kernel on every
+  // ResNet-50 layer (profiles/r03w_find_step_pf.json), so the find step's first candidates stay
+  // the image-tile plans; listed where conv2d_run's arguments will meet conv_pf_applies
+  {
+    const int64_t P = (int64_t)g.N * g.OH * g.OW, hw = (int64_t)g.OH * g.OW;
+    const int mode = attrs->requantize.mode;
+    const int taps = g.KH * g.KW;
+    GemmArgs pa = ga;
+    pa.fast_epi = P * g.O * 4 < 0xFFFFFFC0ll && hw % 4 == 0 && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD);
+    pa.unitap = taps <= 64 && (g.cin_pad % kBK == 0 || taps == 1);
+    pa.ch_is_row = 1;
+    pa.out_nchw = 1;
+    pa.shadow_out = nullptr;  // (bounded like the records)
+    if (conv_pf_applies(g, pa) && (int64_t)(g.O + 15) / 16 * 16 * P < 0xFFFFFF00ll) {
+      for (int al : {kAlgoPf2, kAlgoPf3}) {
+        if (n < max_algos) algos[n] = al;
+        ++n;
+      }
+    }
+  }
   return n;
 }
 

@@ -320,7 +320,8 @@ PATCH_CASES = [
 
 @pytest.mark.parametrize("case", PATCH_CASES, ids=[f"patch{i}" for i in range(len(PATCH_CASES))])
 def test_conv_patch_block(tk, case):
-    n, c, h, o, k, st, dt, za, ap, clip = case
+    n, c, h, o, k, st, dt, za, ap, clip = case[:10]
+    s_lo, s_hi = case[10] if len(case) > 10 else (1e-5, 1e-3)
     rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
     x = _rand(rng, (n, c, h, h), dt)
     wt = _rand(rng, (o, c, k, k), "int8")
@@ -379,7 +380,7 @@ def test_conv_img_block(tk, case):
     x = _rand(rng, (n, c, h, h), dt)
     wt = _rand(rng, (o, c, k, k), "int8")
     bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
-    s_in = rng.uniform(1e-5, 1e-3, size=o).astype(np.float32)
+    s_in = rng.uniform(s_lo, s_hi, size=o).astype(np.float32)
     s_out = np.float32(0.01)
     p = k // 2
     pad = (p, p, p, p)
@@ -415,18 +416,25 @@ ALGO_CASES = [
     (5, 512, 7, 512, 3, 1, "int8", -1, None, (0, 127)),
     (3, 256, 56, 512, 1, 2, "int8", 2, None, None),
     (2, 64, 28, 96, 1, 1, "int8", 0, None, (0, 127)),
+    # 56x56 (the persistent kernel's home): K = 64 (one stage; 800 tiles, so workgroups of both
+    # ring sizes walk several), 3x3 over 64 channels (9 stages; 296 tiles)
+    (8, 64, 56, 256, 1, 1, "int8", 1, (0.05, 3, 0.07, -2, 0.09, 1), (0, 127)),
+    (12, 64, 56, 64, 3, 1, "int8", 0, None, (0, 127)),
+    # requantize scales near 1 (shift > -2: the general requantize form, not the mul_hi one)
+    (2, 128, 28, 128, 1, 1, "int8", 2, None, (0, 127), (0.005, 0.03)),
 ]
 
 
 @pytest.mark.parametrize("case", ALGO_CASES, ids=[f"algo{i}" for i in range(len(ALGO_CASES))])
 def test_conv_block_every_algo(tk, case):
     """Each algo tk_conv2d_block_algos lists gives the oracle's records bit for bit."""
-    n, c, h, o, k, st, dt, za, ap, clip = case
+    n, c, h, o, k, st, dt, za, ap, clip = case[:10]
+    s_lo, s_hi = case[10] if len(case) > 10 else (1e-5, 1e-3)
     rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
     x = _rand(rng, (n, c, h, h), dt)
     wt = _rand(rng, (o, c, k, k), "int8")
     bias = rng.integers(-2**14, 2**14, size=o).astype(np.int32)
-    s_in = rng.uniform(1e-5, 1e-3, size=o).astype(np.float32)
+    s_in = rng.uniform(s_lo, s_hi, size=o).astype(np.float32)
     s_out = np.float32(0.01)
     p = k // 2
     pad = (p, p, p, p)
