@@ -110,3 +110,51 @@ def test_no_gpu_needed_for_host_calls():
     # loading the library and host-only calls must not require a visible GPU
     lib = _lib.load()
     assert lib.tk_last_error() is not None
+
+
+def _host_tensor(shape, code, bits, keep):
+    """A tk_tensor descriptor with no data (host-only calls read shapes and dtypes)."""
+    shp = (ctypes.c_int64 * len(shape))(*shape)
+    keep.append(shp)
+    t = _lib.tk_tensor()
+    t.data = None
+    t.ndim = len(shape)
+    t.dtype.code, t.dtype.bits, t.dtype.lanes = code, bits, 1
+    t.shape = shp
+    t.strides = None
+    return t
+
+
+@pytest.mark.parametrize("n,c,h,o,k,want_pf", [
+    (64, 64, 56, 256, 1, True),     # 56x56 expand: the persistent im2col kernel applies
+    (64, 128, 28, 128, 3, True),    # 28x28 3x3 (taps of 64-byte stages)
+    (64, 512, 7, 512, 3, False),    # 7x7: planes of <= 64 pixels take image-aligned tiles instead
+])
+def test_conv_block_algo_list(n, c, h, o, k, want_pf):
+    # tk_conv2d_block_algos: im2col first, image-tile plans (16 + i), the persistent kernel (3, 4) last
+    lib = _lib.load()
+    keep = []
+    x = _host_tensor((n, c, h, h), 0, 8, keep)
+    w = _host_tensor((o, c, k, k), 0, 8, keep)
+    a = _lib.tk_block_attrs()
+    a.conv.strides[:] = [1, 1]
+    p = k // 2
+    a.conv.padding[:] = [p, p, p, p]
+    a.conv.dilation[:] = [1, 1]
+    a.conv.groups = 1
+    a.requantize.mode = _lib.TK_RQ_AXIS_UPWARD
+    a.requantize.axis = 1
+    buf = (ctypes.c_int32 * 256)()
+    cnt = lib.tk_conv2d_block_algos(ctypes.byref(x), ctypes.byref(w), ctypes.byref(a), buf, 256)
+    assert 1 <= cnt <= 256
+    algos = [int(buf[i]) for i in range(cnt)]
+    assert algos[0] == 1
+    has_pf = 3 in algos and 4 in algos
+    assert has_pf == want_pf, algos
+    if has_pf:
+        assert algos[-2:] == [3, 4], algos
+    assert all(x >= 16 for x in algos[1:len(algos) - (2 if has_pf else 0)]), algos
+    # a short list keeps the head: the find step's first candidates
+    short = (ctypes.c_int32 * 2)()
+    assert lib.tk_conv2d_block_algos(ctypes.byref(x), ctypes.byref(w), ctypes.byref(a), short, 2) == cnt
+    assert list(short) == algos[:2]
