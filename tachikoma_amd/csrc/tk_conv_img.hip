@@ -7,7 +7,8 @@
 //   * a workgroup owns R = 32 or 64 output channels x `ipt` WHOLE images, so each of its records
 //     is one contiguous NCHW run per image (the store pattern that writes at ~5.3 TB/s on 14x14
 //     planes against ~2.4 for image-crossing 128-column tiles, profiles/r02j_store_patterns.txt);
-//   * the K loop walks the input channels in stages of CC channels (32 for 3x3, 128 for 1x1);
+//   * the K loop walks the input channels in stages of CC channels (32 or 64 for 3x3, up to 128
+//     for 1x1);
 //     each stage brings the patch of those channels for the tile's images -- the output pixels'
 //     receptive field incl. the one-pixel halo, out-of-image pixels holding the input zero point --
 //     and the R weight rows of all taps of those channels, both by LDS-DMA into one ring slot that
@@ -15,7 +16,8 @@
 //     and every weight byte once per workgroup, not once per wave (which sank the round-2
 //     patch-tile kernel, profiles/r02g_patch_ab.txt);
 //   * the 3x3 weights are read from a second, chunked packing [rows][cin_pad/32][9][32] so that a
-//     stage's rows are contiguous (conv_img_pack); 1x1 weights use the plain packing.
+//     stage's rows are contiguous (CC / 32 consecutive chunks, conv_img_pack); 1x1 weights use the
+//     plain packing.  In LDS a weight row of a stage is [CC / 32][taps][32] either way.
 // Arithmetic: the same zero-point fold (weights' zero point 0: out = Σ a'w − za·Σw, out-of-bounds
 // taps hold a' = za, python/tvm/relay/qnn/op/legalizations.py:195-226), bias_add, RequantizeLowerInt
 // (src/relay/qnn/op/requantize.cc:195-273), qnn.add (src/relay/qnn/op/add.cc:40-96) and clip
@@ -56,15 +58,16 @@ struct ImgArgs {
 };
 
 // KT: 1 or 3 taps per axis; WM: 32-row wave groups (R = 32 * WM); CT: 32-column tiles per wave
-// (the waves of a row group take columns wn, wn + WN, ...); CC: input channels per K stage (32
-// for 3x3; 32, 64 or 128 for 1x1: smaller stages for larger planes or two workgroups per CU).
+// (the waves of a row group take columns wn, wn + WN, ...); CC: input channels per K stage (32 or
+// 64 for 3x3 -- 64 halves the barrier-separated stages of the 7x7 / 14x14 layers' long K loops;
+// 32, 64 or 128 for 1x1: smaller stages for larger planes or two workgroups per CU).
 template <int KT, int WM, int CT, int CC>
 __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, ImgArgs h) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   __shared__ int s_fast;
   constexpr int R = 32 * WM;
   constexpr int WN = 4 / WM;
-  static_assert(CC % 32 == 0 && (KT == 1 || CC == 32), "3x3 stages hold 32 channels");
+  static_assert(CC % 32 == 0 && (KT == 1 || CC <= 64), "3x3 stages hold 32 or 64 channels");
   constexpr int TAPS = KT * KT;
   constexpr int SUB = CC / 32;             // K = 32 MFMA steps per tap and stage
   constexpr int KS = TAPS * SUB;           // K = 32 MFMA steps per stage
@@ -192,7 +195,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     v4i a[2], b[2][CT];
     auto rd = [&](int ks, int u) __attribute__((always_inline)) {
       const int t = ks / SUB, s = ks - t * SUB, kh = t / KT, kw = t - kh * KT;
-      a[u] = *reinterpret_cast<const v4i*>(base + aoff + t * CC + s * 32);
+      // weight row of the stage: [SUB][TAPS][32] (3x3: CC / 32 consecutive chunks of the chunked
+      // packing; 1x1: TAPS = 1, the plain packing's CC channels)
+      a[u] = *reinterpret_cast<const v4i*>(base + aoff + (s * TAPS + t) * 32);
       const int bo = 2 * s * pl16 + (kh * hc + kw) * 16;
 #pragma unroll
       for (int j = 0; j < CT; ++j)
@@ -495,7 +500,7 @@ ImgKernel img_kernel_cc(int ct) {
 template <int KT, int WM>
 ImgKernel img_kernel(int ct, int cc) {
   if constexpr (KT == 3) {
-    return img_kernel_cc<3, WM, 32>(ct);
+    return cc == 64 ? img_kernel_cc<3, WM, 64>(ct) : img_kernel_cc<3, WM, 32>(ct);
   } else {
     return cc == 32 ? img_kernel_cc<1, WM, 32>(ct) : cc == 64 ? img_kernel_cc<1, WM, 64>(ct) : img_kernel_cc<1, WM, 128>(ct);
   }
@@ -641,7 +646,7 @@ std::vector<ImgPlan> img_plans(const ConvGeom& g, const tk_conv2d_attrs* a, cons
     if (g.O % R || (force_r && R != force_r)) continue;
     const int maxcols = R == 32 ? kImgMaxCols : 256;
     for (int CC : {128, 64, 32}) {
-      if ((kt == 3 && CC != 32) || g.cin_pad % CC || (force_cc && CC != force_cc)) continue;
+      if ((kt == 3 && CC > 64) || g.cin_pad % CC || (force_cc && CC != force_cc)) continue;
       for (int ipt = std::min(maxcols / hw, g.N); ipt >= 1; --ipt) {
         if (force_ipt && ipt != force_ipt) continue;
         for (int two = 0; two < 2; ++two) {
@@ -689,7 +694,7 @@ int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga
   const int kt = best.kt;
   best.a.wimg = kt == 3 ? chunked : ga.A;
   best.a.ldw = kt == 3 ? 9 * g.cin_pad : ga.lda;
-  ImgKernel kern = kt == 3 ? (best.wm == 2 ? img_kernel<3, 2>(best.ct, 32) : img_kernel<3, 1>(best.ct, 32))
+  ImgKernel kern = kt == 3 ? (best.wm == 2 ? img_kernel<3, 2>(best.ct, best.cc) : img_kernel<3, 1>(best.ct, best.cc))
                            : (best.wm == 2 ? img_kernel<1, 2>(best.ct, best.cc) : img_kernel<1, 1>(best.ct, best.cc));
   if (best.lds > 64 * 1024) {
     // dynamic LDS beyond 64 KiB must be allowed per kernel (the static s_fast word counts too)

@@ -538,7 +538,7 @@ class DeviceModule:
             out[key] = float(ms[i])
         return out
 
-    def tune(self, max_candidates: int = 8, reps: int = 5, stream=None) -> List[dict]:
+    def tune(self, max_candidates: int = 16, reps: int = 5, stream=None) -> List[dict]:
         """Find step (tk_module_tune): every MFMA conv-block node keeps the fastest of its first
         ``max_candidates`` kernels, timed on this GPU.  All kernels give bit-identical records.
         Returns (and keeps in ``self.tuning``) per tuned node: records, chosen algo, its time and
