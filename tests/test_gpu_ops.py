@@ -421,6 +421,10 @@ ALGO_CASES = [
     (12, 64, 56, 64, 3, 1, "int8", 0, None, (0, 127)),
     # requantize scales near 1 (shift > -2: the general requantize form, not the mul_hi one)
     (2, 128, 28, 128, 1, 1, "int8", 2, None, (0, 127), (0.005, 0.03)),
+    # 3x3 with 64-channel K stages: an odd number of stages (3, stride 2) through the two-slot ring,
+    # and 5 stages of a uint8 block with a residual join on a 7x7 plane
+    (3, 192, 14, 64, 3, 2, "int8", 0, None, (0, 127)),
+    (2, 320, 7, 64, 3, 1, "uint8", 129, (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
 ]
 
 

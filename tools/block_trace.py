@@ -8,7 +8,7 @@ import glob
 import os
 import sys
 
-FAMS = ("gemm_i8_kernel", "direct_conv_kernel", "conv_img_kernel")
+FAMS = ("gemm_i8_kernel", "direct_conv_kernel", "conv_img_kernel", "conv_pf_kernel")
 
 
 def main(d, ncfg, reps=3, iters=20):

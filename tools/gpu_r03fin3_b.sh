@@ -1,5 +1,5 @@
 set -o pipefail
-# round-3 final evidence (at HEAD with the persistent-kernel algos), part 2: the driver's bench line, rocprofv3 kernel trace + stats of the
+# round-3 final evidence (at HEAD: persistent-kernel algos, 64-channel 3x3 stages), part 2: the driver's bench line, rocprofv3 kernel trace + stats of the
 # default bench command, the PMC HBM-traffic passes
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r03fin3

@@ -44,6 +44,15 @@ def step_period(names, lo=8):
     return None
 
 
+def min_launches(model="resnet50", batch=64):
+    """Block nodes of the bench's default workload (tools/layer_times.py's plan walk)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from tachikoma_amd import zoo
+    from tachikoma_amd.relay.build_module import exec_groups, lower
+    m = zoo.MODELS[model](batch=batch)
+    return sum(1 for g in exec_groups(lower(m.mod, m.params)) if g.kind in ("conv_block", "dense_block"))
+
+
 def summarise(d, launches=None, runs=None):
     """launches: block-kernel dispatches per step (default: the period of the dispatch sequence,
     step_period); runs: only used when no period is found (launches = dispatches / runs)."""
@@ -52,7 +61,9 @@ def summarise(d, launches=None, runs=None):
     if launches is None:
         p0 = passes[0]
         names = [meta[k]["kernel"] for k in sorted(k for k in per if k[0] == p0)]
-        launches = step_period(names)
+        # a step launches at least one kernel per block node: shorter periods are repeats inside a
+        # step (the 14x14 stage's identical bottlenecks), not steps
+        launches = step_period(names, lo=min_launches())
         if launches is None:
             counts = {p: sum(1 for k in per if k[0] == p) for p in passes}
             launches = min(counts.values()) // runs
