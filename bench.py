@@ -639,11 +639,16 @@ def main(argv=None) -> int:
                 "find_step": {"tuned_nodes": len(tuning),
                               "image_tile_nodes": sum(1 for t in tuning if t["algo"] >= 16),
                               "im2col_nodes": sum(1 for t in tuning if t["algo"] == 1),
+                              "persistent_nodes": sum(1 for t in tuning if t["algo"] in (3, 4)),
                               "best_us_sum": round(sum(t["us"] for t in tuning), 1)},
                 "trace_bytes_per_step": trace_bytes,
                 "trace_GBps_per_gpu": round(trace_bytes / (elapsed_max / args.steps) / 1e9, 2),
                 "macs_per_sample": macs_per_sample,
                 "ops_per_sample": 2 * macs_per_sample,
+                # per-op records/s = op-traces/s x records per sample (graph inputs and
+                # every op output)
+                "records_per_sample": len(m.plan.records),
+                "op_records_per_s": round(value * len(m.plan.records), 1),
                 "record_digests": [shard.hex64(d) for d in digests],
                 "library": _lib.build_info(),
                 "host_cpus": {"affinity": len(home_cpus), "cgroup_quota": quota, "os_cpu_count": os.cpu_count()},
