@@ -53,9 +53,10 @@ def min_launches(model="resnet50", batch=64):
     return sum(1 for g in exec_groups(lower(m.mod, m.params)) if g.kind in ("conv_block", "dense_block"))
 
 
-def summarise(d, launches=None, runs=None):
+def summarise(d, launches=None, runs=None, model="resnet50", batch=64):
     """launches: block-kernel dispatches per step (default: the period of the dispatch sequence,
-    step_period); runs: only used when no period is found (launches = dispatches / runs)."""
+    step_period, from the workload's block-node count up); runs: only used when no period is
+    found (launches = dispatches / runs)."""
     per, meta = load(d)
     passes = sorted({k[0] for k in per})
     if launches is None:
@@ -63,7 +64,7 @@ def summarise(d, launches=None, runs=None):
         names = [meta[k]["kernel"] for k in sorted(k for k in per if k[0] == p0)]
         # a step launches at least one kernel per block node: shorter periods are repeats inside a
         # step (the 14x14 stage's identical bottlenecks), not steps
-        launches = step_period(names, lo=min_launches())
+        launches = step_period(names, lo=min_launches(model, batch))
         if launches is None:
             counts = {p: sum(1 for k in per if k[0] == p) for p in passes}
             launches = min(counts.values()) // runs
@@ -99,11 +100,13 @@ def main():
     ap.add_argument("--json")
     ap.add_argument("--workload", default="", help="extra bench args the passes ran with")
     a = ap.parse_args()
-    s = summarise(a.dir, a.launches, a.runs)
     wl = a.workload.split()
+    model = wl[wl.index("--model") + 1] if "--model" in wl else "resnet50"
+    batch = int(wl[wl.index("--batch") + 1]) if "--batch" in wl else 64
+    s = summarise(a.dir, a.launches, a.runs, model, batch)
     s["bench_args"] = wl
-    s["model"] = wl[wl.index("--model") + 1] if "--model" in wl else "resnet50"
-    s["batch"] = int(wl[wl.index("--batch") + 1]) if "--batch" in wl else 64
+    s["model"] = model
+    s["batch"] = batch
     # which kernels these counters belong to: bench.py takes the traffic from the summary whose
     # library digest equals the loaded library's (else the newest by this UTC stamp)
     s["created_utc"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
