@@ -4,6 +4,7 @@
 //   kern G: a copy kernel of G workgroups reading HBM and writing the host-mapped pinned buffer
 //           with 16-byte nontemporal vector stores (zero-copy; no SDMA engine involved)
 // Each variant runs `reps` times; the best and the median GB/s are printed as one JSON line.
+// usage: probe_d2h [MiB=1024] [reps=5] [host buffer kind=mapped] [copy kernels=1]
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
@@ -34,7 +35,20 @@ int main(int argc, char** argv) {
   void *src, *dst, *dst_dev;
   CK(hipMalloc(&src, nbytes));
   CK(hipMemset(src, 1, nbytes));
-  CK(hipHostMalloc(&dst, nbytes, hipHostMallocMapped));
+  // host buffer kind (argv[3]): mapped (default, what torch's pin_memory gives), noncoherent,
+  // coherent, writecombined, register (malloc + hipHostRegister)
+  const char* kind = argc > 3 ? argv[3] : "mapped";
+  if (!strcmp(kind, "register")) {
+    dst = aligned_alloc(4096, nbytes);
+    CK(hipHostRegister(dst, nbytes, hipHostRegisterMapped));
+  } else {
+    unsigned fl = hipHostMallocMapped;
+    if (!strcmp(kind, "noncoherent")) fl |= hipHostMallocNonCoherent;
+    if (!strcmp(kind, "coherent")) fl |= hipHostMallocCoherent;
+    if (!strcmp(kind, "writecombined")) fl |= hipHostMallocWriteCombined;
+    CK(hipHostMalloc(&dst, nbytes, fl));
+  }
+  printf("{\"host_buffer\": \"%s\"}\n", kind);
   memset(dst, 0, nbytes);  // first touch
   CK(hipHostGetDevicePointer(&dst_dev, dst, 0));
   hipStream_t st[8];
@@ -84,7 +98,9 @@ int main(int argc, char** argv) {
     report("sdma_chunks64MiB", ms, (double)nbytes);
   }
   const long n16 = nbytes / 16;
+  const bool kernels = argc > 4 ? atoi(argv[4]) != 0 : true;
   for (int G : {16, 32, 64, 128, 256, 1024}) {
+    if (!kernels) break;
     std::vector<float> ms;
     for (int r = 0; r < reps + 1; ++r) {
       CK(hipDeviceSynchronize());
@@ -106,6 +122,11 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < nbytes; i += 4099) bad += ((unsigned char*)dst)[i] != 1;
   printf("{\"check\": \"kernel copy host bytes\", \"bad\": %ld}\n", bad);
   CK(hipFree(src));
-  CK(hipHostFree(dst));
+  if (!strcmp(kind, "register")) {
+    CK(hipHostUnregister(dst));
+    free(dst);
+  } else {
+    CK(hipHostFree(dst));
+  }
   return 0;
 }
