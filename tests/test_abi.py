@@ -158,3 +158,25 @@ def test_conv_block_algo_list(n, c, h, o, k, want_pf):
     short = (ctypes.c_int32 * 2)()
     assert lib.tk_conv2d_block_algos(ctypes.byref(x), ctypes.byref(w), ctypes.byref(a), short, 2) == cnt
     assert list(short) == algos[:2]
+
+
+def test_conv_block_3x3_stage_widths():
+    # 3x3 image-tile plans come with 32- and 64-channel K stages where the (padded) input channel
+    # count divides by 64: a 512-channel 7x7 layer lists more plans than a 480-channel one (32 only)
+    lib = _lib.load()
+
+    def count(c):
+        keep = []
+        x = _host_tensor((64, c, 7, 7), 0, 8, keep)
+        w = _host_tensor((512, c, 3, 3), 0, 8, keep)
+        a = _lib.tk_block_attrs()
+        a.conv.strides[:] = [1, 1]
+        a.conv.padding[:] = [1, 1, 1, 1]
+        a.conv.dilation[:] = [1, 1]
+        a.conv.groups = 1
+        a.requantize.mode = _lib.TK_RQ_AXIS_UPWARD
+        a.requantize.axis = 1
+        return lib.tk_conv2d_block_algos(ctypes.byref(x), ctypes.byref(w), ctypes.byref(a), None, 0)
+
+    n512, n480 = count(512), count(480)
+    assert n480 > 1 and n512 > n480, (n512, n480)
