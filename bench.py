@@ -60,14 +60,22 @@ def parse(argv=None):
     p.add_argument("--out-dir", default="/tmp")
     p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
     p.add_argument("--tune-report", default=None, help="write the find step's per-node kernel timings (JSON) here")
+    p.add_argument("--tune-table", default="auto",
+                   help="conv-block kernels: 'auto' replays the committed find-step table for this workload "
+                        "(profiles/*_tune_table.json, newest) so that the timed run uses the kernels the committed "
+                        "profiles were taken on, falling back to the find step when none applies; a path replays "
+                        "that table; 'none' runs the find step on this GPU")
+    p.add_argument("--write-tune-table", default=None, help="write the kernel choice this run used as a tune table")
     p.add_argument("--run-mode", choices=["graph", "host", "auto"], default="graph",
                    help="traced-step submission: one replayed HIP graph per step (tk_module_run_graph, the "
                         "default: immune to a host that issues calls late, profiles/r03r_run_modes_slow_host.txt), "
                         "every kernel and copy issued from the host (tk_module_run), or auto = the faster of the "
                         "two over two steps before the warm-up (GraphModule.pick_run_mode)")
     p.add_argument("--graph-copies", type=int, default=0,
-                   help="graph runs' record copies (tk_module_set_graph_copies): 0 memcpy nodes in 4 parallel chains, "
-                        "1 copy kernels, 2-4 memcpy nodes in that many chains, 5 one chain")
+                   help="graph runs' record copies (tk_module_set_graph_copies): 0 packed image chunks copied by "
+                        "host-issued SDMA copies (default), 1 copy kernels, 2-4 memcpy nodes in that many chains, "
+                        "5 one chain")
+    p.add_argument("--trace-chunks", type=int, default=8, help="chunks of the packed capture (tk_module_set_trace_chunks)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse N>1 on one GPU")
     p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
@@ -241,31 +249,61 @@ def cpu_baseline(model_fn, offset: int, batch: int, budget_s: float, threads: in
                       f"{dt:.1f}s timed (first sample excluded as warm-up)"}
 
 
-def pmc_traffic(model: str, batch: int, library: str):
+def pmc_traffic(model: str, batch: int, library: str, tune_digest: str | None = None):
     """HBM traffic of the block kernel from a committed PMC summary (tools/pmc.sh ->
-    profiles/*_pmc_block.json) taken on this workload: the one whose recorded library digest
-    equals the loaded library's; failing that the newest by its embedded UTC stamp (never by
-    file name).  Returns (bytes per launch, bytes per step, launches per step, source, match)."""
+    profiles/*_pmc_block.json) taken on this workload: preferably the one taken with this run's
+    kernel mix (the same tune table, by digest) and library; failing that the newest by its
+    embedded UTC stamp (never by file name).  Returns per launch / per step bytes, launches per
+    step, the source and whether library and kernel mix match."""
     import glob
     docs = []
     for path in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_block.json")):
         with open(path) as f:
             doc = json.load(f)
         if doc.get("model") == model and doc.get("batch") == batch and doc.get("created_utc"):
-            docs.append((doc.get("library") == library, doc["created_utc"], path, doc))
+            kern = tune_digest is not None and doc.get("tune_table_digest") == tune_digest
+            docs.append((kern, doc.get("library") == library, doc["created_utc"], path, doc))
     if not docs:
         return None
-    same, _, path, doc = max(docs, key=lambda d: (d[0], d[1]))
+    kern, same, _, path, doc = max(docs, key=lambda d: (d[0], d[1], d[2]))
     launches = int(doc["launches_per_step"])  # dispatches: a split-K node launches twice
     return {"per_launch": doc["hbm_bytes_per_step"] / max(launches, 1), "per_step": doc["hbm_bytes_per_step"],
             "launches": launches, "source": os.path.relpath(path, ROOT), "library_match": same,
-            "library": doc.get("library")}
+            "kernel_match": kern, "library": doc.get("library")}
+
+
+def find_tune_table(model: str, batch: int):
+    """The newest committed find-step table for this workload (profiles/*_tune_table.json, by its
+    embedded UTC stamp), or None."""
+    import glob
+    best = None
+    for path in glob.glob(os.path.join(ROOT, "profiles", "*_tune_table.json")):
+        with open(path) as f:
+            doc = json.load(f)
+        if doc.get("model") == model and doc.get("batch") == batch and doc.get("created_utc"):
+            if best is None or doc["created_utc"] > best[0]:
+                best = (doc["created_utc"], path)
+    return None if best is None else best[1]
 
 
 # ---------------------------------------------------------------- one rank
 
+def check_gpu_count(args) -> None:
+    """`--gpus N` over RCCL needs N visible GPUs (one rank per GPU): fail at once, before any rank
+    starts or ``init_process_group("nccl")`` waits on a rank that cannot exist.  Counting devices
+    does not initialise HIP.  The gloo backend rehearses N ranks on fewer GPUs and is exempt."""
+    if args.dist_backend != "nccl" or args.gpus <= 1:
+        return
+    import torch
+    have = torch.cuda.device_count()
+    if args.gpus > have:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs (one rank per GPU over "
+                         f"RCCL), this host shows {have}; use --dist-backend gloo to rehearse N ranks on one GPU")
+
+
 def main(argv=None) -> int:
     args = parse(argv)
+    check_gpu_count(args)
     if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
         return launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] +
                             (sys.argv[1:] if argv is None else list(argv)))
@@ -304,16 +342,36 @@ def main(argv=None) -> int:
     _log(f"rank {rank}/{world}: building {args.model} batch {B} on {device} "
          f"(numa node {placement['numa_node']}, {placement['cpus']} cpus)")
     lib = relay.build(model.mod, target="mi355x", params=model.params)
-    m = graph_executor.GraphModule(lib["default"](device.index))
+    # conv-block kernels: a committed / given tune table (the kernels the committed profiles were
+    # taken on) or the find step on this GPU (tk_module_tune)
+    table = None if args.tune_table == "none" else (find_tune_table(args.model, B) if args.tune_table == "auto"
+                                                    else args.tune_table)
+    tune_info = {"source": "find step on this GPU", "table": None}
+    try:
+        m = graph_executor.GraphModule(lib["default"](device.index, tune=table or True))
+        if table:
+            tune_info = {"source": "tune table", "table": os.path.relpath(table, ROOT)}
+    except _lib.TachikomaError as e:
+        if args.tune_table != "auto":
+            raise
+        _log(f"tune table {table} does not apply ({e}); running the find step")
+        m = graph_executor.GraphModule(lib["default"](device.index))
+        tune_info = {"source": "find step on this GPU (table did not apply)", "table": None}
+    tune_info["digest"] = m.module.tune_table_digest
     m.module.use_graph = args.run_mode == "graph"
     if args.graph_copies:
         _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, args.graph_copies),
                    "tk_module_set_graph_copies")
-    # the module's find step (tk_module_tune) picked each conv block's kernel on this GPU
+    _lib.check(m.module.lib.tk_module_set_trace_chunks(m.module.handle, args.trace_chunks), "tk_module_set_trace_chunks")
     tuning = m.module.tuning
     if args.tune_report and rank == 0:
         with open(args.tune_report, "w") as f:
             json.dump(tuning, f, indent=1)
+    if args.write_tune_table and rank == 0:
+        doc = m.module.tuning_table()
+        doc.update(model=args.model, batch=B, created_utc=time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()))
+        with open(args.write_tune_table, "w") as f:
+            json.dump(doc, f, indent=1)
     # weak scaling: B samples per GPU; this rank traces samples [offset, offset + B) of the global batch
     offset, count = shard.shard_range(B * world, world, rank)
     x = model.sample_inputs(offset, count)
@@ -475,7 +533,7 @@ def main(argv=None) -> int:
     achieved_bw = blk_bytes / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
     achieved_ops = blk_ops / (blk_ms * 1e-3) if blk_ms > 0 else 0.0
     total_ms = step_ms
-    pmc = pmc_traffic(args.model, B, _lib.build_info())
+    pmc = pmc_traffic(args.model, B, _lib.build_info(), m.module.tune_table_digest)
 
     # ---- trace-digest all-gather (RCCL over xGMI): one u64 record digest per rank, computed
     # on the device over the records of one more traced step (outside the timed region); the
@@ -608,6 +666,7 @@ def main(argv=None) -> int:
                                          "per step / launches per step)",
                          "traffic_source": None if pmc is None else pmc["source"],
                          "traffic_library_match": None if pmc is None else pmc["library_match"],
+                         "traffic_kernel_match": None if pmc is None else pmc["kernel_match"],
                          "traffic_bytes_per_step": None if pmc is None else int(pmc["per_step"]),
                          "launches_per_step": None if pmc is None else pmc["launches"],
                          "algorithmic_bytes_per_node": int(blk_bytes / max(n_launch, 1)),
@@ -622,7 +681,10 @@ def main(argv=None) -> int:
                                  "measured_peak_2streams_GBps": round(d2h_peak2, 2),
                                  "per_step_GBps": per_step,
                                  "note": "trace image bytes per step / max-over-ranks step time vs a 1 GiB pinned "
-                                         "D2H copy measured on rank 0 in this run"}},
+                                         "D2H copy measured on rank 0 in this run; per_step_GBps: record bytes per "
+                                         "step over the capture stream's span (HIP events around each step's copies "
+                                         "on that stream, which in the packed graph mode also waits for the first "
+                                         "chunk's kernels)"}},
             "cpu_baseline": cpu,
             "parity": par,
             "file_sink": None if args.sink != "file" else
@@ -636,6 +698,10 @@ def main(argv=None) -> int:
                 "run_mode": "hip graph per step (tk_module_run_graph)" if m.module.use_graph else
                             "host-issued kernels and copies (tk_module_run)",
                 "run_mode_pick": mode_pick,
+                "graph_copies": ("packed image, %d host-issued chunk copies" % args.trace_chunks
+                                 if args.graph_copies == 0 else f"tk_module_set_graph_copies({args.graph_copies})")
+                if m.module.use_graph else None,
+                "kernels": tune_info,
                 "find_step": {"tuned_nodes": len(tuning),
                               "image_tile_nodes": sum(1 for t in tuning if t["algo"] >= 16),
                               "im2col_nodes": sum(1 for t in tuning if t["algo"] == 1),

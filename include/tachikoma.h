@@ -346,6 +346,76 @@ int tk_dense_f32(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
 int tk_find_scale_by_kl(const int32_t* hist, const float* edges, int num_bins, int num_quantized_bins,
                         float* threshold);
 
+/* ---------------------------------------------------------------- pre-quantized QNN graphs
+ * The QNN ops a frontend-produced quantized graph carries besides conv / dense / requantize /
+ * add: the float32 input quantize, the float32 head dequantize, and the
+ * quantized concatenate / mul / subtract.  Each follows its reference canonicalization exactly;
+ * float32 steps are single IEEE operations in the reference's order (no contraction, correctly
+ * rounded division). */
+
+/* Scale / zero point of qnn.quantize (output params) and qnn.dequantize (input params):
+ * per-tensor (`scales` / `zero_points` NULL) or one float32 scale / int32 zero point per index
+ * of `axis` (device arrays; ExpandBiasToMatchAxis). */
+typedef struct {
+  int32_t axis;
+  float scale;
+  const float* scales;
+  int32_t zero_point;
+  const int32_t* zero_points;
+} tk_qparams_attrs;
+/* qnn.quantize (src/relay/qnn/op/quantize.cc:113-149, QuantizeLower): float32 data →
+ * int8 / uint8 / int16 / int32: out = cast(clip(round(x / scale) + float(zp), qmin, qmax)),
+ * round = llvm.round (halves away from zero), every step float32. */
+int tk_qnn_quantize(const tk_tensor* data, tk_tensor* out, const tk_qparams_attrs* attrs, void* stream);
+/* qnn.dequantize (src/relay/qnn/op/dequantize.cc:96-129, DequantizeLower): int8 / uint8 / int16 /
+ * int32 data → float32: out = float(int32(x) - zp) * scale (int32 subtract wraps). */
+int tk_qnn_dequantize(const tk_tensor* data, tk_tensor* out, const tk_qparams_attrs* attrs, void* stream);
+
+/* qnn.add / qnn.subtract / qnn.mul with numpy broadcasting (up to 6-D, BroadcastRel) and per-tensor
+ * or per-axis parameters (QnnBroadcastRel, src/relay/qnn/op/op_common.h:231-320):
+ *   add       (add.cc:40-96):       o = RQ(a) + RQ(b) - zp_c
+ *   subtract  (subtract.cc:40-94):  o = RQ(a) - RQ(b) + zp_c
+ *     RQ = RequantizeOrUpcast (op_common.h:193-207): requantize to int32 at the output params, or
+ *     a plain upcast when scale and zero point equal the output's (`*_upcast`); `lhs.axis` /
+ *     `rhs.axis` index the operand's own dimensions for per-axis plans;
+ *   mul       (mul.cc:43-159):      o = RQ_out((int32(a) - zp_a) * (int32(b) - zp_b)) where the
+ *     zero points are lhs.input_zero_point(s) / rhs.input_zero_point(s) (per lhs.axis / rhs.axis)
+ *     and RQ_out (`out`) requantizes the int32 product from scale s_a*s_b, zero point 0 (per-axis
+ *     along out.axis, an axis of lhs) — every int32 step wraps;
+ * then clip to the output dtype (the input dtype) and cast. */
+enum { TK_QB_ADD = 0, TK_QB_SUBTRACT = 1, TK_QB_MUL = 2 };
+typedef struct {
+  int32_t op;                   /* TK_QB_* */
+  tk_requantize_attrs lhs, rhs;
+  int32_t lhs_upcast, rhs_upcast;
+  tk_requantize_attrs out;      /* TK_QB_MUL only */
+  int32_t output_zero_point;    /* add / subtract */
+} tk_qnn_binary_attrs;
+int tk_qnn_binary(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const tk_qnn_binary_attrs* attrs,
+                  void* stream);
+
+/* qnn.concatenate (src/relay/qnn/op/concatenate.cc:153-221): input i is requantized to the output
+ * params with out dtype = its own dtype (per-tensor, `requant[i]`) unless its scale and zero point
+ * equal the output's, then all are concatenated along `axis`. */
+#define TK_CONCAT_MAX 8
+typedef struct {
+  int32_t axis;
+  int32_t n;
+  int32_t requant[TK_CONCAT_MAX];
+  tk_requantize_attrs rq[TK_CONCAT_MAX];
+} tk_concat_attrs;
+int tk_qnn_concatenate(const tk_tensor* const* inputs, int n, tk_tensor* out, const tk_concat_attrs* attrs,
+                       void* stream);
+
+/* transpose / layout_transform of a compact tensor (up to 6-D, 1/2/4/8-byte elements):
+ * out.shape[k] = data.shape[perm[k]].  The NHWC / HWIO / OHWI / HWOI qnn.conv2d layouts run the
+ * NCHW / OIHW kernels between two of these (convolution.cc:718-722 accepts them). */
+typedef struct {
+  int32_t ndim;
+  int32_t perm[6];
+} tk_transpose_attrs;
+int tk_transpose(const tk_tensor* data, tk_tensor* out, const tk_transpose_attrs* attrs, void* stream);
+
 /* ---------------------------------------------------------------- executor
  * Native run loop replacing GraphExecutor::Run (graph_executor.cc:61-66) and
  * the debug executor's per-node copy-out (graph_executor_debug.cc:249-284).
@@ -373,9 +443,14 @@ enum {
   TK_NODE_CONV2D_F32 = 18, /* in: data, weight (float32); attrs.conv2d */
   TK_NODE_DENSE_F32 = 19,  /* in: data, weight (float32) */
   TK_NODE_PAD = 20,        /* in: data; attrs.pad */
+  TK_NODE_QUANTIZE = 21,   /* in: data (float32); attrs.qparams */
+  TK_NODE_DEQUANTIZE = 22, /* in: data; out float32; attrs.qparams */
+  TK_NODE_QNN_BINARY = 23, /* in: lhs, rhs; attrs.qnn_binary */
+  TK_NODE_CONCAT = 24,     /* in: 1..TK_MAX_NODE_INPUTS tensors; attrs.concat */
+  TK_NODE_TRANSPOSE = 25,  /* in: data; attrs.transpose (layout changes around NHWC convs) */
 };
 
-#define TK_MAX_NODE_INPUTS 4
+#define TK_MAX_NODE_INPUTS 8
 #define TK_MAX_NODE_OUTPUTS 6
 
 typedef struct {
@@ -396,6 +471,10 @@ typedef struct {
     tk_postops_attrs postops;
     tk_ewise_attrs ewise;
     tk_pad_attrs pad;
+    tk_qparams_attrs qparams;
+    tk_qnn_binary_attrs qnn_binary;
+    tk_concat_attrs concat;
+    tk_transpose_attrs transpose;
     struct { int64_t a_min, a_max; } clip;
     struct { int32_t axis; } bias_add;
   } attrs;
@@ -425,11 +504,21 @@ int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* cons
  * queued on it afterwards (as with tk_module_run).  Up to four graphs (streams / destinations)
  * are kept; tk_module_tune drops them; profiling mode runs tk_module_run. */
 int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst);
-/* How tk_module_run_graph copies records to host memory: 0 (default) one memcpy node per record,
- * the nodes' copies spread over 4 parallel chains; 2..4 the same over that many chains (1 chain:
- * pass 5); 1 one copy kernel per node (kernel nodes writing pinned memory with 16-byte stores;
- * measured slower on ResNet-50 traces). */
+/* How tk_module_run_graph copies records to host memory:
+ *   0 (default) packed: the graph runs the nodes plus, after the node that completes each chunk of
+ *     the trace image (tk_module_set_trace_chunks, 8 by default; chunks end where every record below
+ *     them is written), a kernel that gathers the chunk's records into a device mirror of the image
+ *     range the records span (header bytes included, loaded once from the host image) and an external
+ *     event-record node; the chunk then leaves as one host-issued hipMemcpyAsync on capture_stream
+ *     gated on that event.  Two mirrors alternate, so a run's kernels overlap the previous run's
+ *     copies.  Whole-chunk copies run at 57.0 GB/s against 56.0 for per-record copies and 54.0-54.6
+ *     for graph memcpy nodes (profiles/r04c_copyprobe.jsonl).  Record buffers must be 16-byte aligned
+ *     and readable in whole 16-byte chunks; host destinations must not overlap.
+ *   2..4 one memcpy node per record in that many parallel chains (1 chain: pass 5);
+ *   1 one copy kernel per node (kernel nodes writing pinned memory with 16-byte stores). */
 int tk_module_set_graph_copies(tk_module* mod, int copy_kernels);
+/* Chunks of the packed capture (1..256). */
+int tk_module_set_trace_chunks(tk_module* mod, int chunks);
 /* Makes `stream` wait for the copies of the last traced run: call before writing any
  * tensor the module reads (GraphModule.set_input / load_params,
  * graph_executor.cc:158-166 SetInput) on a stream of your own. */
@@ -451,6 +540,10 @@ int tk_module_node_times(tk_module* mod, float* node_ms);
  * (max_candidates + 1) each: algo_out[i][0] = the chosen algo (-1: node not tuned), [i][1 + c]
  * = candidate c (-1 past the last); us_out likewise in microseconds per launch. */
 int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, int32_t* algo_out, float* us_out);
+/* Sets conv-block node `node` to run kernel `algo` (0 = the library's choice, else one of
+ * tk_conv2d_block_algos for that node): replays a saved find-step table, so that a profile and a
+ * timed run use the same kernels.  TK_ERR_INVALID_ARG for other nodes or algos. */
+int tk_module_set_node_algo(tk_module* mod, int node, int algo);
 
 /* ---------------------------------------------------------------- trace format
  * NDArray-list blob (src/runtime/file_utils.cc:184-236, include/tvm/runtime/ndarray.h:447-494):

@@ -108,10 +108,26 @@ def eval_call(call, args, backend: str = "numpy", threads: int = 1):
     if op == "qnn.conv2d":
         x, w = args[0], args[1]
         za, zw = _const(call.args[2]), _const(call.args[3])
+        # NHWC data / HWIO, OHWI, HWOI kernels: the same contraction on the transposed operands, the
+        # result in the data layout (Conv2DRel: out_layout defaults to data_layout)
+        dl, kl = a.get("data_layout", "NCHW"), a.get("kernel_layout", "OIHW")
+        if dl == "NHWC":
+            x = np.ascontiguousarray(x.transpose(0, 3, 1, 2))
+        if kl != "OIHW":
+            w = np.ascontiguousarray(w.transpose([kl.index(ch) for ch in "OIHW"]))
+        mult = a.get("depthwise_multiplier", 1)
+        if mult > 1:
+            # Conv2DRel's depthwise weight (C, M, KH, KW): output channel c * M + m reads [c, m]
+            # (src/relay/op/nn/convolution.cc:243-274; topi depthwise_conv2d_nchw)
+            w = w.reshape(w.shape[0] * w.shape[1], 1, w.shape[2], w.shape[3])
+            if np.ndim(zw):
+                zw = np.repeat(np.asarray(zw).reshape(-1), mult)
         if backend == "c":
-            return _conv_c(x, w, za, zw, a, threads)
-        return ref.qnn_conv2d(x, w, za, zw, strides=a["strides"], padding=a["padding"], dilation=a["dilation"],
-                              groups=a["groups"])
+            out = _conv_c(x, w, za, zw, a, threads)
+        else:
+            out = ref.qnn_conv2d(x, w, za, zw, strides=a["strides"], padding=a["padding"], dilation=a["dilation"],
+                                 groups=a["groups"])
+        return np.ascontiguousarray(out.transpose(0, 2, 3, 1)) if dl == "NHWC" else out
     if op == "qnn.dense":
         x, w = args[0], args[1]
         za, zw = _const(call.args[2]), _const(call.args[3])
@@ -122,9 +138,23 @@ def eval_call(call, args, backend: str = "numpy", threads: int = 1):
         return ref.requantize(args[0], _const(call.args[1]), _const(call.args[2]), _const(call.args[3]),
                               _const(call.args[4]), axis=a["axis"], rounding=_resolve_rounding(a),
                               out_dtype=a["out_dtype"])
-    if op == "qnn.add":
+    if op in ("qnn.add", "qnn.subtract", "qnn.mul"):
         c = [_const(call.args[i]) for i in range(2, 8)]
-        return ref.qnn_add(args[0], args[1], *c)
+        fn = {"qnn.add": ref.qnn_add, "qnn.subtract": ref.qnn_subtract, "qnn.mul": ref.qnn_mul}[op]
+        kw = {"rounding": _resolve_rounding(a)} if op == "qnn.mul" else {}
+        return fn(args[0], args[1], *c, lhs_axis=a.get("lhs_axis", -1), rhs_axis=a.get("rhs_axis", -1), **kw)
+    if op == "qnn.concatenate":
+        scales = [_const(f) for f in call.args[1].fields]
+        zps = [_const(f) for f in call.args[2].fields]
+        return ref.qnn_concatenate(args[0], scales, zps, _const(call.args[3]), _const(call.args[4]), axis=a["axis"],
+                                   rounding=_resolve_rounding(a))
+    if op == "qnn.quantize":
+        return ref.quantize(args[0], _const(call.args[1]), _const(call.args[2]), axis=a["axis"],
+                            out_dtype=a["out_dtype"])
+    if op == "qnn.dequantize":
+        return ref.dequantize(args[0], _const(call.args[1]), _const(call.args[2]), axis=a["axis"])
+    if op == "transpose":
+        return np.ascontiguousarray(np.transpose(args[0], a["axes"]))
     if op == "nn.bias_add":
         return ref.bias_add(args[0], args[1], axis=a["axis"])
     if op in ("tachikoma.qnn.conv2d", "tachikoma.qnn.dense"):
@@ -189,6 +219,10 @@ def calibrate(mod, params: Dict[str, np.ndarray], inputs: Dict[str, np.ndarray],
                 records[node.name_hint] = v
         elif kind == "Constant":
             values[id(node)] = node.data
+        elif kind == "Tuple":
+            # a tuple is no op: it has no record and takes no symbol name (MRT's expr2symbol
+            # names Calls and TupleGetItems, python/tvm/mrt/symbol.py:212-253)
+            values[id(node)] = [values[id(f)] for f in node.fields]
         elif kind == "Call":
             name = f"%{counter}"
             counter += 1

@@ -171,7 +171,7 @@ def eval_call(call, args):
         return args[0]
     if op == "relay.op.annotation.simulated_quantize":
         return simulated_quantize(args[0], args[1], args[2], args[3])
-    if args and np.asarray(args[0]).dtype.kind == "f":
+    if args and not op.startswith("qnn.") and np.asarray(args[0]).dtype.kind == "f":
         x = args[0]
         if op == "clip":
             return clip(x, a["a_min"], a["a_max"])

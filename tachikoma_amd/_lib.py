@@ -160,6 +160,45 @@ class tk_pool2d_attrs(ctypes.Structure):
     ]
 
 
+class tk_qparams_attrs(ctypes.Structure):
+    _fields_ = [
+        ("axis", ctypes.c_int32),
+        ("scale", ctypes.c_float),
+        ("scales", ctypes.c_void_p),
+        ("zero_point", ctypes.c_int32),
+        ("zero_points", ctypes.c_void_p),
+    ]
+
+
+class tk_qnn_binary_attrs(ctypes.Structure):
+    _fields_ = [
+        ("op", ctypes.c_int32),
+        ("lhs", tk_requantize_attrs),
+        ("rhs", tk_requantize_attrs),
+        ("lhs_upcast", ctypes.c_int32),
+        ("rhs_upcast", ctypes.c_int32),
+        ("out", tk_requantize_attrs),
+        ("output_zero_point", ctypes.c_int32),
+    ]
+
+
+TK_QB = {"qnn.add": 0, "qnn.subtract": 1, "qnn.mul": 2}
+CONCAT_MAX = 8
+
+
+class tk_concat_attrs(ctypes.Structure):
+    _fields_ = [
+        ("axis", ctypes.c_int32),
+        ("n", ctypes.c_int32),
+        ("requant", ctypes.c_int32 * CONCAT_MAX),
+        ("rq", tk_requantize_attrs * CONCAT_MAX),
+    ]
+
+
+class tk_transpose_attrs(ctypes.Structure):
+    _fields_ = [("ndim", ctypes.c_int32), ("perm", ctypes.c_int32 * 6)]
+
+
 class _clip(ctypes.Structure):
     _fields_ = [("a_min", ctypes.c_int64), ("a_max", ctypes.c_int64)]
 
@@ -180,6 +219,10 @@ class tk_node_attrs(ctypes.Union):
         ("postops", tk_postops_attrs),
         ("ewise", tk_ewise_attrs),
         ("pad", tk_pad_attrs),
+        ("qparams", tk_qparams_attrs),
+        ("qnn_binary", tk_qnn_binary_attrs),
+        ("concat", tk_concat_attrs),
+        ("transpose", tk_transpose_attrs),
         ("clip", _clip),
         ("bias_add", _bias_add),
     ]
@@ -189,7 +232,7 @@ class tk_node(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_int32),
         ("n_inputs", ctypes.c_int32),
-        ("inputs", ctypes.POINTER(tk_tensor) * 4),
+        ("inputs", ctypes.POINTER(tk_tensor) * 8),
         ("n_outputs", ctypes.c_int32),
         ("outputs", ctypes.POINTER(tk_tensor) * 6),
         ("ext", ctypes.c_void_p * 5),
@@ -217,8 +260,9 @@ NODE_KINDS = {
     "qnn.add": 7, "nn.max_pool2d": 8, "nn.avg_pool2d": 9, "nn.global_avg_pool2d": 10, "copy": 11, "shadow": 12,
     "conv_block": 13, "dense_block": 14, "add_block": 15, "postops": 16,
     "ewise": 17, "conv2d_f32": 18, "dense_f32": 19, "nn.pad": 20,
+    "qnn.quantize": 21, "qnn.dequantize": 22, "qnn_binary": 23, "qnn.concatenate": 24, "transpose": 25,
 }
-MAX_NODE_INPUTS = 4
+MAX_NODE_INPUTS = 8
 MAX_NODE_OUTPUTS = 6
 
 # Every symbol declared in include/tachikoma.h, with its ctypes signature.
@@ -264,6 +308,12 @@ SIGNATURES = {
     "tk_ewise": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_ewise_attrs), _VP]),
     "tk_conv2d_f32": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_conv2d_attrs), _VP]),
     "tk_dense_f32": (ctypes.c_int, [_PT, _PT, _PT, _VP]),
+    "tk_qnn_quantize": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_qparams_attrs), _VP]),
+    "tk_qnn_dequantize": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_qparams_attrs), _VP]),
+    "tk_qnn_binary": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_qnn_binary_attrs), _VP]),
+    "tk_qnn_concatenate": (ctypes.c_int, [ctypes.POINTER(_PT), ctypes.c_int, _PT, ctypes.POINTER(tk_concat_attrs),
+                                          _VP]),
+    "tk_transpose": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_transpose_attrs), _VP]),
     "tk_find_scale_by_kl": (ctypes.c_int, [ctypes.POINTER(_I32), ctypes.POINTER(_F32), ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(_F32)]),
     "tk_module_create": (ctypes.c_int, [ctypes.POINTER(tk_node), ctypes.c_int, ctypes.POINTER(_VP)]),
@@ -277,8 +327,10 @@ SIGNATURES = {
     "tk_module_node_times": (ctypes.c_int, [_VP, ctypes.POINTER(_F32)]),
     "tk_module_run_graph": (ctypes.c_int, [_VP, _VP, _VP, ctypes.POINTER(_VP)]),
     "tk_module_set_graph_copies": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "tk_module_set_trace_chunks": (ctypes.c_int, [_VP, ctypes.c_int]),
     "tk_module_tune": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
                                       ctypes.POINTER(_F32)]),
+    "tk_module_set_node_algo": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int]),
     "tk_conv2d_block_algos": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_block_attrs), ctypes.POINTER(ctypes.c_int32),
                                              ctypes.c_int]),
     "tk_ndlist_layout": (_I64, [ctypes.POINTER(tk_array_meta), ctypes.c_int, ctypes.POINTER(_I64)]),

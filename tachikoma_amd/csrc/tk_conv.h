@@ -257,7 +257,8 @@ int conv_img_pack(const tk_tensor* weight, int8_t* dst, int rows_pad, int cin_pa
 // tk_block_attrs.algo values (tk_conv2d_block_algos): 0 the library's choice, 1 im2col tiles
 // (gemm_i8_kernel), 2 image tiles with the planner's plan, 3 / 4 persistent im2col tiles with
 // cross-tile prefetch and a 2- / 3-slot ring (conv_pf_kernel), 16 + i image-tile plan i.
-constexpr int kAlgoIm2col = 1, kAlgoImg = 2, kAlgoPf2 = 3, kAlgoPf3 = 4, kAlgoImg0 = 16;
+// 5: the small-batch dense tile kernel (tk_dense.hip) for dense blocks run as 1x1 conv blocks.
+constexpr int kAlgoIm2col = 1, kAlgoImg = 2, kAlgoPf2 = 3, kAlgoPf3 = 4, kAlgoDense = 5, kAlgoImg0 = 16;
 // Runs the conv block on the image-tile kernel when its plan applies (returns 1 and sets *rc;
 // algo 0: the cheapest plan by the planner's estimate), else returns 0 (im2col path).
 // `chunked`: the chunked weight image (NULL for 1x1 convs, whose packed weight has that layout).
@@ -272,5 +273,10 @@ int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& 
 // persistent kernel, and its launch (ring: 2 or 3 slots).
 bool conv_pf_applies(const ConvGeom& g, const GemmArgs& ga);
 int conv_pf_run(const ConvGeom& g, GemmArgs ga, int ring, hipStream_t s);
+
+// ---------------------------------------------------------------- small-batch dense blocks
+// (tk_dense.hip) [B, K] x [U, K]^T on 32 x 32 tiles with K split over the four waves, one launch.
+bool conv_dense_applies(const ConvGeom& g, const GemmArgs& ga);
+int conv_dense_run(const ConvGeom& g, const GemmArgs& ga, hipStream_t s);
 
 }  // namespace tk

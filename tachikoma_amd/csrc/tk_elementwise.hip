@@ -621,6 +621,79 @@ int host_copy_impl(const void* const* src, void* const* dst, const int64_t* byte
   return TK_OK;
 }
 
+// ---------------------------------------------------------------- trace image pack
+// Packed trace capture (tk_module_run_graph's default): a chunk's records are gathered from their
+// own device buffers into a device mirror of the trace image's records section, at their final
+// (NDArray-list, any-alignment) offsets, so that the chunk leaves for host memory as ONE contiguous
+// SDMA copy (host-issued copies of whole chunks run at 57.0 GB/s, per-record copies at 56.0 and
+// graph memcpy nodes at 54.0-54.6, profiles/r04c_copyprobe.jsonl).  One thread writes one 16-byte
+// aligned chunk of the mirror: whole chunks from two aligned 16-byte source loads and a funnel
+// shift, partial chunks (next to a header) byte by byte, header bytes left as they are.  Record
+// buffers must be 16-byte aligned and readable in whole 16-byte chunks (torch allocations are).
+struct PackRec {
+  const uint8_t* src;
+  int64_t dst;        // offset in the mirror
+  int64_t bytes;
+  int64_t first_blk;  // first workgroup of this record in the launch
+};
+
+__device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t r) {
+  return r ? __builtin_amdgcn_alignbyte(hi, lo, r) : lo;
+}
+
+__global__ __launch_bounds__(256) void pack_records_kernel(const PackRec* __restrict__ recs, int nrec,
+                                                           uint8_t* __restrict__ mirror) {
+  int lo = 0, hi = nrec - 1;
+  const int64_t b = blockIdx.x;
+  while (lo < hi) {  // the record whose workgroups include b
+    const int mid = (lo + hi + 1) >> 1;
+    if (recs[mid].first_blk <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const PackRec r = recs[lo];
+  const int64_t a0 = r.dst & ~(int64_t)15;  // first 16-byte chunk touching the payload
+  const int64_t a = a0 + ((b - r.first_blk) * 256 + threadIdx.x) * 16;
+  const int64_t end = r.dst + r.bytes;
+  if (a >= end) return;
+  if (a >= r.dst && a + 16 <= end) {
+    const int64_t so = a - r.dst;  // source offset of the chunk's first byte
+    const int64_t base = so & ~(int64_t)15;
+    const uint32_t s = (uint32_t)(so - base);
+    tk_v4i v0 = __builtin_nontemporal_load(reinterpret_cast<const tk_v4i*>(r.src + base));
+    tk_v4i out;
+    if (s == 0) {
+      out = v0;
+    } else {
+      tk_v4i v1 = __builtin_nontemporal_load(reinterpret_cast<const tk_v4i*>(r.src + base + 16));
+      const uint32_t w[8] = {(uint32_t)v0.x, (uint32_t)v0.y, (uint32_t)v0.z, (uint32_t)v0.w,
+                             (uint32_t)v1.x, (uint32_t)v1.y, (uint32_t)v1.z, (uint32_t)v1.w};
+      const uint32_t q = s >> 2, rb = s & 3;
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        // w[k + q] / w[k + q + 1] through selects (no dynamic register indexing)
+        const uint32_t x0 = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+        const uint32_t x1 = q == 0 ? w[k + 1] : q == 1 ? w[k + 2] : q == 2 ? w[k + 3] : w[k + 4];
+        o[k] = funnel(x0, x1, rb);
+      }
+      out = tk_v4i{(int)o[0], (int)o[1], (int)o[2], (int)o[3]};
+    }
+    *reinterpret_cast<tk_v4i*>(mirror + a) = out;
+  } else {
+    const int64_t from = a > r.dst ? a : r.dst;
+    const int64_t to = a + 16 < end ? a + 16 : end;
+    for (int64_t i = from; i < to; ++i) mirror[i] = r.src[i - r.dst];
+  }
+}
+
+int pack_records_impl(const void* table, int nrec, int64_t blocks, void* mirror, hipStream_t s) {
+  TK_CHECK_ARG(table && mirror && nrec > 0 && blocks > 0, "bad arguments");
+  hipLaunchKernelGGL(pack_records_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const PackRec*)table, nrec,
+                     (uint8_t*)mirror);
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
 // ---------------------------------------------------------------- nn.pad
 // One thread per output element (its index decomposed over up to 6 dimensions, innermost first):
 // inside the data's range it copies data[i - before], else writes the pad value.

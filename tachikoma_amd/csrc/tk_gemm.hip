@@ -1848,6 +1848,13 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
     ga.RB = ps;
     ga.zA_vec = a->kernel_zero_points;
   }
+  if (blk && blk->attrs->algo == kAlgoDense) {
+    if (!conv_dense_applies(g, ga)) {
+      set_error("tk_qnn_conv2d_block: algo 5 (dense tiles) does not apply to this block; see tk_conv2d_block_algos");
+      return TK_ERR_INVALID_ARG;
+    }
+    return conv_dense_run(g, ga, s);
+  }
   if (blk) {
     // whole-image tiles with the patch staged per channel stage (tk_conv_img.hip) where they apply
     const int8_t* chunked = conv_img_chunked_bytes(g.rows_pad, g.cin_pad, g.KH * g.KW)
@@ -1955,10 +1962,15 @@ int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, cons
   ga.zA_vec = attrs->conv.kernel_zero_points;
   ga.RB = conv_needs_patch(weight, &attrs->conv) ? &marker : nullptr;
   int n = 0;
-  if (max_algos > 0) algos[0] = kAlgoIm2col;
+  // dense blocks (1x1 over [B, K, 1, 1]) with a zero weight zero point: the dense tile kernel first
+  if (conv_dense_applies(g, ga)) {
+    if (n < max_algos) algos[n] = kAlgoDense;
+    ++n;
+  }
+  if (n < max_algos) algos[n] = kAlgoIm2col;
   ++n;
   n += conv_img_algos(g, &attrs->conv, ga, g.KH * g.KW == 1 || conv_img_chunked_bytes(g.rows_pad, g.cin_pad, g.KH * g.KW),
-                      algos && max_algos > 1 ? algos + 1 : nullptr, max_algos - 1);
+                      algos && max_algos > n ? algos + n : nullptr, max_algos - n);
   // the persistent im2col kernel, last: it measured slower than the im2col kernel on every
   // ResNet-50 layer (profiles/r03w_find_step_pf.json), so the find step's first candidates stay
   // the image-tile plans; listed where conv2d_run's arguments will meet conv_pf_applies
@@ -1967,8 +1979,12 @@ int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, cons
     const int mode = attrs->requantize.mode;
     const int taps = g.KH * g.KW;
     GemmArgs pa = ga;
-    pa.fast_epi = P * g.O * 4 < 0xFFFFFFC0ll && hw % 4 == 0 && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD);
-    pa.unitap = taps <= 64 && (g.cin_pad % kBK == 0 || taps == 1);
+    // the same gates (incl. the TK_FASTEPI / TK_UNITAP overrides) as conv2d_run, so that every
+    // algo listed here runs there
+    const int epi = hw % 32 == 0 || hw <= 64 ? 1 : 2;
+    pa.fast_epi = P * g.O * 4 < 0xFFFFFFC0ll && hw % 4 == 0 && (mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_TENSOR_UPWARD)
+                      ? env_int("TK_FASTEPI", epi) : 0;
+    pa.unitap = taps <= 64 && (g.cin_pad % kBK == 0 || taps == 1) && env_int("TK_UNITAP", 1);
     pa.ch_is_row = 1;
     pa.out_nchw = 1;
     pa.shadow_out = nullptr;  // (bounded like the records)

@@ -1,0 +1,465 @@
+// The QNN ops of a pre-quantized (frontend-produced) graph beside conv / dense / requantize / add:
+// qnn.quantize, qnn.dequantize, qnn.concatenate, qnn.mul, qnn.subtract (and qnn.add with
+// broadcasting / per-axis parameters), plus the transpose that carries NHWC / HWIO / OHWI / HWOI
+// qnn.conv2d operands to the NCHW / OIHW kernels.
+//
+// All of them are HBM-bound streaming kernels (a few bytes in and out per element, a handful of
+// integer or float32 operations).  Integer steps wrap in int32 exactly where the reference's
+// canonicalized Relay is int32; float32 steps are single IEEE operations in the reference's order
+// (correctly rounded division, hipcc's default; no FMA contraction).
+#include <algorithm>
+#include <climits>
+
+#include "tk_common.h"
+
+#pragma clang fp contract(off)
+
+namespace tk {
+
+namespace {
+
+constexpr int kQBlock = 256;
+
+int qgrid(int64_t items) {
+  int64_t g = (items + kQBlock - 1) / kQBlock;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 256 * 8));
+}
+
+// channel index of element i along an axis with `inner` elements after it and C entries
+__device__ __forceinline__ int chan(int64_t i, int32_t inner, int32_t C) {
+  return (int)((i / inner) % C);
+}
+
+bool axis_inner(const tk_tensor* t, int axis, int32_t* inner, int32_t* C) {
+  if (t->ndim == 0) {
+    *inner = 1;
+    *C = 1;
+    return true;
+  }
+  const int ax = axis < 0 ? t->ndim + axis : axis;
+  if (ax < 0 || ax >= t->ndim) return false;
+  int64_t in = 1;
+  for (int i = ax + 1; i < t->ndim; ++i) in *= t->shape[i];
+  if (in > INT32_MAX || t->shape[ax] > INT32_MAX) return false;
+  *inner = (int32_t)in;
+  *C = (int32_t)t->shape[ax];
+  return true;
+}
+
+// a full RqParams (per-axis arrays included) from the ABI struct
+RqParams rq_params(const tk_requantize_attrs& a) {
+  RqParams p{};
+  p.mode = a.mode;
+  p.multiplier = a.multiplier;
+  p.shift = a.shift;
+  p.zp_in = a.input_zero_point;
+  p.zp_out = a.output_zero_point;
+  p.ms = a.multipliers;
+  p.ss = a.shifts;
+  p.zps = a.input_zero_points;
+  p.inner = 1;
+  p.C = 1;
+  return p;
+}
+
+bool per_axis_mode(int mode) { return mode == TK_RQ_AXIS_UPWARD || mode == TK_RQ_AXIS_TONEAREST; }
+
+template <typename T> struct Lim {
+  static constexpr int64_t lo = (int64_t)std::numeric_limits<T>::min();
+  static constexpr int64_t hi = (int64_t)std::numeric_limits<T>::max();
+};
+
+template <typename F> int dispatch_q(const tk_tensor* t, F&& f) {
+  if (is_int(t, 8)) return f((int8_t)0);
+  if (is_uint(t, 8)) return f((uint8_t)0);
+  if (is_int(t, 16)) return f((int16_t)0);
+  if (is_int(t, 32)) return f((int32_t)0);
+  set_error("qnn op: dtype must be int8, uint8, int16 or int32");
+  return TK_ERR_DTYPE;
+}
+
+// any integer dtype (concatenate without requantize moves the bytes as they are)
+template <typename F> int dispatch_q_any(const tk_tensor* t, F&& f) {
+  switch (dt_of(t)) {
+    case DT_I8: return f((int8_t)0);
+    case DT_U8: return f((uint8_t)0);
+    case DT_I16: return f((int16_t)0);
+    case DT_U16: return f((uint16_t)0);
+    case DT_I32: return f((int32_t)0);
+    case DT_U32: return f((uint32_t)0);
+    case DT_I64: return f((int64_t)0);
+    case DT_U64: return f((uint64_t)0);
+  }
+  set_error("qnn.concatenate: integer dtype expected");
+  return TK_ERR_DTYPE;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- qnn.quantize
+// QuantizeLower (src/relay/qnn/op/quantize.cc:113-149):
+//   Cast(Clip(Add(Round(Divide(x, scale)), Cast(zp, float32)), qmin, qmax), out_dtype)
+// Clip's bounds are float32 constants (topi clip, python/tvm/topi/math.py:615-640); the float ->
+// int cast is fptosi.  For an int32 output the upper bound float32(2^31 - 1) is 2^31, which the
+// reference's x86 cvttss2si turns into INT32_MIN ("integer indefinite"); that is reproduced.
+template <typename To>
+__global__ __launch_bounds__(kQBlock) void quantize_kernel(const float* __restrict__ x, To* __restrict__ y, int64_t n,
+                                                            float scale, const float* __restrict__ scales,
+                                                            int32_t zp, const int32_t* __restrict__ zps,
+                                                            int32_t inner, int32_t C, float qmin, float qmax) {
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    const int c = (scales || zps) ? chan(i, inner, C) : 0;
+    const float s = scales ? scales[c] : scale;
+    const float z = (float)(zps ? zps[c] : zp);
+    float v = x[i] / s;
+    v = roundf(v);  // llvm.round: halves away from zero
+    v = v + z;
+    v = v < qmax ? v : qmax;  // max(min(v, qmax), qmin)
+    v = v > qmin ? v : qmin;
+    if constexpr (sizeof(To) == 4) {
+      y[i] = v >= 2147483648.0f ? (To)INT32_MIN : (To)(int32_t)v;
+    } else {
+      y[i] = (To)(int32_t)v;
+    }
+  }
+}
+
+static bool qparams_geometry(const tk_tensor* t, const tk_qparams_attrs* a, int32_t* inner, int32_t* C) {
+  if (!a->scales && !a->zero_points) {
+    *inner = 1;
+    *C = 1;
+    return true;
+  }
+  return axis_inner(t, a->axis, inner, C);
+}
+
+int qnn_quantize_impl(const tk_tensor* x, tk_tensor* y, const tk_qparams_attrs* a, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y) && numel(x) == numel(y), "bad tensors");
+  TK_CHECK_ARG(is_f32(x), "qnn.quantize: float32 data expected");
+  int32_t inner, C;
+  if (!qparams_geometry(x, a, &inner, &C)) {
+    set_error("tk_qnn_quantize: bad axis");
+    return TK_ERR_INVALID_ARG;
+  }
+  const int64_t n = numel(x);
+  return dispatch_q(y, [&](auto tag) -> int {
+    using To = decltype(tag);
+    hipLaunchKernelGGL((quantize_kernel<To>), dim3(qgrid(n)), dim3(kQBlock), 0, s, (const float*)ptr(x), (To*)ptr(y),
+                       n, a->scale, a->scales, a->zero_point, a->zero_points, inner, C, (float)Lim<To>::lo,
+                       (float)Lim<To>::hi);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  });
+}
+
+// ---------------------------------------------------------------- qnn.dequantize
+// DequantizeLower (src/relay/qnn/op/dequantize.cc:96-129):
+//   Multiply(Cast(Subtract(Cast(x, int32), zp), float32), scale)
+template <typename Ti>
+__global__ __launch_bounds__(kQBlock) void dequantize_kernel(const Ti* __restrict__ x, float* __restrict__ y, int64_t n,
+                                                              float scale, const float* __restrict__ scales,
+                                                              int32_t zp, const int32_t* __restrict__ zps,
+                                                              int32_t inner, int32_t C) {
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    const int c = (scales || zps) ? chan(i, inner, C) : 0;
+    const int32_t t = (int32_t)((uint32_t)(int32_t)x[i] - (uint32_t)(zps ? zps[c] : zp));
+    y[i] = (float)t * (scales ? scales[c] : scale);
+  }
+}
+
+int qnn_dequantize_impl(const tk_tensor* x, tk_tensor* y, const tk_qparams_attrs* a, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y) && numel(x) == numel(y), "bad tensors");
+  TK_CHECK_ARG(is_f32(y), "qnn.dequantize: float32 output expected");
+  int32_t inner, C;
+  if (!qparams_geometry(x, a, &inner, &C)) {
+    set_error("tk_qnn_dequantize: bad axis");
+    return TK_ERR_INVALID_ARG;
+  }
+  const int64_t n = numel(x);
+  return dispatch_q(x, [&](auto tag) -> int {
+    using Ti = decltype(tag);
+    hipLaunchKernelGGL((dequantize_kernel<Ti>), dim3(qgrid(n)), dim3(kQBlock), 0, s, (const Ti*)ptr(x),
+                       (float*)ptr(y), n, a->scale, a->scales, a->zero_point, a->zero_points, inner, C);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  });
+}
+
+// ---------------------------------------------------------------- qnn binary ops
+// Broadcast geometry over the output (numpy rules, operands right-aligned, up to 6-D): element
+// strides of each operand per output dimension (0 where it broadcasts), and for each per-axis
+// parameter set the output dimension its channel index is read from (-1: none, or a broadcast
+// size-1 axis whose single entry is channel 0).
+struct BinGeom {
+  int32_t nd;
+  int64_t shape[6];
+  int64_t ls[6], rs[6];
+  int32_t lax, rax, oax;
+};
+
+template <typename T, int OP, bool FLAT>
+__global__ __launch_bounds__(kQBlock) void qnn_binary_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                              T* __restrict__ y, int64_t n, BinGeom g, RqParams pa,
+                                                              RqParams pb, RqParams po, int32_t zp_c, int32_t up_a,
+                                                              int32_t up_b) {
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    int64_t ia = i, ib = i;
+    int ca = 0, cb = 0, co = 0;
+    if constexpr (!FLAT) {
+      ia = 0;
+      ib = 0;
+      int64_t r = i;
+      for (int d = g.nd - 1; d >= 0; --d) {
+        const int64_t q = r / g.shape[d];
+        const int64_t k = r - q * g.shape[d];
+        r = q;
+        ia += k * g.ls[d];
+        ib += k * g.rs[d];
+        if (d == g.lax) ca = (int)k;
+        if (d == g.rax) cb = (int)k;
+        if (d == g.oax) co = (int)k;
+      }
+    }
+    const int32_t x0 = (int32_t)a[ia], x1 = (int32_t)b[ib];
+    int32_t o;
+    if constexpr (OP == TK_QB_MUL) {
+      // mul.cc:77-101 (per-tensor) / :109-152 (per-channel): shifted operands, int32 product,
+      // requantized from s_a*s_b with zero point 0
+      const int32_t sa = (int32_t)((uint32_t)x0 - (uint32_t)(pa.zps ? pa.zps[ca] : pa.zp_in));
+      const int32_t sb = (int32_t)((uint32_t)x1 - (uint32_t)(pb.zps ? pb.zps[cb] : pb.zp_in));
+      o = rq_apply((int32_t)((uint32_t)sa * (uint32_t)sb), co, po);
+    } else {
+      const int32_t ra = up_a ? x0 : rq_apply(x0, ca, pa);
+      const int32_t rb = up_b ? x1 : rq_apply(x1, cb, pb);
+      if constexpr (OP == TK_QB_ADD) {
+        o = (int32_t)((uint32_t)ra + (uint32_t)rb - (uint32_t)zp_c);
+      } else {
+        o = (int32_t)((uint32_t)ra - (uint32_t)rb + (uint32_t)zp_c);
+      }
+    }
+    y[i] = (T)std::min<int64_t>(std::max<int64_t>(o, Lim<T>::lo), Lim<T>::hi);
+  }
+}
+
+int qnn_binary_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* y, const tk_qnn_binary_attrs* at,
+                    hipStream_t s) {
+  TK_CHECK_ARG(a && b && y && at, "null argument");
+  TK_CHECK_ARG(compact(a) && compact(b) && compact(y), "strided tensors are not supported");
+  TK_CHECK_ARG(dt_of(a) == dt_of(b) && dt_of(a) == dt_of(y), "dtype mismatch");
+  TK_CHECK_ARG(at->op >= TK_QB_ADD && at->op <= TK_QB_MUL, "bad op");
+  TK_CHECK_ARG(y->ndim <= 6 && a->ndim <= y->ndim && b->ndim <= y->ndim, "up to 6-D, operands no wider than the output");
+  BinGeom g{};
+  g.nd = y->ndim;
+  bool same = a->ndim == y->ndim && b->ndim == y->ndim;
+  {
+    int64_t sa = 1, sb = 1;
+    for (int d = y->ndim - 1; d >= 0; --d) {
+      g.shape[d] = y->shape[d];
+      const int da = d - (y->ndim - a->ndim), db = d - (y->ndim - b->ndim);
+      const int64_t ea = da >= 0 ? a->shape[da] : 1, eb = db >= 0 ? b->shape[db] : 1;
+      if ((ea != 1 && ea != y->shape[d]) || (eb != 1 && eb != y->shape[d])) {
+        set_error("tk_qnn_binary: operands do not broadcast to the output shape");
+        return TK_ERR_SHAPE;
+      }
+      same = same && ea == y->shape[d] && eb == y->shape[d];
+      g.ls[d] = ea == 1 ? 0 : sa;
+      g.rs[d] = eb == 1 ? 0 : sb;
+      sa *= ea;
+      sb *= eb;
+    }
+  }
+  // the output dimension a per-axis parameter set indexes (axis of the operand, right-aligned)
+  auto out_axis = [&](const tk_tensor* t, int axis) -> int {
+    if (t->ndim == 0) return -1;
+    const int ax = axis < 0 ? t->ndim + axis : axis;
+    if (ax < 0 || ax >= t->ndim || t->shape[ax] == 1) return -1;
+    return ax + (y->ndim - t->ndim);
+  };
+  RqParams pa = rq_params(at->lhs), pb = rq_params(at->rhs), po = rq_params(at->out);
+  const bool mul = at->op == TK_QB_MUL;
+  const bool axis_a = pa.zps || (!mul && !at->lhs_upcast && per_axis_mode(pa.mode));
+  const bool axis_b = pb.zps || (!mul && !at->rhs_upcast && per_axis_mode(pb.mode));
+  const bool axis_o = mul && per_axis_mode(po.mode);
+  TK_CHECK_ARG(!per_axis_mode(pa.mode) || pa.ms, "per-axis lhs plan needs multipliers");
+  TK_CHECK_ARG(!per_axis_mode(pb.mode) || pb.ms, "per-axis rhs plan needs multipliers");
+  TK_CHECK_ARG(!axis_o || po.ms, "per-axis output plan needs multipliers");
+  g.lax = axis_a ? out_axis(a, at->lhs.axis) : -1;
+  g.rax = axis_b ? out_axis(b, at->rhs.axis) : -1;
+  g.oax = axis_o ? out_axis(a, at->out.axis) : -1;
+  const bool flat = same && !axis_a && !axis_b && !axis_o;
+  const int64_t n = numel(y);
+  return dispatch_q(y, [&](auto tag) -> int {
+    using T = decltype(tag);
+    auto go = [&](auto op_tag, auto flat_tag) -> int {
+      constexpr int OP = decltype(op_tag)::value;
+      constexpr bool FLAT = decltype(flat_tag)::value;
+      hipLaunchKernelGGL((qnn_binary_kernel<T, OP, FLAT>), dim3(qgrid(n)), dim3(kQBlock), 0, s, (const T*)ptr(a),
+                         (const T*)ptr(b), (T*)ptr(y), n, g, pa, pb, po, at->output_zero_point, at->lhs_upcast,
+                         at->rhs_upcast);
+      TK_LAUNCH_CHECK();
+      return TK_OK;
+    };
+    using TF = std::true_type;
+    using FF = std::false_type;
+    switch (at->op) {
+      case TK_QB_ADD: return flat ? go(std::integral_constant<int, TK_QB_ADD>{}, TF{})
+                                  : go(std::integral_constant<int, TK_QB_ADD>{}, FF{});
+      case TK_QB_SUBTRACT: return flat ? go(std::integral_constant<int, TK_QB_SUBTRACT>{}, TF{})
+                                       : go(std::integral_constant<int, TK_QB_SUBTRACT>{}, FF{});
+      default: return flat ? go(std::integral_constant<int, TK_QB_MUL>{}, TF{})
+                           : go(std::integral_constant<int, TK_QB_MUL>{}, FF{});
+    }
+  });
+}
+
+// ---------------------------------------------------------------- qnn.concatenate
+// ConcatenateQnnCanonicalize (concatenate.cc:153-221): each input requantized (RequantizeLower, out
+// dtype = the input's: clip + cast) unless its params equal the output's, then concatenate.
+// One launch per input writes its slab: element i of the input (outer index o, offset r inside
+// the input's Ck * inner run) lands at o * (Ctot * inner) + Coff * inner + r.
+template <typename T>
+__global__ __launch_bounds__(kQBlock) void concat_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n,
+                                                          int64_t run, int64_t out_run, int64_t off, RqParams p,
+                                                          int32_t rq) {
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    const int64_t o = i / run;
+    const int64_t r = i - o * run;
+    T v = x[i];
+    if constexpr (sizeof(T) <= 4) {
+      if (rq) v = (T)std::min<int64_t>(std::max<int64_t>(rq_apply((int32_t)v, 0, p), Lim<T>::lo), Lim<T>::hi);
+    }
+    y[o * out_run + off + r] = v;
+  }
+}
+
+int qnn_concatenate_impl(const tk_tensor* const* xs, int n_in, tk_tensor* y, const tk_concat_attrs* a,
+                         hipStream_t s) {
+  TK_CHECK_ARG(xs && y && a && n_in >= 1 && n_in <= TK_CONCAT_MAX && a->n == n_in, "bad arguments");
+  TK_CHECK_ARG(compact(y) && is_integer(y), "integer output expected");
+  const int nd = y->ndim;
+  const int ax = a->axis < 0 ? nd + a->axis : a->axis;
+  TK_CHECK_ARG(nd >= 1 && ax >= 0 && ax < nd, "bad axis");
+  int64_t inner = 1, outer = 1;
+  for (int d = ax + 1; d < nd; ++d) inner *= y->shape[d];
+  for (int d = 0; d < ax; ++d) outer *= y->shape[d];
+  int64_t coff = 0;
+  for (int k = 0; k < n_in; ++k) {
+    const tk_tensor* x = xs[k];
+    TK_CHECK_ARG(x && compact(x) && x->ndim == nd && dt_of(x) == dt_of(y), "inputs must match the output's rank and dtype");
+    for (int d = 0; d < nd; ++d)
+      TK_CHECK_ARG(d == ax || x->shape[d] == y->shape[d], "inputs differ outside the concatenation axis");
+    TK_CHECK_ARG(!a->requant[k] || (!per_axis_mode(a->rq[k].mode) && elem_bytes(y) <= 4),
+                 "per-tensor requantize of 8/16/32-bit inputs only");
+    coff += x->shape[ax];
+  }
+  TK_CHECK_ARG(coff == y->shape[ax], "input sizes along the axis do not add up to the output's");
+  coff = 0;
+  for (int k = 0; k < n_in; ++k) {
+    const tk_tensor* x = xs[k];
+    const int64_t n = numel(x);
+    const int64_t run = x->shape[ax] * inner;
+    const RqParams p = rq_params(a->rq[k]);
+    if (n > 0) {
+      int rc = dispatch_q_any(y, [&](auto tag) -> int {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((concat_kernel<T>), dim3(qgrid(n)), dim3(kQBlock), 0, s, (const T*)ptr(x), (T*)ptr(y), n,
+                           run, y->shape[ax] * inner, coff * inner, p, a->requant[k]);
+        TK_LAUNCH_CHECK();
+        return TK_OK;
+      });
+      if (rc) return rc;
+    }
+    coff += x->shape[ax];
+  }
+  (void)outer;
+  return TK_OK;
+}
+
+// ---------------------------------------------------------------- transpose
+struct TransGeom {
+  int32_t nd;
+  int64_t shape[6];   // output shape
+  int64_t src[6];     // input element stride of each output dimension
+};
+
+template <typename T>
+__global__ __launch_bounds__(kQBlock) void transpose_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n,
+                                                             TransGeom g) {
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    int64_t r = i, si = 0;
+    for (int d = g.nd - 1; d >= 0; --d) {
+      const int64_t q = r / g.shape[d];
+      si += (r - q * g.shape[d]) * g.src[d];
+      r = q;
+    }
+    y[i] = x[si];
+  }
+}
+
+int transpose_impl(const tk_tensor* x, tk_tensor* y, const tk_transpose_attrs* a, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y) && x->ndim == a->ndim && y->ndim == a->ndim && a->ndim >= 1 && a->ndim <= 6,
+               "bad tensors");
+  TK_CHECK_ARG(elem_bytes(x) == elem_bytes(y) && x->dtype.code == y->dtype.code, "dtype mismatch");
+  TransGeom g{};
+  g.nd = a->ndim;
+  int64_t st[6];
+  st[a->ndim - 1] = 1;
+  for (int d = a->ndim - 2; d >= 0; --d) st[d] = st[d + 1] * x->shape[d + 1];
+  int seen = 0;
+  for (int k = 0; k < a->ndim; ++k) {
+    const int p = a->perm[k];
+    TK_CHECK_ARG(p >= 0 && p < a->ndim && !(seen & (1 << p)), "perm is not a permutation");
+    seen |= 1 << p;
+    TK_CHECK_ARG(y->shape[k] == x->shape[p], "output shape is not the permuted input shape");
+    g.shape[k] = y->shape[k];
+    g.src[k] = st[p];
+  }
+  const int64_t n = numel(x);
+  if (n == 0) return TK_OK;
+  auto go = [&](auto tag) -> int {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((transpose_kernel<T>), dim3(qgrid(n)), dim3(kQBlock), 0, s, (const T*)ptr(x), (T*)ptr(y), n, g);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  };
+  switch (elem_bytes(x)) {
+    case 1: return go((uint8_t)0);
+    case 2: return go((uint16_t)0);
+    case 4: return go((uint32_t)0);
+    case 8: return go((uint64_t)0);
+  }
+  set_error("tk_transpose: 1, 2, 4 or 8-byte elements");
+  return TK_ERR_DTYPE;
+}
+
+}  // namespace tk
+
+extern "C" {
+
+int tk_qnn_quantize(const tk_tensor* data, tk_tensor* out, const tk_qparams_attrs* attrs, void* stream) {
+  return tk::qnn_quantize_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_dequantize(const tk_tensor* data, tk_tensor* out, const tk_qparams_attrs* attrs, void* stream) {
+  return tk::qnn_dequantize_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_binary(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const tk_qnn_binary_attrs* attrs,
+                  void* stream) {
+  return tk::qnn_binary_impl(lhs, rhs, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_concatenate(const tk_tensor* const* inputs, int n, tk_tensor* out, const tk_concat_attrs* attrs,
+                       void* stream) {
+  return tk::qnn_concatenate_impl(inputs, n, out, attrs, tk::as_stream(stream));
+}
+int tk_transpose(const tk_tensor* data, tk_tensor* out, const tk_transpose_attrs* attrs, void* stream) {
+  return tk::transpose_impl(data, out, attrs, tk::as_stream(stream));
+}
+
+}  // extern "C"

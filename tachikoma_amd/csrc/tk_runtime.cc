@@ -7,6 +7,7 @@
 // flat node list on one HIP stream and, when asked, copies every node output to
 // host memory on a second stream, each copy gated by an event recorded right
 // after the node, so the PCIe transfer of node i overlaps the kernels of nodes > i.
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -34,6 +35,7 @@ int postops_impl(const tk_tensor* acc, const tk_tensor* sum_src, tk_tensor* y, c
                  hipStream_t s);
 int digest_impl(const void* data, int64_t nbytes, uint64_t* out, hipStream_t s);
 int host_copy_impl(const void* const* src, void* const* dst, const int64_t* bytes, int n, hipStream_t s);
+int pack_records_impl(const void* table, int nrec, int64_t blocks, void* mirror, hipStream_t s);
 int ewise_impl(const tk_tensor* x, const tk_tensor* r, tk_tensor* y, const tk_ewise_attrs* a, hipStream_t s);
 int conv2d_f32_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, const tk_conv2d_attrs* a, hipStream_t s);
 int dense_f32_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, hipStream_t s);
@@ -55,8 +57,18 @@ int conv2d_block_impl(const tk_tensor* data, const void* shadow, const tk_tensor
                       const tk_block_attrs* attrs, void* scratch, void* shadow_out, hipStream_t s);
 int dense_block_impl(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,
                      int n_outs, const tk_block_attrs* attrs, void* workspace, hipStream_t s);
+int qnn_quantize_impl(const tk_tensor* x, tk_tensor* y, const tk_qparams_attrs* a, hipStream_t s);
+int qnn_dequantize_impl(const tk_tensor* x, tk_tensor* y, const tk_qparams_attrs* a, hipStream_t s);
+int qnn_binary_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* y, const tk_qnn_binary_attrs* at,
+                    hipStream_t s);
+int qnn_concatenate_impl(const tk_tensor* const* xs, int n_in, tk_tensor* y, const tk_concat_attrs* a,
+                         hipStream_t s);
+int transpose_impl(const tk_tensor* x, tk_tensor* y, const tk_transpose_attrs* a, hipStream_t s);
 int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
                             int32_t* algos, int max_algos);
+
+// run_packed's "nothing to capture, run the plain graph" answer (not an error code)
+constexpr int TK_OK_RUN = 1;
 
 // A tensor descriptor owned by the module (shape copied).
 struct OwnedTensor {
@@ -139,12 +151,67 @@ static int run_node(Node& n, hipStream_t s) {
       return dense_f32_impl(i0, i1, o, s);
     case TK_NODE_PAD:
       return pad_impl(i0, o, &d.attrs.pad, s);
+    case TK_NODE_QUANTIZE:
+      return qnn_quantize_impl(i0, o, &d.attrs.qparams, s);
+    case TK_NODE_DEQUANTIZE:
+      return qnn_dequantize_impl(i0, o, &d.attrs.qparams, s);
+    case TK_NODE_QNN_BINARY:
+      return qnn_binary_impl(i0, i1, o, &d.attrs.qnn_binary, s);
+    case TK_NODE_CONCAT: {
+      const tk_tensor* xs[TK_MAX_NODE_INPUTS];
+      for (int k = 0; k < d.n_inputs; ++k) xs[k] = &n.in[k].t;
+      return qnn_concatenate_impl(xs, d.n_inputs, o, &d.attrs.concat, s);
+    }
+    case TK_NODE_TRANSPOSE:
+      return transpose_impl(i0, o, &d.attrs.transpose, s);
   }
   set_error("tk_module: unknown node kind " + std::to_string(d.kind));
   return TK_ERR_INVALID_ARG;
 }
 
 }  // namespace tk
+
+// Packed trace capture for tk_module_run_graph (the default graph copy mode): the node outputs that
+// have host destinations are gathered, chunk by chunk, into a device mirror of the host image range
+// they span (header bytes included, loaded once from the host image), and each chunk is copied to
+// host memory by ONE host-issued hipMemcpyAsync gated on an external event-record node after the
+// chunk's pack kernel.  Two mirrors alternate between runs, so a run's kernels overlap the previous
+// run's copies (only the pack into a mirror waits for that mirror's last copies).
+struct PackRecHost {
+  const void* src;
+  int64_t dst, bytes, first_blk;
+};
+struct PackPlan {
+  std::vector<void*> dst;         // host_dst this plan was built for (the cache key)
+  char* host_lo = nullptr;        // mirrored host range [host_lo, host_lo + span)
+  int64_t span = 0;
+  void* mirror[2] = {nullptr, nullptr};
+  struct Chunk {
+    int after_node;               // pack + event after this node
+    int64_t off, len;             // mirror range copied to host_lo + off
+    int64_t table_off;            // first entry in `table`
+    int n_rec;
+    int64_t blocks;
+  };
+  std::vector<Chunk> chunks;
+  void* table = nullptr;          // device PackRec entries of every chunk
+  std::vector<hipEvent_t> ev[2];  // per chunk, external event-record nodes of graph[m]
+  hipEvent_t mirror_done[2] = {nullptr, nullptr};
+  bool mirror_used[2] = {false, false};
+  hipGraph_t g[2] = {nullptr, nullptr};
+  hipGraphExec_t ge[2] = {nullptr, nullptr};
+  int next = 0;
+  ~PackPlan() {
+    for (int m = 0; m < 2; ++m) {
+      if (ge[m]) (void)hipGraphExecDestroy(ge[m]);
+      if (g[m]) (void)hipGraphDestroy(g[m]);
+      for (auto e : ev[m]) (void)hipEventDestroy(e);
+      if (mirror_done[m]) (void)hipEventDestroy(mirror_done[m]);
+      if (mirror[m]) (void)hipFree(mirror[m]);
+    }
+    if (table) (void)hipFree(table);
+  }
+};
 
 struct tk_module {
   std::vector<tk::Node> nodes;
@@ -156,6 +223,7 @@ struct tk_module {
   // would mix two runs in one trace image (write-after-read across streams).
   hipEvent_t capture_done = nullptr;
   bool capture_recorded = false;
+  bool capture_plain = false;  // the last capture copied from the record buffers themselves
   bool profiling = false;
   bool have_times = false;
   // tk_module_run_graph: the whole run (every node, and the copies when capturing) as one HIP
@@ -178,12 +246,18 @@ struct tk_module {
   // memcpy nodes in this many parallel chains (1..4): 4 measured 53.4 GB/s per traced ResNet-50
   // step against 52.7 for one chain (profiles/r03s_graph_copy_chains.txt)
   int graph_copy_chains = 4;
+  // packed capture (default): records gathered into device mirrors, copied in this many chunks
+  bool graph_packed = true;
+  int pack_chunks = 8;
+  std::vector<std::unique_ptr<PackPlan>> packs;
   void drop_graph() {
     for (Graph& x : graphs) {
       if (x.ge) (void)hipGraphExecDestroy(x.ge);
       if (x.g) (void)hipGraphDestroy(x.g);
     }
     graphs.clear();
+    if (!packs.empty()) (void)hipDeviceSynchronize();  // their mirrors may still be copied from
+    packs.clear();
   }
   ~tk_module() {
     drop_graph();
@@ -418,9 +492,10 @@ int tk_module_node_times(tk_module* mod, float* node_ms) {
 // recorded after node i (shared by tk_module_run and the graph capture of tk_module_run_graph).
 static int enqueue_nodes(tk_module* mod, hipStream_t s, hipStream_t cs, void* const* host_dst, bool capture,
                          bool profiling, bool copy_kernels = false, hipStream_t const* chains = nullptr,
-                         int n_chains = 1) {
+                         int n_chains = 1, int* n_copied = nullptr) {
   if (profiling) TK_HIP(hipEventRecord(mod->prof[0], s));
   int copied = 0;  // captured nodes so far: node copies rotate over the chains
+  if (n_copied) *n_copied = 0;
   for (size_t i = 0; i < mod->nodes.size(); ++i) {
     tk::Node& n = mod->nodes[i];
     int rc = tk::run_node(n, s);
@@ -434,7 +509,9 @@ static int enqueue_nodes(tk_module* mod, hipStream_t s, hipStream_t cs, void* co
       bool any = false;
       for (int k = 0; k < n.desc.n_outputs; ++k) any |= dst[k] != nullptr;
       if (any) {
-        if (chains) cs = chains[copied++ % n_chains];
+        if (chains) cs = chains[copied % n_chains];
+        ++copied;
+        if (n_copied) *n_copied = copied;
         TK_HIP(hipEventRecord(mod->done[i], s));
         TK_HIP(hipStreamWaitEvent(cs, mod->done[i], 0));
         if (copy_kernels) {
@@ -471,21 +548,206 @@ int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* cons
     // the next run / input write waits for these copies (wait_capture)
     TK_HIP(hipEventRecord(mod->capture_done, cs));
     mod->capture_recorded = true;
+    mod->capture_plain = true;
   }
   mod->have_times = mod->profiling;
   return TK_OK;
 }
 
 int tk_module_set_graph_copies(tk_module* mod, int copy_kernels) {
-  if (!mod) {
-    tk::set_error("tk_module_set_graph_copies: null module");
+  if (!mod || copy_kernels < 0 || copy_kernels > 5) {
+    tk::set_error("tk_module_set_graph_copies: invalid argument");
     return TK_ERR_INVALID_ARG;
   }
+  const bool packed = copy_kernels == 0;
   const bool kern = copy_kernels == 1;
-  const int chains = copy_kernels == 5 ? 1 : copy_kernels >= 2 ? std::min(copy_kernels, 4) : copy_kernels == 0 ? 4 : 1;
-  if (mod->graph_copy_kernels != kern || mod->graph_copy_chains != chains) mod->drop_graph();
+  const int chains = copy_kernels == 5 ? 1 : copy_kernels >= 2 ? std::min(copy_kernels, 4) : 1;
+  if (mod->graph_packed != packed || mod->graph_copy_kernels != kern || mod->graph_copy_chains != chains)
+    mod->drop_graph();
+  mod->graph_packed = packed;
   mod->graph_copy_kernels = kern;
   mod->graph_copy_chains = chains;
+  return TK_OK;
+}
+
+int tk_module_set_trace_chunks(tk_module* mod, int chunks) {
+  if (!mod || chunks < 1 || chunks > 256) {
+    tk::set_error("tk_module_set_trace_chunks: chunks must be 1..256");
+    return TK_ERR_INVALID_ARG;
+  }
+  if (mod->pack_chunks != chunks) mod->drop_graph();
+  mod->pack_chunks = chunks;
+  return TK_OK;
+}
+
+// Builds the packed-capture plan for host destinations `dst`: the mirrored range, the chunks (cut
+// at node boundaries where every record below the cut is written), the device pack tables, two
+// mirrors loaded with the host image's bytes, and one graph per mirror.
+static int build_pack_plan(tk_module* mod, const std::vector<void*>& dst, PackPlan** out) {
+  auto plan = std::make_unique<PackPlan>();
+  plan->dst = dst;
+  struct Rec {
+    char* host;
+    const void* src;
+    int64_t bytes;
+    int node;
+  };
+  std::vector<Rec> recs;
+  for (size_t i = 0; i < mod->nodes.size(); ++i) {
+    const tk::Node& n = mod->nodes[i];
+    for (int k = 0; k < n.desc.n_outputs; ++k) {
+      char* h = (char*)dst[i * TK_MAX_NODE_OUTPUTS + k];
+      const int64_t nb = tk::nbytes(&n.out[k].t);
+      if (h && nb > 0) recs.push_back({h, tk::ptr(&n.out[k].t), nb, (int)i});
+    }
+  }
+  if (recs.empty()) {
+    *out = nullptr;
+    return TK_OK;
+  }
+  std::sort(recs.begin(), recs.end(), [](const Rec& a, const Rec& b) { return a.host < b.host; });
+  for (size_t r = 0; r + 1 < recs.size(); ++r)
+    if (recs[r].host + recs[r].bytes > recs[r + 1].host) {
+      tk::set_error("tk_module_run_graph: overlapping record destinations");
+      return TK_ERR_INVALID_ARG;
+    }
+  plan->host_lo = recs.front().host;
+  plan->span = recs.back().host + recs.back().bytes - plan->host_lo;
+  // after node i, every record below complete_upto[i] (host order) is written
+  const int nn = (int)mod->nodes.size();
+  std::vector<int64_t> complete_upto(nn);
+  {
+    int r = 0;
+    int last_node = -1;  // max producer node among records [0, r)
+    std::vector<int> prefix_max(recs.size());
+    for (size_t q = 0; q < recs.size(); ++q) prefix_max[q] = std::max(q ? prefix_max[q - 1] : -1, recs[q].node);
+    for (int i = 0; i < nn; ++i) {
+      while (r < (int)recs.size() && prefix_max[r] <= i) ++r;
+      complete_upto[i] = r == (int)recs.size() ? plan->span : recs[r].host - plan->host_lo;
+      (void)last_node;
+    }
+  }
+  const int64_t target = std::max<int64_t>(1, (plan->span + mod->pack_chunks - 1) / mod->pack_chunks);
+  std::vector<PackRecHost> table;
+  int64_t cut = 0;
+  size_t next_rec = 0;
+  for (int i = 0; i < nn; ++i) {
+    const int64_t upto = complete_upto[i];
+    if (upto <= cut) continue;
+    if (upto - cut < target && upto < plan->span) continue;
+    PackPlan::Chunk c{i, cut, upto - cut, (int64_t)table.size(), 0, 0};
+    int64_t blocks = 0;
+    while (next_rec < recs.size() && recs[next_rec].host - plan->host_lo < upto) {
+      const Rec& rc = recs[next_rec++];
+      const int64_t off = rc.host - plan->host_lo;
+      const int64_t a0 = off & ~(int64_t)15;
+      const int64_t nblk = (off + rc.bytes - a0 + 256 * 16 - 1) / (256 * 16);
+      table.push_back({rc.src, off, rc.bytes, blocks});
+      blocks += nblk;
+      ++c.n_rec;
+    }
+    c.blocks = blocks;
+    plan->chunks.push_back(c);
+    cut = upto;
+  }
+  if (cut != plan->span || next_rec != recs.size()) {
+    tk::set_error("tk_module_run_graph: pack plan does not cover every record");
+    return TK_ERR_INVALID_ARG;
+  }
+  TK_HIP(hipMalloc(&plan->table, table.size() * sizeof(PackRecHost)));
+  TK_HIP(hipMemcpy(plan->table, table.data(), table.size() * sizeof(PackRecHost), hipMemcpyHostToDevice));
+  for (int m = 0; m < 2; ++m) {
+    // the mirror holds the image's bytes between records (headers) from the start
+    TK_HIP(hipMalloc(&plan->mirror[m], (size_t)plan->span + 16));
+    TK_HIP(hipMemcpy(plan->mirror[m], plan->host_lo, (size_t)plan->span, hipMemcpyHostToDevice));
+    TK_HIP(hipEventCreateWithFlags(&plan->mirror_done[m], hipEventDisableTiming));
+    plan->ev[m].resize(plan->chunks.size(), nullptr);
+    for (auto& e : plan->ev[m]) TK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  if (!mod->cap_s) TK_HIP(hipStreamCreateWithFlags(&mod->cap_s, hipStreamNonBlocking));
+  for (int m = 0; m < 2; ++m) {
+    hipStream_t qs = mod->cap_s;
+    TK_HIP(hipStreamBeginCapture(qs, hipStreamCaptureModeThreadLocal));
+    int rc = TK_OK;
+    size_t c = 0;
+    for (int i = 0; i < nn && rc == TK_OK; ++i) {
+      rc = tk::run_node(mod->nodes[i], qs);
+      if (rc) {
+        tk::set_error("node " + std::to_string(i) + ": " + tk_last_error());
+        break;
+      }
+      while (c < plan->chunks.size() && plan->chunks[c].after_node == i && rc == TK_OK) {
+        const PackPlan::Chunk& ch = plan->chunks[c];
+        rc = tk::pack_records_impl((const char*)plan->table + ch.table_off * sizeof(PackRecHost), ch.n_rec, ch.blocks,
+                                   plan->mirror[m], qs);
+        if (rc == TK_OK && hipEventRecordWithFlags(plan->ev[m][c], qs, hipEventRecordExternal) != hipSuccess) {
+          tk::set_error("tk_module_run_graph: event record in capture failed");
+          rc = TK_ERR_HIP;
+        }
+        ++c;
+      }
+    }
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(qs, &g);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    if (e != hipSuccess || !g) {
+      (void)hipGetLastError();
+      tk::set_error(std::string("tk_module_run_graph: stream capture failed: ") + hipGetErrorString(e));
+      return TK_ERR_HIP;
+    }
+    plan->g[m] = g;
+    e = hipGraphInstantiate(&plan->ge[m], g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+      tk::set_error(std::string("tk_module_run_graph: instantiate failed: ") + hipGetErrorString(e));
+      return TK_ERR_HIP;
+    }
+  }
+  *out = plan.release();
+  return TK_OK;
+}
+
+// One packed traced run: the graph of mirror m (kernels, pack kernels, event records) on s, then the
+// chunk copies on cs, each after its event.
+static int run_packed(tk_module* mod, hipStream_t s, hipStream_t cs, void* const* host_dst) {
+  const size_t nd = mod->nodes.size() * TK_MAX_NODE_OUTPUTS;
+  std::vector<void*> dst(host_dst, host_dst + nd);
+  PackPlan* plan = nullptr;
+  for (auto& p : mod->packs)
+    if (p->dst == dst) plan = p.get();
+  if (!plan) {
+    if (mod->packs.size() >= 2) {  // keep the newest (a file sink alternates two images)
+      TK_HIP(hipDeviceSynchronize());
+      mod->packs.erase(mod->packs.begin());
+    }
+    PackPlan* built = nullptr;
+    int rc = build_pack_plan(mod, dst, &built);
+    if (rc) return rc;
+    if (!built) return tk::TK_OK_RUN;  // nothing to capture
+    mod->packs.emplace_back(built);
+    plan = built;
+  }
+  // a previous per-record (unpacked) capture still reads the record buffers on cs
+  if (mod->capture_recorded && mod->capture_plain) TK_HIP(hipStreamWaitEvent(s, mod->capture_done, 0));
+  const int m = plan->next;
+  plan->next ^= 1;
+  // the pack into mirror m waits for that mirror's last copies (two runs ago); the records the
+  // kernels overwrite are only read by the packs of the previous launch on the same stream
+  if (plan->mirror_used[m]) TK_HIP(hipStreamWaitEvent(s, plan->mirror_done[m], 0));
+  TK_HIP(hipGraphLaunch(plan->ge[m], s));
+  for (size_t c = 0; c < plan->chunks.size(); ++c) {
+    const PackPlan::Chunk& ch = plan->chunks[c];
+    TK_HIP(hipStreamWaitEvent(cs, plan->ev[m][c], 0));
+    TK_HIP(hipMemcpyAsync(plan->host_lo + ch.off, (char*)plan->mirror[m] + ch.off, (size_t)ch.len,
+                          hipMemcpyDeviceToHost, cs));
+  }
+  TK_HIP(hipEventRecord(plan->mirror_done[m], cs));
+  plan->mirror_used[m] = true;
+  TK_HIP(hipEventRecord(mod->capture_done, cs));
+  mod->capture_recorded = true;
+  mod->capture_plain = false;
   return TK_OK;
 }
 
@@ -498,6 +760,14 @@ int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void
   hipStream_t s = tk::as_stream(stream);
   hipStream_t cs = tk::as_stream(capture_stream);
   const bool capture = capture_stream && host_dst;
+  if (capture && mod->graph_packed) {
+    const int rc = run_packed(mod, s, cs, host_dst);
+    if (rc != tk::TK_OK_RUN) {
+      mod->have_times = false;
+      return rc;
+    }
+    // no record has a host destination: an ordinary graph run below
+  }
   const size_t nd = capture ? mod->nodes.size() * TK_MAX_NODE_OUTPUTS : 0;
   std::vector<void*> dst(nd);
   for (size_t i = 0; i < nd; ++i) dst[i] = host_dst[i];
@@ -526,8 +796,12 @@ int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void
     // capture: the node loop on qs, the copies forked onto qcs through the per-node events and
     // joined back into qs at the end, so that one launch covers the run and its copies
     TK_HIP(hipStreamBeginCapture(qs, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_nodes(mod, qs, qcs, host_dst, capture, false, mod->graph_copy_kernels, chains, nch);
-    for (int c = 0; c < nch && rc == TK_OK && capture; ++c) {
+    int copied = 0;
+    int rc = enqueue_nodes(mod, qs, qcs, host_dst, capture, false, mod->graph_copy_kernels, chains, nch, &copied);
+    // a chain enters the capture only once a node's copy was routed to it: join only those
+    // (joining an idle chain would record on a stream that is not capturing)
+    const int joined = std::min(copied, nch);
+    for (int c = 0; c < joined && rc == TK_OK && capture; ++c) {
       // every copy chain joins back into qs (one event per join: record, then wait, in order)
       if (hipEventRecord(mod->graph_join, chains[c]) != hipSuccess || hipStreamWaitEvent(qs, mod->graph_join, 0) != hipSuccess) {
         tk::set_error("tk_module_run_graph: joining the capture streams failed");
@@ -575,6 +849,7 @@ int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void
     // synchronisation) sees the copies complete
     TK_HIP(hipEventRecord(mod->capture_done, s));
     mod->capture_recorded = true;
+    mod->capture_plain = true;
     TK_HIP(hipStreamWaitEvent(cs, mod->capture_done, 0));
   }
   mod->have_times = false;
@@ -647,6 +922,31 @@ static std::string tune_key(const tk::Node& n) {
   return k;
 }
 
+int tk_module_set_node_algo(tk_module* mod, int node, int algo) {
+  if (!mod || node < 0 || node >= (int)mod->nodes.size()) {
+    tk::set_error("tk_module_set_node_algo: bad node");
+    return TK_ERR_INVALID_ARG;
+  }
+  tk::Node& n = mod->nodes[node];
+  if (n.desc.kind != TK_NODE_CONV_BLOCK) {
+    tk::set_error("tk_module_set_node_algo: node " + std::to_string(node) + " is not a conv block");
+    return TK_ERR_INVALID_ARG;
+  }
+  if (algo != 0) {
+    std::vector<int32_t> algos(256, -1);
+    const int total = tk_conv2d_block_algos(&n.in[0].t, &n.in[1].t, &n.desc.attrs.block, algos.data(), 256);
+    if (total < 0) return total;
+    if (std::find(algos.begin(), algos.begin() + std::min(total, 256), algo) == algos.begin() + std::min(total, 256)) {
+      tk::set_error("tk_module_set_node_algo: algo " + std::to_string(algo) + " is not a candidate of node " +
+                    std::to_string(node) + " (tk_conv2d_block_algos)");
+      return TK_ERR_INVALID_ARG;
+    }
+  }
+  if (n.desc.attrs.block.algo != algo) mod->drop_graph();  // captured graphs hold the old kernel
+  n.desc.attrs.block.algo = algo;
+  return TK_OK;
+}
+
 int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, int32_t* algo_out, float* us_out) {
   if (!mod || max_candidates < 1 || reps < 1) {
     tk::set_error("tk_module_tune: invalid argument");
@@ -693,6 +993,11 @@ int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, i
       for (int c = 0; c < std::min(total, max_candidates) && rc == TK_OK; ++c) {
         node.desc.attrs.block.algo = r.algos[c];
         rc = tk::run_node(node, s);  // warm-up (and the image-tile kernel's LDS attribute)
+        if (rc == TK_ERR_INVALID_ARG) {
+          // a candidate this node's arguments rule out (refused before any launch): skip it
+          rc = TK_OK;
+          continue;
+        }
         if (rc) break;
         if (hipEventRecord(e0, s) != hipSuccess) rc = TK_ERR_HIP;
         for (int k = 0; k < reps && rc == TK_OK; ++k) rc = tk::run_node(node, s);
@@ -701,7 +1006,7 @@ int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, i
         if (rc == TK_OK && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = TK_ERR_HIP;
         if (rc) break;
         r.us[c] = ms * 1e3f / (float)reps;
-        if (c == 0 || r.us[c] < best_us) best_us = r.us[c], r.best = r.algos[c];
+        if (best_us <= 0.0f || r.us[c] < best_us) best_us = r.us[c], r.best = r.algos[c];
       }
       if (rc) {
         node.desc.attrs.block.algo = 0;

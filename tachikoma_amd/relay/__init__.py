@@ -1,10 +1,11 @@
 """Relay-compatible front door: ``relay.var/const``, ``relay.qnn.op.*``, ``relay.nn.*`` and
 ``relay.build`` (python/tvm/relay/build_module.py:409) targeting the MI355X engine."""
 from . import qnn  # noqa: F401
-from .expr import (Call, Constant, Expr, Function, IRModule, TensorType, Var, const, free_vars,  # noqa: F401
-                   post_order, var)
+from .expr import (Call, Constant, Expr, Function, IRModule, TensorType, Tuple, Var, const,  # noqa: F401
+                   free_vars, post_order, var)
 from .op import (add, avg_pool2d, batch_flatten, bias_add, cast, cast_hint, clip, fixed_point_multiply,  # noqa: F401
-                 global_avg_pool2d, left_shift, max_pool2d, multiply, relu, reshape, right_shift, round, stop_fusion)
+                 global_avg_pool2d, left_shift, max_pool2d, multiply, relu, reshape, right_shift, round, stop_fusion,
+                 transpose)
 from . import op as _op
 from .parser import ParseError, astext, fromtext, parse  # noqa: F401  (tvm.parser.parse / fromtext)
 from . import contrib  # noqa: F401,E402  (relay.op.contrib.tachikoma analogue: contrib.tachikoma)

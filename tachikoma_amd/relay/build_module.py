@@ -22,7 +22,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import numpy as np
 
 from .. import _lib
-from .expr import Call, Constant, Expr, Function, IRModule, Var, post_order
+from .expr import Call, Constant, Expr, Function, IRModule, Tuple, Var, post_order
 from .op import INT_DTYPES
 
 TARGETS = ("mi355x", "rocm", "hip", "gfx950")
@@ -169,8 +169,8 @@ def lower(mod, params: Optional[Dict[str, Any]] = None) -> Plan:
                 plist.append(t)
             else:
                 inputs.append(t)
-        elif isinstance(node, Constant):
-            continue
+        elif isinstance(node, (Constant, Tuple)):
+            continue  # a tuple is no op: no record, no symbol name (expr.Tuple)
         elif isinstance(node, Call):
             name = f"%{counter}"
             counter += 1
@@ -192,6 +192,106 @@ def _tensor_args(call: Call, k: int, names) -> List[str]:
     return out
 
 
+def _is_equal_scalar(x: np.ndarray, y: np.ndarray) -> bool:
+    """IsEqualScalar (src/relay/qnn/utils.h): both rank-0, same dtype, same bytes."""
+    x, y = np.asarray(x), np.asarray(y)
+    return x.ndim == 0 and y.ndim == 0 and x.dtype == y.dtype and x.tobytes() == y.tobytes()
+
+
+def _norm_axis(axis: int, nd: int) -> int:
+    return axis + nd if axis < 0 else axis if nd else 0
+
+
+def _rq_side(a: Dict[str, Any], consts: Dict[str, np.ndarray], side: str, s_in, zp_in, s_out, zp_out, axis: int,
+             nd: int, rounding: str) -> None:
+    """One requantize plan (RequantizeLowerInt constants: mode, multiplier(s), shift(s), zero
+    point(s)) into attrs ``{side}_*`` and per-axis consts ``{side}_multipliers`` / ``_shifts`` /
+    ``_zero_points``.  ``axis`` indexes the operand (rank ``nd``)."""
+    s_in = np.asarray(s_in, np.float32)
+    zp_in = np.asarray(zp_in, np.int32)
+    mode, ms, ss = requantize_plan(s_in if s_in.ndim else np.float32(s_in), np.float32(s_out), rounding)
+    a[f"{side}_mode"] = mode
+    a[f"{side}_axis"] = _norm_axis(axis, nd)
+    if mode >= _lib.TK_RQ_AXIS_UPWARD:
+        consts[f"{side}_multipliers"], consts[f"{side}_shifts"] = ms, ss
+        a[f"{side}_multiplier"] = a[f"{side}_shift"] = 0
+    else:
+        a[f"{side}_multiplier"], a[f"{side}_shift"] = int(ms[0]), int(ss[0])
+    if zp_in.ndim == 0:
+        a[f"{side}_zero_point"] = int(zp_in)
+    else:
+        a[f"{side}_zero_point"] = 0
+        consts[f"{side}_zero_points"] = zp_in.reshape(-1).astype(np.int32)
+    a["output_zero_point"] = int(np.asarray(zp_out))
+
+
+def _qnn_rounding(a: Dict[str, Any]) -> str:
+    """The requantize rounding a QNN canonicalization's inner ``Requantize`` gets: the
+    requantize_config in effect when the op was built, else UPWARD (qnn/utils.h:106-122)."""
+    r = a.pop("cfg_rounding", None) or "UPWARD"
+    cd = a.pop("cfg_compute_dtype", None) or "int64"
+    if cd != "int64":
+        raise UnsupportedError(f"compute_dtype={cd}: only the pinned integer (int64) requantize path is implemented")
+    return r
+
+
+def _lower_binary(call: Call, a: Dict[str, Any], consts: Dict[str, np.ndarray]) -> None:
+    """qnn.add / qnn.subtract (RequantizeOrUpcast of both sides, op_common.h:193-207) and qnn.mul
+    (mul.cc:43-159) into requantize plans for the device's tk_qnn_binary."""
+    op = call.op
+    lhs, rhs = call.args[0], call.args[1]
+    vals = [_scalar(call.args[i], f"{op} param") for i in range(2, 8)]
+    ls, lz, rs, rz, os_, oz = [np.asarray(v) for v in vals]
+    rounding = _qnn_rounding(a)
+    a["rounding"] = rounding
+    ln, rn = len(lhs.shape), len(rhs.shape)
+    if op in ("qnn.add", "qnn.subtract"):
+        for side, s_, z_, ax, nd in (("lhs", ls, lz, a["lhs_axis"], ln), ("rhs", rs, rz, a["rhs_axis"], rn)):
+            up = _is_equal_scalar(s_.astype(np.float32), os_.astype(np.float32)) and \
+                _is_equal_scalar(z_.astype(np.int32), oz.astype(np.int32))
+            a[f"{side}_upcast"] = int(up)
+            if up:
+                a.update({f"{side}_mode": 0, f"{side}_multiplier": 0, f"{side}_shift": 0,
+                          f"{side}_zero_point": int(z_), f"{side}_axis": 0})
+            else:
+                _rq_side(a, consts, side, s_, z_, os_, oz, ax, nd, rounding)
+        a["output_zero_point"] = int(oz)
+        # scalar floats for the fused residual-join kernels (add_block / conv-block join)
+        a.update(lhs_scale=float(np.float32(ls)) if ls.ndim == 0 else None,
+                 rhs_scale=float(np.float32(rs)) if rs.ndim == 0 else None, output_scale=float(np.float32(os_)))
+        a["per_tensor"] = int(not consts and lhs.shape == rhs.shape == call.shape)
+        return
+    # qnn.mul
+    a["lhs_upcast"] = a["rhs_upcast"] = 0
+    if ls.ndim == 0 and rs.ndim == 0:
+        # per-tensor: Requantize(Q', s_a * s_b (a float32 product), 0 -> s_out, zp_out); vector zero
+        # points are subtracted as written, i.e. broadcast along the operand's last axis
+        for side, z_, x in (("lhs", lz, lhs), ("rhs", rz, rhs)):
+            if z_.ndim and (not x.shape or z_.reshape(-1).shape[0] != x.shape[-1]):
+                raise UnsupportedError(f"qnn.mul: a {side} zero point of shape {z_.shape} for {x.shape}")
+        new_scale = np.float32(np.float32(ls) * np.float32(rs))
+        out_axis = -1
+    else:
+        if a["lhs_axis"] != a["rhs_axis"]:
+            raise UnsupportedError("qnn.mul: lhs_axis and rhs_axis differ (mul.cc:154-156)")
+        if ls.ndim == 0 or rs.ndim == 0 or ls.size != rs.size:
+            raise UnsupportedError("qnn.mul: per-channel scales on both sides, of equal length")
+        new_scale = np.array([float(np.float64(x) * np.float64(y)) for x, y in
+                              zip(ls.reshape(-1), rs.reshape(-1))], dtype=np.float32)
+        out_axis = a["lhs_axis"]
+    for side, z_, ax, nd in (("lhs", lz, a["lhs_axis"] if ls.ndim else -1, ln),
+                             ("rhs", rz, a["rhs_axis"] if ls.ndim else -1, rn)):
+        a[f"{side}_axis"] = _norm_axis(ax, nd)
+        a[f"{side}_mode"], a[f"{side}_multiplier"], a[f"{side}_shift"] = 0, 0, 0
+        if z_.ndim == 0:
+            a[f"{side}_zero_point"] = int(z_)
+        else:
+            a[f"{side}_zero_point"] = 0
+            consts[f"{side}_zero_points"] = z_.reshape(-1).astype(np.int32)
+    _rq_side(a, consts, "out", new_scale, np.int32(0), os_, oz, out_axis, ln, rounding)
+    a["per_tensor"] = 0
+
+
 def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
     op = call.op
     out = PlanTensor(name, call.shape, call.dtype)
@@ -208,7 +308,10 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
             a["kernel_zero_point"] = int(zw)
         else:
             a["kernel_zero_point"] = 0
-            consts["kernel_zero_points"] = np.asarray(zw, np.int32).reshape(-1)
+            # one per O-dim entry of the kernel; a depthwise-multiplier kernel (C, M, KH, KW) has C
+            # of them, each shared by the M output channels c * M + m
+            consts["kernel_zero_points"] = np.repeat(np.asarray(zw, np.int32).reshape(-1),
+                                                     a.get("depthwise_multiplier", 1))
         a["input_scale"] = _scalar(call.args[4], "scale").tolist()
         a["kernel_scale"] = _scalar(call.args[5], "scale").tolist()
     elif op == "qnn.dense":
@@ -254,23 +357,50 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
         else:
             a["input_zero_point"] = 0
             consts["input_zero_points"] = np.asarray(zp_in, np.int32).reshape(-1)
-    elif op == "qnn.add":
+    elif op in ("qnn.add", "qnn.subtract", "qnn.mul"):
         ins = _tensor_args(call, 2, names)
-        vals = [_scalar(call.args[i], "qnn.add param") for i in range(2, 8)]
-        if any(np.ndim(v) != 0 for v in vals):
-            raise UnsupportedError("qnn.add: per-tensor scales/zero points only")
-        ls, lz, rs, rz, os_, oz = vals
-        a.update(lhs_scale=float(np.float32(ls)), lhs_zero_point=int(lz), rhs_scale=float(np.float32(rs)),
-                 rhs_zero_point=int(rz), output_scale=float(np.float32(os_)), output_zero_point=int(oz))
-        for side, s, z in (("lhs", ls, lz), ("rhs", rs, rz)):
-            # RequantizeOrUpcast (op_common.h:186-200): cast when scale AND zero point match
-            up = np.float32(s).tobytes() == np.float32(os_).tobytes() and int(z) == int(oz)
-            a[f"{side}_upcast"] = int(up)
-            if not up:
-                mode, ms, ss = requantize_plan(np.float32(s), np.float32(os_), "UPWARD")
-                a[f"{side}_mode"], a[f"{side}_multiplier"], a[f"{side}_shift"] = mode, int(ms[0]), int(ss[0])
-            else:
-                a[f"{side}_mode"], a[f"{side}_multiplier"], a[f"{side}_shift"] = 0, 0, 0
+        _lower_binary(call, a, consts)
+    elif op == "qnn.concatenate":
+        tup = call.args[0]
+        if not isinstance(tup, Tuple):
+            raise UnsupportedError("qnn.concatenate: the data must be a tuple expression")
+        if any(isinstance(f, Constant) for f in tup.fields):
+            raise UnsupportedError("qnn.concatenate: constant tensor operands must be passed as params (MRT symbols)")
+        ins = [names[id(f)] for f in tup.fields]
+        if len(ins) > _lib.CONCAT_MAX:
+            raise UnsupportedError(f"qnn.concatenate: at most {_lib.CONCAT_MAX} inputs")
+        rounding = _qnn_rounding(a)
+        s_out = np.asarray(_scalar(call.args[3], "qnn.concatenate output_scale"), np.float32)
+        z_out = np.asarray(_scalar(call.args[4], "qnn.concatenate output_zero_point"), np.int32)
+        plans = []
+        for sc, zc in zip(call.args[1].fields, call.args[2].fields):
+            s_i = np.asarray(_scalar(sc, "qnn.concatenate input scale"), np.float32)
+            z_i = np.asarray(_scalar(zc, "qnn.concatenate input zero point"), np.int32)
+            same = _is_equal_scalar(s_i, s_out) and _is_equal_scalar(z_i, z_out)
+            mode, ms, ss = requantize_plan(s_i, s_out, rounding)
+            plans.append({"requant": int(not same), "mode": mode, "multiplier": int(ms[0]), "shift": int(ss[0]),
+                          "input_zero_point": int(z_i), "output_zero_point": int(z_out)})
+        a.update(axis=_norm_axis(a["axis"], len(call.shape)), rounding=rounding, inputs=plans)
+    elif op in ("qnn.quantize", "qnn.dequantize"):
+        ins = _tensor_args(call, 1, names)
+        sv = np.asarray(_scalar(call.args[1], f"{op} scale"), np.float32)
+        zv = np.asarray(_scalar(call.args[2], f"{op} zero point"), np.int32)
+        nd = len(call.shape)
+        a["axis"] = _norm_axis(a["axis"], nd)
+        if sv.size == 1:
+            a["scale"] = float(sv.reshape(-1)[0])
+        else:
+            a["scale"] = 0.0
+            consts["scales"] = sv.reshape(-1)
+        if zv.size == 1:
+            a["zero_point"] = int(zv.reshape(-1)[0])
+        else:
+            a["zero_point"] = 0
+            consts["zero_points"] = zv.reshape(-1)
+    elif op == "transpose":
+        ins = _tensor_args(call, 1, names)
+        if len(call.shape) > 6:
+            raise UnsupportedError("transpose: up to 6-D")
     elif op == "nn.bias_add":
         ins = _tensor_args(call, 2, names)
         nd = len(call.args[0].shape)
@@ -425,7 +555,7 @@ def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
         if len(cs) != 1 or cs[0].op != "qnn.add" or cs[0].name in taken:
             return None
         add = cs[0]
-        if add.out.dtype != rq.out.dtype or add.inputs[0] == add.inputs[1]:
+        if add.out.dtype != rq.out.dtype or add.inputs[0] == add.inputs[1] or not add.attrs.get("per_tensor"):
             return None
         other = add.inputs[1] if add.inputs[0] == rq.name else add.inputs[0]
         if plan.tensor(other).shape != rq.out.shape or plan.tensor(other).dtype != rq.out.dtype:
@@ -443,7 +573,9 @@ def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
     for op in plan.ops:
         if op.name in taken:
             continue
-        if fuse and op.op in ("qnn.conv2d", "qnn.dense"):
+        nchw = op.attrs.get("data_layout", "NCHW") == "NCHW" and op.attrs.get("kernel_layout", "OIHW") == "OIHW" \
+            and op.attrs.get("depthwise_multiplier", 1) == 1
+        if fuse and op.op in ("qnn.conv2d", "qnn.dense") and nchw:
             b = first_consumer(op, ("nn.bias_add",))
             rq = first_consumer(b, ("qnn.requantize",)) if b is not None and b.attrs["axis"] == 1 else None
             if rq is not None and rq.out.dtype in ("int8", "uint8") and rq.attrs["channel_axis"] == 1 \
@@ -462,7 +594,7 @@ def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
                 kind = "conv_block" if op.op == "qnn.conv2d" else "dense_block"
                 place(pos[add.name] if add is not None else pos[op.name], ExecGroup(kind, chain))
                 continue
-        if fuse and op.op == "qnn.add" and op.out.dtype in ("int8", "uint8") and \
+        if fuse and op.op == "qnn.add" and op.out.dtype in ("int8", "uint8") and op.attrs.get("per_tensor") and \
                 all(plan.tensor(x).shape == op.out.shape for x in op.inputs[:2]):
             chain = [op]
             cl = first_consumer(op, ("clip", "nn.relu"))
@@ -518,9 +650,11 @@ class ExecutorFactory:
             f.write(self.save())
         return path
 
-    def _create(self, dev=None):
+    def _create(self, dev=None, tune=True):
+        """``lib["default"](dev)``; ``tune`` as for DeviceModule (True: find step on this GPU; a tune
+        table or its path: replay it)."""
         from .device_module import DeviceModule
-        return DeviceModule(self.plan, self.params, dev, fuse=self.fuse)
+        return DeviceModule(self.plan, self.params, dev, fuse=self.fuse, tune=tune)
 
 
 def build(mod, target: str = "mi355x", params=None, mod_name: str = "default", fuse: bool = True) -> ExecutorFactory:
@@ -582,9 +716,20 @@ def lift_constants(mod, params: Dict[str, np.ndarray]):
 
     new: Dict[int, Expr] = {}
     for n in post_order(func.body):
+        if isinstance(n, Tuple):
+            fields = [new.get(id(x), x) for x in n.fields]
+            if any(x is not y for x, y in zip(fields, n.fields)):
+                new[id(n)] = Tuple(fields)
+            continue
         if not isinstance(n, Call):
             continue
-        k = 2 if n.op.startswith("qnn.") and n.op != "qnn.requantize" else (1 if n.op == "qnn.requantize" else len(n.args))
+        # tensor operands only: a QNN op's scale / zero-point arguments stay constants
+        if n.op in ("qnn.requantize", "qnn.quantize", "qnn.dequantize", "qnn.concatenate"):
+            k = 1
+        elif n.op.startswith("qnn."):
+            k = 2
+        else:
+            k = len(n.args)
         args = [new.get(id(x), x) for x in n.args]
         args = [lift(x) if i < k and isinstance(x, Constant) and x.data.size > 1 else x for i, x in enumerate(args)]
         if any(x is not y for x, y in zip(args, n.args)):

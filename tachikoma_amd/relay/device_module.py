@@ -37,8 +37,20 @@ def torch_dtype(name: str):
             "int64": torch.int64, "float32": torch.float32}[name]
 
 
+def tune_table_digest(entries) -> str:
+    """Digest of a find-step choice: sorted (records, algo) pairs (entries of ``tuning`` or of a
+    tune table)."""
+    import hashlib
+    import json
+    return hashlib.sha256(json.dumps(sorted((list(e["records"]), int(e["algo"])) for e in entries)).encode()
+                          ).hexdigest()[:16]
+
+
 class DeviceModule:
-    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], dev=None, fuse: bool = True, tune: bool = True):
+    def __init__(self, plan: Plan, params: Dict[str, np.ndarray], dev=None, fuse: bool = True, tune=True):
+        """``tune``: True runs the find step (tk_module_tune) on this GPU, False keeps the library's
+        own kernel choice, a tune table (``tuning_table()`` output, or the path of its JSON file)
+        replays a saved find step so that a profile and a timed run use the same kernels."""
         torch = _torch()
         if not torch.cuda.is_available():
             raise _lib.TachikomaError("no MI355X visible: the engine runs on the GPU only (no CPU fallback)")
@@ -60,7 +72,9 @@ class DeviceModule:
         with torch.cuda.device(self.device):
             self._alloc(params)
             self._build_nodes()
-            if tune:
+            if isinstance(tune, (str, dict)):
+                self.apply_tuning(tune)
+            elif tune:
                 self.tune()
 
     # ------------------------------------------------------------ setup
@@ -72,6 +86,75 @@ class DeviceModule:
             self.buffers[t.name] = torch.from_numpy(np.ascontiguousarray(params[t.name])).to(self.device)
         for op in self.plan.ops:
             self.buffers[op.name] = torch.empty(op.out.shape, dtype=torch_dtype(op.out.dtype), device=self.device)
+        self._alloc_layouts()
+
+    # NHWC data / HWIO, OHWI, HWOI kernels of qnn.conv2d (convolution.cc:718-722): the NCHW / OIHW
+    # kernels run between device transposes into untraced buffers named "<op>:nchw_in",
+    # "<op>:oihw_w" (re-derived from the param whenever it is rewritten) and "<op>:nchw_out"; the
+    # record itself stays in the op's own layout.
+    _TO_NCHW = (0, 3, 1, 2)
+    _TO_NHWC = (0, 2, 3, 1)
+
+    def _alloc_layouts(self):
+        torch = _torch()
+        self.layout: Dict[str, Dict[str, object]] = {}
+        for op in self.plan.ops:
+            if op.op != "qnn.conv2d":
+                continue
+            dl, kl = op.attrs.get("data_layout", "NCHW"), op.attrs.get("kernel_layout", "OIHW")
+            mult = op.attrs.get("depthwise_multiplier", 1)
+            if dl == "NCHW" and kl == "OIHW" and mult == 1:
+                continue
+            wt = self.plan.tensor(op.inputs[1])
+            ws = tuple(wt.shape[kl.index(ch)] for ch in "OIHW")
+            # the grouped-conv weight the kernels read: a depthwise-multiplier weight (C, M, KH, KW)
+            # is the same bytes as (C * M, 1, KH, KW) (out channel c * M + m reads [c, m])
+            w_shape = (ws[0] * ws[1], 1, ws[2], ws[3]) if mult > 1 else ws
+            L: Dict[str, object] = {"x": op.inputs[0], "w": op.inputs[1], "y": op.name, "w_shape": w_shape}
+            if dl == "NHWC":
+                xt = self.plan.tensor(op.inputs[0])
+                n_, h_, w_, c_ = xt.shape
+                L["x"] = f"{op.name}:nchw_in"
+                self.buffers[L["x"]] = torch.empty((n_, c_, h_, w_), dtype=torch_dtype(xt.dtype), device=self.device)
+                n_, oh, ow, o_ = op.out.shape
+                L["y"] = f"{op.name}:nchw_out"
+                self.buffers[L["y"]] = torch.empty((n_, o_, oh, ow), dtype=torch.int32, device=self.device)
+            if kl != "OIHW":
+                perm = tuple(kl.index(ch) for ch in "OIHW")
+                L["w"] = f"{op.name}:oihw_w"
+                self.buffers[L["w"]] = torch.empty(tuple(wt.shape[k] for k in perm), dtype=torch_dtype(wt.dtype),
+                                                   device=self.device)
+                self._register_transpose(op.inputs[1], L["w"], perm)
+            self.layout[op.name] = L
+
+    def _transpose_attrs(self, perm):
+        ta = _lib.tk_transpose_attrs()
+        ta.ndim = len(perm)
+        for k, p in enumerate(perm):
+            ta.perm[k] = p
+        return ta
+
+    def _register_transpose(self, src: str, dst: str, perm) -> None:
+        """dst = transpose(src) now, and again whenever the param ``src`` is rewritten."""
+        x, y = self._ref(src), self._ref(dst)
+        ta = self._transpose_attrs(perm)
+        self._keep.append(ta)
+
+        def run(s: int) -> None:
+            _lib.check(self.lib.tk_transpose(x.ptr, y.ptr, ctypes.byref(ta), ctypes.c_void_p(s)), f"transpose {src}")
+        run(_lib.stream_handle())
+        self._derived.setdefault(src, []).append(run)
+
+    def _conv_io(self, op: PlanOp):
+        """(data buffer, weight buffer) the NCHW / OIHW conv kernels read for ``op``."""
+        L = self.layout.get(op.name)
+        return (L["x"], L["w"]) if L else (op.inputs[0], op.inputs[1])
+
+    def _conv_refs(self, op: PlanOp):
+        """TensorRefs of the NCHW data and the OIHW grouped-conv weight for ``op``."""
+        xn, wn = self._conv_io(op)
+        L = self.layout.get(op.name)
+        return self._ref(xn), (self._view_ref(wn, L["w_shape"]) if L else self._ref(wn))
 
     def _ref(self, name: str) -> _lib.TensorRef:
         r = _lib.TensorRef.from_torch(self.buffers[name])
@@ -126,7 +209,7 @@ class DeviceModule:
     def _is_mfma_conv(self, op: PlanOp) -> bool:
         ca = _lib.tk_conv2d_attrs()
         self._conv_attrs(ca, op)
-        x, w = self._ref(op.inputs[0]), self._ref(op.inputs[1])
+        x, w = self._conv_refs(op)
         ws = self.lib.tk_qnn_conv2d_workspace_bytes(x.ptr, w.ptr, ctypes.byref(ca))
         if ws < 0:
             _lib.check(-3, f"{op.name} qnn.conv2d workspace")
@@ -144,7 +227,7 @@ class DeviceModule:
         # their own output's shadow when an MFMA conv reads it
         pool_ops = [g.ops[0] for g in self.groups if g.ops[0].op == "nn.max_pool2d" and
                     g.ops[0].out.dtype in ("int8", "uint8") and len(g.ops[0].out.shape) == 4]
-        need = [op.inputs[0] for op in conv_ops if mfma[op.name]] + [op.inputs[0] for op in pool_ops]
+        need = [self._conv_io(op)[0] for op in conv_ops if mfma[op.name]] + [op.inputs[0] for op in pool_ops]
         for name in need:
             if name not in shadow_bufs:
                 x = self._ref(name)
@@ -224,6 +307,9 @@ class DeviceModule:
                 ins = [self._ref(x) for x in op.inputs]
                 outs = [self._ref(op.name)]
                 a = op.attrs
+                if kind == "qnn.conv2d" and op.name in self.layout:
+                    self._emit_layout_conv(n, op, mfma[op.name], shadow_bufs, ensure_shadow, stream, emit)
+                    continue
                 if kind == "qnn.conv2d":
                     n.kind = _lib.NODE_KINDS["qnn.conv2d"]
                     self._conv_attrs(n.attrs.conv2d, op)
@@ -235,9 +321,38 @@ class DeviceModule:
                 elif kind == "qnn.requantize":
                     n.kind = _lib.NODE_KINDS["qnn.requantize"]
                     self._fill_rq(n.attrs.requantize, op)
-                elif kind == "qnn.add":
+                elif kind == "qnn.add" and a.get("per_tensor"):
                     n.kind = _lib.NODE_KINDS["qnn.add"]
                     _fill_qnn_add(n.attrs.qnn_add, a)
+                elif kind in ("qnn.add", "qnn.subtract", "qnn.mul"):
+                    n.kind = _lib.NODE_KINDS["qnn_binary"]
+                    self._fill_binary(n.attrs.qnn_binary, op)
+                elif kind in ("qnn.quantize", "qnn.dequantize"):
+                    n.kind = _lib.NODE_KINDS[kind]
+                    qa = n.attrs.qparams
+                    qa.axis = a["axis"]
+                    qa.scale = a["scale"]
+                    qa.zero_point = a["zero_point"]
+                    if "scales" in op.consts:
+                        t = _torch().from_numpy(np.ascontiguousarray(op.consts["scales"], np.float32)).to(self.device)
+                        self._keep.append(t)
+                        qa.scales = t.data_ptr()
+                    if "zero_points" in op.consts:
+                        qa.zero_points = self._dev_i32(op.consts["zero_points"]).data_ptr()
+                elif kind == "qnn.concatenate":
+                    n.kind = _lib.NODE_KINDS[kind]
+                    ca = n.attrs.concat
+                    ca.axis = a["axis"]
+                    ca.n = len(ins)
+                    for k, pl in enumerate(a["inputs"]):
+                        ca.requant[k] = pl["requant"]
+                        r = ca.rq[k]
+                        r.mode, r.axis = pl["mode"], -1
+                        r.multiplier, r.shift = pl["multiplier"], pl["shift"]
+                        r.input_zero_point, r.output_zero_point = pl["input_zero_point"], pl["output_zero_point"]
+                elif kind == "transpose":
+                    n.kind = _lib.NODE_KINDS["transpose"]
+                    n.attrs.transpose = self._transpose_attrs(a["axes"])
                 elif kind == "nn.bias_add":
                     n.kind = _lib.NODE_KINDS["nn.bias_add"]
                     n.attrs.bias_add.axis = a["axis"]
@@ -304,11 +419,63 @@ class DeviceModule:
                 n.outputs[k] = r.ptr
             emit(n, g.kind, [o.name for o in g.ops])
         torch.cuda.current_stream().synchronize()
+        self._node_kind_codes = [int(n.kind) for n in nodes]
         arr = (_lib.tk_node * max(1, len(nodes)))(*nodes)
         handle = ctypes.c_void_p()
         _lib.check(self.lib.tk_module_create(arr, len(nodes), ctypes.byref(handle)), "tk_module_create")
         self.handle = handle
         self.n_nodes = len(nodes)
+
+    def _fill_binary(self, qb, op: PlanOp) -> None:
+        """tk_qnn_binary_attrs from a lowered qnn.add / qnn.subtract / qnn.mul."""
+        a = op.attrs
+        qb.op = _lib.TK_QB[op.op]
+        for side in ("lhs", "rhs", "out"):
+            if f"{side}_mode" not in a:
+                continue
+            r = getattr(qb, side)
+            r.mode = a[f"{side}_mode"]
+            r.axis = a[f"{side}_axis"]
+            r.multiplier = a[f"{side}_multiplier"]
+            r.shift = a[f"{side}_shift"]
+            if f"{side}_multipliers" in op.consts:
+                r.multipliers = self._dev_i32(op.consts[f"{side}_multipliers"]).data_ptr()
+                r.shifts = self._dev_i32(op.consts[f"{side}_shifts"]).data_ptr()
+            r.input_zero_point = a[f"{side}_zero_point"]
+            if f"{side}_zero_points" in op.consts:
+                r.input_zero_points = self._dev_i32(op.consts[f"{side}_zero_points"]).data_ptr()
+            r.output_zero_point = a["output_zero_point"] if side != "lhs" or op.op != "qnn.mul" else 0
+        if op.op == "qnn.mul":
+            qb.lhs.output_zero_point = qb.rhs.output_zero_point = 0
+        qb.lhs_upcast = a.get("lhs_upcast", 0)
+        qb.rhs_upcast = a.get("rhs_upcast", 0)
+        qb.output_zero_point = a["output_zero_point"]
+
+    def _emit_layout_conv(self, n, op: PlanOp, is_mfma: bool, shadow_bufs, ensure_shadow, stream, emit) -> None:
+        """qnn.conv2d with NHWC data and/or a non-OIHW kernel: [transpose data -> NCHW], the NCHW /
+        OIHW conv into an int32 NCHW buffer, [transpose -> the NHWC record]."""
+        L = self.layout[op.name]
+
+        def transpose_node(src: str, dst: str, perm, records):
+            t = _lib.tk_node()
+            t.kind = _lib.NODE_KINDS["transpose"]
+            t.attrs.transpose = self._transpose_attrs(perm)
+            t.n_inputs, t.n_outputs = 1, 1
+            t.inputs[0], t.outputs[0] = self._ref(src).ptr, self._ref(dst).ptr
+            emit(t, "transpose", records)
+
+        if L["x"] != op.inputs[0]:
+            transpose_node(op.inputs[0], L["x"], self._TO_NCHW, [])
+        ins = list(self._conv_refs(op))
+        n.kind = _lib.NODE_KINDS["qnn.conv2d"]
+        self._conv_attrs(n.attrs.conv2d, op)
+        self._prep_conv(n, op, ins, is_mfma, shadow_bufs, ensure_shadow, stream)
+        n.n_inputs, n.n_outputs = 2, 1
+        n.inputs[0], n.inputs[1] = ins[0].ptr, ins[1].ptr
+        n.outputs[0] = self._ref(L["y"]).ptr
+        emit(n, "qnn.conv2d", [] if L["y"] != op.name else [op.name])
+        if L["y"] != op.name:
+            transpose_node(L["y"], op.name, self._TO_NHWC, [op.name])
 
     def _view_ref(self, name: str, shape) -> _lib.TensorRef:
         r = _lib.TensorRef.from_torch(self.buffers[name].view(*shape))
@@ -421,12 +588,13 @@ class DeviceModule:
         split-K partial tiles)."""
         if not is_mfma:
             return
-        ensure_shadow(op.inputs[0])
+        xname = self._conv_io(op)[0]
+        ensure_shadow(xname)
         packed = self._scratch(self.lib.tk_conv2d_packed_weight_bytes(ins[1].ptr, 1))
-        o = op.out.shape[1]
+        o = ins[1].shape[0]
         sums = self._scratch(((o + 127) // 128 * 128) * 4)
         self._pack(op.inputs[1], op.name, ins[1], packed, sums, stream)
-        n.ext[0] = shadow_bufs[op.inputs[0]].data_ptr()
+        n.ext[0] = shadow_bufs[xname].data_ptr()
         n.ext[1] = packed.data_ptr()
         n.ext[2] = sums.data_ptr()
         block = n.kind == _lib.NODE_KINDS["conv_block"]
@@ -557,7 +725,42 @@ class DeviceModule:
             out.append({"node": i, "records": list(self.node_records[i]), "algo": int(algos[i * w]),
                         "us": round(float(us[i * w]), 2), "candidates": cands})
         self.tuning = out
+        self.tune_table_digest = tune_table_digest(out)
         return out
+
+    def tuning_table(self) -> dict:
+        """The find step's choice per conv-block node, keyed by the node's records (stable across
+        processes for one plan), with the library it was measured with."""
+        return {"format": "tachikoma-tune-table", "version": 1, "library": _lib.build_info(),
+                "entries": [{"records": t["records"], "algo": t["algo"], "us": t["us"]} for t in self.tuning]}
+
+    def apply_tuning(self, table) -> List[dict]:
+        """Replays a tune table (``tuning_table()``, or a JSON file of one) with tk_module_set_node_algo;
+        every conv-block node must be listed.  Returns (and keeps in ``self.tuning``) the applied
+        entries; the table's digest is ``self.tune_table_digest``."""
+        import json
+        if isinstance(table, str):
+            with open(table) as f:
+                table = json.load(f)
+        if table.get("format") != "tachikoma-tune-table":
+            raise _lib.TachikomaError("not a tachikoma tune table")
+        by_records = {tuple(e["records"]): e for e in table["entries"]}
+        applied = []
+        for i, (kind, recs) in enumerate(zip(self.node_kinds, self.node_records)):
+            if self._node_kind(i) != _lib.NODE_KINDS["conv_block"]:  # dense blocks run as 1x1 conv blocks
+                continue
+            e = by_records.get(tuple(recs))
+            if e is None:
+                raise _lib.TachikomaError(f"tune table has no entry for the conv block writing {recs}")
+            _lib.check(self.lib.tk_module_set_node_algo(self.handle, i, int(e["algo"])), "tk_module_set_node_algo")
+            applied.append({"node": i, "records": list(recs), "algo": int(e["algo"]), "us": e.get("us"),
+                            "candidates": []})
+        self.tuning = applied
+        self.tune_table_digest = tune_table_digest(applied)
+        return applied
+
+    def _node_kind(self, i: int) -> int:
+        return self._node_kind_codes[i]
 
     def set_profiling(self, enable: bool) -> None:
         _lib.check(self.lib.tk_module_set_profiling(self.handle, int(enable)), "tk_module_set_profiling")

@@ -70,6 +70,29 @@ class Call(Expr):
         return f"{self.op}({', '.join(type(a).__name__ for a in self.args)})"
 
 
+class Tuple(Expr):
+    """``relay.Tuple`` (python/tvm/relay/expr.py): the tensor list of ``qnn.concatenate`` and the
+    scale / zero-point tuples beside it.  It is no op: it has no record and takes no ``%N`` name
+    (MRT's ``expr2symbol`` names only Calls and TupleGetItems, python/tvm/mrt/symbol.py:212-253)."""
+
+    def __init__(self, fields: Sequence[Expr]):
+        self.fields = list(fields)
+        self.checked_type = TensorType((len(self.fields),), "tuple")
+
+    @property
+    def args(self) -> List[Expr]:
+        return self.fields
+
+    def __len__(self):
+        return len(self.fields)
+
+    def __getitem__(self, i: int) -> Expr:
+        return self.fields[i]
+
+    def __repr__(self):
+        return f"({', '.join(type(f).__name__ for f in self.fields)})"
+
+
 class Function:
     def __init__(self, params: List[Var], body: Expr):
         self.params = list(params)
@@ -121,7 +144,8 @@ def const(value, dtype: Optional[str] = None) -> Constant:
 
 
 def post_order(expr: Expr) -> List[Expr]:
-    """Post-order DFS over args (``relay.analysis.post_order_visit``); each node once."""
+    """Post-order DFS over args (``relay.analysis.post_order_visit``); each node once (a Tuple's
+    fields are its args)."""
     out: List[Expr] = []
     seen = set()
     stack = [(expr, False)]
@@ -129,7 +153,7 @@ def post_order(expr: Expr) -> List[Expr]:
         node, expanded = stack.pop()
         if id(node) in seen:
             continue
-        if expanded or not isinstance(node, Call):
+        if expanded or not isinstance(node, (Call, Tuple)):
             seen.add(id(node))
             out.append(node)
             continue

@@ -47,6 +47,10 @@ _PATTERNS = {
     "left_shift": kBroadcast, "right_shift": kBroadcast, "subtract": kBroadcast,
     "fixed_point_multiply_per_axis": kBroadcast,  # transform.cc:4421-4432
     "nn.batch_flatten": kInjective, "reshape": kInjective, "nn.pad": kInjective,
+    # pre-quantized graphs: the pattern of each op's canonical form (divide / round / add / clip /
+    # cast; cast / subtract / multiply; requantizes + subtract / multiply; requantizes + concatenate)
+    "qnn.quantize": kBroadcast, "qnn.dequantize": kBroadcast, "qnn.subtract": kBroadcast, "qnn.mul": kBroadcast,
+    "qnn.concatenate": kInjective, "transpose": kInjective,
     "annotation.stop_fusion": kOpaque, "annotation.cast_hint": kOpaque,
     "tachikoma.qnn.conv2d": kOpaque, "tachikoma.qnn.dense": kOpaque,  # external (BYOC) functions
 }

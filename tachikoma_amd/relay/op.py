@@ -53,15 +53,19 @@ def bias_add(data: Expr, bias: Expr, axis: int = 1) -> Call:
     return Call("nn.bias_add", [data, bias], {"axis": axis}, data.checked_type)
 
 
+def _broadcast_shape(name: str, a, b) -> Tuple[int, ...]:
+    try:
+        shape = np.broadcast_shapes(tuple(a), tuple(b))
+    except ValueError as e:
+        raise TypeError(f"{name}: {tuple(a)} and {tuple(b)} do not broadcast") from e
+    return tuple(int(d) for d in shape)
+
+
 def _broadcast(name: str, lhs: Expr, rhs: Expr) -> TensorType:
     """Relay's BroadcastRel (src/relay/op/type_relations.cc): numpy broadcasting, equal dtypes."""
     if lhs.dtype != rhs.dtype:
         raise TypeError(f"{name}: dtype mismatch {lhs.dtype} vs {rhs.dtype}")
-    try:
-        shape = np.broadcast_shapes(tuple(lhs.shape), tuple(rhs.shape))
-    except ValueError as e:
-        raise TypeError(f"{name}: {lhs.shape} and {rhs.shape} do not broadcast") from e
-    return TensorType(tuple(int(d) for d in shape), lhs.dtype)
+    return TensorType(_broadcast_shape(name, lhs.shape, rhs.shape), lhs.dtype)
 
 
 def add(lhs: Expr, rhs: Expr) -> Call:
@@ -142,6 +146,15 @@ def dense(data: Expr, weight: Expr, units=None, out_dtype="") -> Call:
         raise TypeError(f"nn.dense: {data.shape} x {weight.shape}")
     odt = str(np.dtype(out_dtype)) if out_dtype else data.dtype
     return Call("nn.dense", [data, weight], {"units": nn_, "out_dtype": odt}, TensorType((m, nn_), odt))
+
+
+def transpose(data: Expr, axes=None) -> Call:
+    """``relay.transpose`` (src/relay/op/tensor/transform.cc TransposeRel): axes=None reverses."""
+    nd = len(data.shape)
+    ax = tuple(range(nd))[::-1] if axes is None else tuple(int(a) + nd if int(a) < 0 else int(a) for a in axes)
+    if sorted(ax) != list(range(nd)):
+        raise TypeError(f"transpose: {axes} is not a permutation of {nd} axes")
+    return Call("transpose", [data], {"axes": ax}, TensorType(tuple(data.shape[a] for a in ax), data.dtype))
 
 
 def clip(a: Expr, a_min: float, a_max: float) -> Call:

@@ -35,7 +35,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import numpy as np
 
 from . import op as _op
-from .expr import Call, Constant, Expr, Function, IRModule, Var, const, post_order
+from .expr import Call, Constant, Expr, Function, IRModule, Tuple, Var, const, post_order
 from .qnn import op as _qnn
 
 __all__ = ["ParseError", "parse", "fromtext", "astext", "load_meta_json", "dump_meta_json"]
@@ -167,8 +167,10 @@ def _call(op: str, args: List[Expr], attrs: Dict[str, Any]) -> Expr:
             return _qnn.dense(*args, **a)
         if op == "qnn.requantize":
             return _qnn.requantize(*args, **a)
-        if op == "qnn.add":
-            return _qnn.add(*args, **a)
+        if op in ("qnn.add", "qnn.subtract", "qnn.mul", "qnn.concatenate", "qnn.quantize", "qnn.dequantize"):
+            return getattr(_qnn, op.split(".")[1])(*args, **a)
+        if op == "transpose":
+            return _op.transpose(*args, **a)
         if op == "nn.bias_add":
             return _op.bias_add(*args, **a)
         if op == "clip":
@@ -344,6 +346,10 @@ class _Parser:
                 base, dot, idx = name.rpartition(".")
                 if dot and idx.isdigit() and base in self.scope:
                     tup = self.scope[base]
+                    if isinstance(tup, Tuple):
+                        if int(idx) >= len(tup):
+                            raise ParseError(f"{name}: {base} has {len(tup)} fields")
+                        return tup[int(idx)]
                     if not isinstance(tup, _op.BatchNormOutputs):
                         raise ParseError(f"{name}: {base} is not a tuple")
                     try:
@@ -355,6 +361,16 @@ class _Parser:
             if isinstance(v, _op.BatchNormOutputs):
                 raise ParseError(f"{name} is a tuple (nn.batch_norm): use a field, e.g. {name}.0")
             return v
+        if t[1] == "(":
+            # a tuple literal: qnn.concatenate's tensors, scales and zero points
+            self.next()
+            fields = []
+            while self.peek()[1] != ")":
+                fields.append(self.parse_expr())
+                if self.peek()[1] == ",":
+                    self.next()
+            self.next()
+            return Tuple(fields)
         if t[0] == "number":
             self.next()
             v = _number(t[1])
@@ -445,6 +461,8 @@ def astext(mod: IRModule, show_meta_data: bool = True) -> str:
             return "%" + e.name_hint
         if isinstance(e, Constant):
             return _fmt_const(e, metas)
+        if isinstance(e, Tuple):  # printed inline: it takes no %N (no record, no MRT symbol)
+            return "(" + ", ".join(ref(f) for f in e.fields) + ("," if len(e.fields) == 1 else "") + ")"
         return names[id(e)]
 
     for node in post_order(fn.body):

@@ -12,8 +12,8 @@ from typing import Optional
 
 import numpy as np
 
-from ..expr import Call, Constant, Expr, TensorType, const
-from ..op import _check_int, _tuple2, get_pad_tuple2d
+from ..expr import Call, Constant, Expr, TensorType, Tuple, const
+from ..op import _broadcast_shape, _check_int, _tuple2, get_pad_tuple2d
 
 _cfg = threading.local()
 
@@ -69,17 +69,39 @@ def requantize(data: Expr, input_scale, input_zero_point, output_scale, output_z
                 TensorType(data.shape, str(np.dtype(out_dtype))))
 
 
+KERNEL_LAYOUTS = ("OIHW", "HWIO", "OHWI", "HWOI")
+
+
 def conv2d(data: Expr, kernel: Expr, input_zero_point, kernel_zero_point, input_scale, kernel_scale, kernel_size,
            channels, strides=(1, 1), padding=(0, 0), dilation=(1, 1), groups: int = 1, data_layout="NCHW",
            kernel_layout="OIHW", out_layout="", out_dtype="int32") -> Call:
-    if data_layout != "NCHW" or kernel_layout != "OIHW":
-        raise NotImplementedError("qnn.conv2d: NCHW/OIHW only (the layout the reference traces)")
+    """``qnn.conv2d`` with the layouts the reference's QNN conv accepts
+    (src/relay/qnn/op/convolution.cc:718-722): NCHW / NHWC data, OIHW / HWIO / OHWI / HWOI kernel;
+    the output is in the data layout (Conv2DRel's default out_layout)."""
+    if data_layout not in ("NCHW", "NHWC") or kernel_layout not in KERNEL_LAYOUTS:
+        raise NotImplementedError(f"qnn.conv2d: data layout {data_layout} / kernel layout {kernel_layout}: "
+                                  f"NCHW or NHWC data with {', '.join(KERNEL_LAYOUTS)} kernels")
+    if out_layout not in ("", data_layout):
+        raise NotImplementedError("qnn.conv2d: out_layout must be the data layout")
     if str(np.dtype(out_dtype)) != "int32":
         raise NotImplementedError("qnn.conv2d: out_dtype must be int32")
     _check_int(data, "qnn.conv2d")
     _check_int(kernel, "qnn.conv2d")
-    n, c, h, w = data.shape
-    o, cg, kh, kw = kernel.shape
+    if data_layout == "NCHW":
+        n, c, h, w = data.shape
+    else:
+        n, h, w, c = data.shape
+    ks = dict(zip(kernel_layout, kernel.shape))
+    o, cg, kh, kw = ks["O"], ks["I"], ks["H"], ks["W"]
+    multiplier = 1
+    if groups > 1 and groups == c and o == groups and cg > 1:
+        # Conv2DRel's depthwise form (src/relay/op/nn/convolution.cc:243-274): the OIHW-space weight is
+        # (C, multiplier, KH, KW) and output channel c * multiplier + m reads weight[c, m]
+        multiplier = cg
+        if channels is not None and int(channels) != c * multiplier:
+            raise TypeError(f"qnn.conv2d: depthwise kernel {kernel.shape} gives {c * multiplier} channels, "
+                            f"not {channels}")
+        o, cg = c * multiplier, 1
     if c != cg * groups:
         raise TypeError(f"qnn.conv2d: {c} input channels vs kernel {kernel.shape} with groups={groups}")
     sh, sw = _tuple2(strides)
@@ -92,9 +114,12 @@ def conv2d(data: Expr, kernel: Expr, input_zero_point, kernel_zero_point, input_
     attrs = {"strides": (sh, sw), "padding": (pt, pl, pb, pr), "dilation": (dh, dw), "groups": int(groups),
              "channels": int(channels) if channels is not None else o, "kernel_size": (kh, kw),
              "data_layout": data_layout, "kernel_layout": kernel_layout, "out_dtype": "int32"}
+    if multiplier > 1:
+        attrs["depthwise_multiplier"] = multiplier
     args = [data, kernel, _c(input_zero_point, "int32"), _c(kernel_zero_point, "int32"),
             _c(input_scale, "float32"), _c(kernel_scale, "float32")]
-    return Call("qnn.conv2d", args, attrs, TensorType((n, o, oh, ow), "int32"))
+    shape = (n, o, oh, ow) if data_layout == "NCHW" else (n, oh, ow, o)
+    return Call("qnn.conv2d", args, attrs, TensorType(shape, "int32"))
 
 
 def dense(data: Expr, weight: Expr, input_zero_point, kernel_zero_point, input_scale, kernel_scale, units,
@@ -112,11 +137,122 @@ def dense(data: Expr, weight: Expr, input_zero_point, kernel_zero_point, input_s
     return Call("qnn.dense", args, {"units": nn_, "out_dtype": "int32"}, TensorType((m, nn_), "int32"))
 
 
-def add(lhs: Expr, rhs: Expr, lhs_scale, lhs_zero_point, rhs_scale, rhs_zero_point, output_scale,
-        output_zero_point, lhs_axis: int = -1, rhs_axis: int = -1) -> Call:
-    _check_int(lhs, "qnn.add")
-    if lhs.shape != rhs.shape or lhs.dtype != rhs.dtype:
-        raise NotImplementedError("qnn.add: same-shape, same-dtype operands only")
+def _binary(name: str, lhs: Expr, rhs: Expr, lhs_scale, lhs_zero_point, rhs_scale, rhs_zero_point, output_scale,
+            output_zero_point, lhs_axis: int, rhs_axis: int) -> Call:
+    """QNN_REGISTER_BINARY_OP operands (src/relay/qnn/op/op_common.h:231-320, QnnBroadcastRel):
+    numpy broadcasting of equal-dtype operands; scales / zero points rank-0 (per-tensor) or one
+    per index of ``lhs_axis`` / ``rhs_axis`` of that operand."""
+    _check_int(lhs, name)
+    if lhs.dtype != rhs.dtype:
+        raise TypeError(f"{name}: dtype mismatch {lhs.dtype} vs {rhs.dtype}")
+    if lhs.dtype not in ("int8", "uint8", "int16", "int32"):
+        raise TypeError(f"{name}: int8, uint8, int16 or int32 operands expected, got {lhs.dtype}")
+    shape = _broadcast_shape(name, lhs.shape, rhs.shape)
     args = [lhs, rhs, _c(lhs_scale, "float32"), _c(lhs_zero_point, "int32"), _c(rhs_scale, "float32"),
             _c(rhs_zero_point, "int32"), _c(output_scale, "float32"), _c(output_zero_point, "int32")]
-    return Call("qnn.add", args, {"lhs_axis": lhs_axis, "rhs_axis": rhs_axis}, lhs.checked_type)
+    for side, x, ax, (si, zi) in (("lhs", lhs, lhs_axis, (2, 3)), ("rhs", rhs, rhs_axis, (4, 5))):
+        nd = len(x.shape)
+        a = 0 if nd <= 1 else (nd + ax if ax < 0 else ax)
+        for k in (si, zi):
+            p = args[k].checked_type.shape
+            if p != () and (nd and not (0 <= a < nd) or p != ((x.shape[a] if nd else 1),)):
+                raise TypeError(f"{name}: {side} parameter of shape {p} does not match axis {ax} of {x.shape}")
+    if args[6].checked_type.shape != () or args[7].checked_type.shape != ():
+        raise TypeError(f"{name}: output scale / zero point must be scalars")
+    cfg = current_requantize_config()
+    attrs = {"lhs_axis": int(lhs_axis), "rhs_axis": int(rhs_axis), "cfg_rounding": cfg["rounding"],
+             "cfg_compute_dtype": cfg["compute_dtype"]}
+    return Call(name, args, attrs, TensorType(shape, lhs.dtype))
+
+
+def add(lhs: Expr, rhs: Expr, lhs_scale, lhs_zero_point, rhs_scale, rhs_zero_point, output_scale,
+        output_zero_point, lhs_axis: int = -1, rhs_axis: int = -1) -> Call:
+    """``qnn.add`` (src/relay/qnn/op/add.cc:40-96)."""
+    return _binary("qnn.add", lhs, rhs, lhs_scale, lhs_zero_point, rhs_scale, rhs_zero_point, output_scale,
+                   output_zero_point, lhs_axis, rhs_axis)
+
+
+def subtract(lhs: Expr, rhs: Expr, lhs_scale, lhs_zero_point, rhs_scale, rhs_zero_point, output_scale,
+             output_zero_point, lhs_axis: int = -1, rhs_axis: int = -1) -> Call:
+    """``qnn.subtract`` (src/relay/qnn/op/subtract.cc:40-94)."""
+    return _binary("qnn.subtract", lhs, rhs, lhs_scale, lhs_zero_point, rhs_scale, rhs_zero_point, output_scale,
+                   output_zero_point, lhs_axis, rhs_axis)
+
+
+def mul(lhs: Expr, rhs: Expr, lhs_scale, lhs_zero_point, rhs_scale, rhs_zero_point, output_scale,
+        output_zero_point, lhs_axis: int = -1, rhs_axis: int = -1) -> Call:
+    """``qnn.mul`` (src/relay/qnn/op/mul.cc:43-159)."""
+    return _binary("qnn.mul", lhs, rhs, lhs_scale, lhs_zero_point, rhs_scale, rhs_zero_point, output_scale,
+                   output_zero_point, lhs_axis, rhs_axis)
+
+
+def _as_tuple(v, dtype) -> Tuple:
+    if isinstance(v, Tuple):
+        return v
+    return Tuple([_c(x, dtype) for x in v])
+
+
+def concatenate(data, input_scales, input_zero_points, output_scale, output_zero_point, axis: int) -> Call:
+    """``qnn.concatenate`` (src/relay/qnn/op/concatenate.cc:39-97 QnnConcatenateRel, :137-144): a
+    tuple of equal-rank, equal-dtype tensors that agree outside ``axis``; one scalar scale and zero
+    point per input, scalar output params."""
+    data = data if isinstance(data, Tuple) else Tuple(list(data))
+    scales, zps = _as_tuple(input_scales, "float32"), _as_tuple(input_zero_points, "int32")
+    if not data.fields or len(scales) != len(data) or len(zps) != len(data):
+        raise TypeError("qnn.concatenate: one scale and one zero point per input tensor")
+    for f in scales.fields + zps.fields:
+        if f.checked_type.shape != ():
+            raise TypeError("qnn.concatenate: input scales / zero points must be scalars")
+    first = data.fields[0]
+    nd = len(first.shape)
+    ax = axis + nd if axis < 0 else axis
+    if not 0 <= ax < nd:
+        raise TypeError(f"qnn.concatenate: axis {axis} out of range for rank {nd}")
+    total = 0
+    for x in data.fields:
+        _check_int(x, "qnn.concatenate")
+        if len(x.shape) != nd or x.dtype != first.dtype or any(
+                x.shape[d] != first.shape[d] for d in range(nd) if d != ax):
+            raise TypeError(f"qnn.concatenate: {x.shape} {x.dtype} does not concatenate with "
+                            f"{first.shape} {first.dtype} on axis {axis}")
+        total += x.shape[ax]
+    shape = tuple(total if d == ax else first.shape[d] for d in range(nd))
+    out_s, out_z = _c(output_scale, "float32"), _c(output_zero_point, "int32")
+    if out_s.checked_type.shape != () or out_z.checked_type.shape != ():
+        raise TypeError("qnn.concatenate: output scale / zero point must be scalars")
+    cfg = current_requantize_config()
+    attrs = {"axis": int(axis), "cfg_rounding": cfg["rounding"], "cfg_compute_dtype": cfg["compute_dtype"]}
+    return Call("qnn.concatenate", [data, scales, zps, out_s, out_z], attrs, TensorType(shape, first.dtype))
+
+
+def _axis_param(p: Expr, x_shape, axis: int, what: str):
+    nd = len(x_shape)
+    a = axis + nd if axis < 0 else axis
+    shp = p.checked_type.shape
+    if shp == () or int(np.prod(shp)) == 1:
+        return
+    if not (0 <= a < max(nd, 1)) or shp != (x_shape[a],):
+        raise TypeError(f"{what}: parameter of shape {shp} does not match axis {axis} of {x_shape}")
+
+
+def quantize(data: Expr, output_scale, output_zero_point, axis: int = -1, out_dtype: str = "int8") -> Call:
+    """``qnn.quantize`` (src/relay/qnn/op/quantize.cc:39-111): float32 → int8 / uint8 / int16 / int32."""
+    if data.dtype != "float32":
+        raise TypeError(f"qnn.quantize: float32 data expected, got {data.dtype}")
+    odt = str(np.dtype(out_dtype))
+    if odt not in ("int8", "uint8", "int16", "int32"):
+        raise TypeError(f"qnn.quantize: out_dtype must be int8, uint8, int16 or int32, got {odt}")
+    s, z = _c(output_scale, "float32"), _c(output_zero_point, "int32")
+    _axis_param(s, data.shape, axis, "qnn.quantize")
+    _axis_param(z, data.shape, axis, "qnn.quantize")
+    return Call("qnn.quantize", [data, s, z], {"axis": int(axis), "out_dtype": odt}, TensorType(data.shape, odt))
+
+
+def dequantize(data: Expr, input_scale, input_zero_point, axis: int = -1) -> Call:
+    """``qnn.dequantize`` (src/relay/qnn/op/dequantize.cc:39-94): int8 / uint8 / int16 / int32 → float32."""
+    if data.dtype not in ("int8", "uint8", "int16", "int32"):
+        raise TypeError(f"qnn.dequantize: int8, uint8, int16 or int32 data expected, got {data.dtype}")
+    s, z = _c(input_scale, "float32"), _c(input_zero_point, "int32")
+    _axis_param(s, data.shape, axis, "qnn.dequantize")
+    _axis_param(z, data.shape, axis, "qnn.dequantize")
+    return Call("qnn.dequantize", [data, s, z], {"axis": int(axis)}, TensorType(data.shape, "float32"))

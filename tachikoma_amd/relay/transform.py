@@ -92,11 +92,12 @@ def fold_scale_axis(mod) -> IRModule:
     ``multiply`` by a per-output-channel constant is folded into the producer of its data when
     every node on the way has this multiply as its only consumer:
 
-    * ``nn.conv2d(x, W)`` (NCHW / OIHW, any groups: output channel o is weight row o)
+    * ``nn.conv2d(x, W)`` (NCHW / OIHW, groups == 1 or depthwise: output channel o is weight row o)
       -> ``nn.conv2d(x, W * s[o])`` (Conv2DBackwardTransform);
     * ``nn.dense(x, W)`` -> ``nn.dense(x, W * s[:, None])`` (DenseBackwardTransform);
     * ``add(a, b)`` -> ``add(fold(a), fold(b))`` when both sides fold, a constant side (a bias
-      [C, 1, 1]) being multiplied by s (AddSubBackwardTransform).
+      [C, 1, 1] / [1, C, 1, 1], or [C] / [1, C] on a dense output) being multiplied by s
+      (AddSubBackwardTransform).
 
     The new weights are ``multiply`` calls on constants that the FoldConstant after this pass
     evaluates (float32 elementwise, like the reference).  The forward direction (a scale on a
@@ -109,21 +110,30 @@ def fold_scale_axis(mod) -> IRModule:
         for a in getattr(n, "args", []):
             uses[id(a)] = uses.get(id(a), 0) + 1
 
-    def fold(e: Expr, orig: Expr, s: np.ndarray) -> Optional[Expr]:
-        """e: the rewritten node, orig: the node it replaces (use counts are the original graph's)."""
+    def fold(e: Expr, orig: Expr, s: np.ndarray, ndim: int) -> Optional[Expr]:
+        """e: the rewritten node, orig: the node it replaces (use counts are the original graph's),
+        ndim: the rank of the tensor ``s`` scales along its channel axis (1)."""
         if isinstance(e, Constant):
-            shape = tuple(e.data.shape)
+            # only a constant that broadcasts onto the channel axis of a rank-``ndim`` output
+            # (AddSubBackwardPrep's MatchBroadcastToLeftAxes, fold_scale_axis.cc): a (C,) vector
+            # on an NCHW output would broadcast along W instead
+            shape, c = tuple(e.data.shape), len(s)
             if e.data.dtype.kind != "f":
                 return None
-            if len(shape) == 3 and shape[1:] == (1, 1) and shape[0] == len(s):
-                return _op.multiply(e, Constant(s.reshape(-1, 1, 1)))
-            if shape == (len(s),):
-                return _op.multiply(e, Constant(s))
+            if ndim == 4 and shape in ((c, 1, 1), (1, c, 1, 1)):
+                return _op.multiply(e, Constant(s.reshape(shape)))
+            if ndim == 2 and shape in ((c,), (1, c)):
+                return _op.multiply(e, Constant(s.reshape(shape)))
             return None
         if not isinstance(e, Call) or uses.get(id(orig), 0) != 1:
             return None
         if e.op == "nn.conv2d" and e.dtype == "float32" and isinstance(e.args[1], Constant):
             w = e.args[1]
+            # ConvBackwardPrep folds only into groups == 1 or depthwise convs (fold_scale_axis.cc:
+            # 986-987; IsDepthwiseConv, pattern_utils.h:223-229: O == groups and I == 1)
+            g = int(e.attrs.get("groups", 1))
+            if not (g == 1 or (w.data.shape[0] == g and w.data.shape[1] == 1)):
+                return None
             nw = _op.multiply(w, Constant(s.reshape(-1, 1, 1, 1).astype(w.data.dtype)))
             return Call("nn.conv2d", [e.args[0], nw], e.attrs, e.checked_type)
         if e.op == "nn.dense" and e.dtype == "float32" and isinstance(e.args[1], Constant):
@@ -131,8 +141,8 @@ def fold_scale_axis(mod) -> IRModule:
             return Call("nn.dense", [e.args[0], _op.multiply(w, Constant(s.reshape(-1, 1).astype(w.data.dtype)))],
                         e.attrs, e.checked_type)
         if e.op == "add":
-            a = fold(e.args[0], orig.args[0], s)
-            b = fold(e.args[1], orig.args[1], s)
+            a = fold(e.args[0], orig.args[0], s, len(e.shape))
+            b = fold(e.args[1], orig.args[1], s, len(e.shape))
             if a is None or b is None:
                 return None
             return _op.add(a, b)
@@ -142,7 +152,7 @@ def fold_scale_axis(mod) -> IRModule:
         if call.op == "multiply" and call.dtype == "float32":
             s = _channel_scale(args[1], call)
             if s is not None:
-                folded = fold(args[0], call.args[0], s)
+                folded = fold(args[0], call.args[0], s, len(call.shape))
                 if folded is not None:
                     return folded
         if all(x is y for x, y in zip(args, call.args)):

@@ -19,6 +19,11 @@ RQ = "tests/python/relay/test_op_qnn_requantize.py"
 DENSE = "tests/python/relay/test_op_qnn_dense.py"
 CONV = "tests/python/relay/test_op_qnn_conv2d.py"
 ADD = "tests/python/relay/test_op_qnn_add.py"
+QUANT = "tests/python/relay/test_op_qnn_quantize.py"
+DEQUANT = "tests/python/relay/test_op_qnn_dequantize.py"
+CONCAT = "tests/python/relay/test_op_qnn_concatenate.py"
+MUL = "tests/python/relay/test_op_qnn_mul.py"
+SUB = "tests/python/relay/test_op_qnn_subtract.py"
 
 
 def arr(a, dtype):
@@ -210,12 +215,165 @@ def add_cases():
     return c
 
 
+def quantize_cases():
+    """test_op_qnn_quantize.py: literal float32 inputs and their int8 / uint8 codes."""
+    c = []
+    d = np.array([-63.5, -63, -62.5, -62, -61.5, 62, 62.5, 63, 63.5, 64], dtype="float32").reshape(2, 5)
+    for name, src, zp, out_dtype, exp in (
+            ("float32_to_uint8", f"{QUANT}:51-66", 127, "uint8", [0, 1, 2, 3, 4, 251, 252, 253, 254, 255]),
+            ("float32_to_int8", f"{QUANT}:69-88", -1, "int8", [-128, -127, -126, -125, -124, 123, 124, 125, 126, 127])):
+        c.append({"op": "qnn.quantize", "source": src, "name": name, "inputs": {"data": arr(d, "float32")},
+                  "attrs": {"output_scale": 0.5, "output_zero_point": zp, "axis": -1, "out_dtype": out_dtype},
+                  "expected": arr(np.array(exp).reshape(2, 5), out_dtype)})
+    c.append({"op": "qnn.quantize", "source": f"{QUANT}:91-102", "name": "scalar_float32_to_int8",
+              "inputs": {"data": arr(np.array(-63.5), "float32")},
+              "attrs": {"output_scale": 0.5, "output_zero_point": -1, "axis": -1, "out_dtype": "int8"},
+              "expected": arr(np.array(-128), "int8")})
+    d = np.array([-63.5, -63, -62.5, -62, -61.5, 30, 31, 31.5, 31.75, 32], dtype="float32").reshape(2, 5)
+    e = np.array([0, 1, 2, 3, 4, 243, 247, 249, 250, 251]).reshape(2, 5)
+    c.append({"op": "qnn.quantize", "source": f"{QUANT}:105-124", "name": "channelwise_axis_0",
+              "inputs": {"data": arr(d, "float32")},
+              "attrs": {"output_scale": [0.5, 0.25], "output_zero_point": [127, 123], "axis": 0, "out_dtype": "uint8"},
+              "expected": arr(e, "uint8")})
+    c.append({"op": "qnn.quantize", "source": f"{QUANT}:127-148", "name": "channelwise_axis_1",
+              "inputs": {"data": arr(d.T, "float32")},
+              "attrs": {"output_scale": [0.5, 0.25], "output_zero_point": [127, 123], "axis": -1,
+                        "out_dtype": "uint8"},
+              "expected": arr(e.T, "uint8")})
+    return c
+
+
+def dequantize_cases():
+    """test_op_qnn_dequantize.py: literal codes and their float32 values."""
+    c = []
+    f = np.array([-63.5, -63, -62.5, -62, -61.5, 62, 62.5, 63, 63.5, 64], dtype="float32")
+    c.append({"op": "qnn.dequantize", "source": f"{DEQUANT}:47-57", "name": "uint8_to_float32",
+              "inputs": {"data": arr(np.array([0, 1, 2, 3, 4, 251, 252, 253, 254, 255]).reshape(2, 5), "uint8")},
+              "attrs": {"input_scale": 0.5, "input_zero_point": 127, "axis": -1},
+              "expected": arr(f.reshape(2, 5), "float32")})
+    c.append({"op": "qnn.dequantize", "source": f"{DEQUANT}:60-74", "name": "int8_to_float32",
+              "inputs": {"data": arr(np.array([-128, -127, -126, -125, -124, 123, 124, 125, 126, 127]).reshape(2, 5),
+                                     "int8")},
+              "attrs": {"input_scale": 0.5, "input_zero_point": -1, "axis": -1},
+              "expected": arr(f.reshape(2, 5), "float32")})
+    c.append({"op": "qnn.dequantize", "source": f"{DEQUANT}:77-83", "name": "scalar_int8_to_float32",
+              "inputs": {"data": arr(np.array(-128), "int8")},
+              "attrs": {"input_scale": 0.5, "input_zero_point": -1, "axis": -1},
+              "expected": arr(np.array(-63.5), "float32")})
+    c.append({"op": "qnn.dequantize", "source": f"{DEQUANT}:86-92", "name": "int32_to_float32",
+              "inputs": {"data": arr(np.array([113, 29, -1052]), "int32")},
+              "attrs": {"input_scale": 0.0057968604, "input_zero_point": 0, "axis": -1},
+              "expected": arr(np.array([0.6550452, 0.16810896, -6.098297]), "float32")})
+    codes = np.array([0, 1, 2, 3, 4, 243, 247, 249, 250, 251]).reshape(2, 5)
+    vals = np.array([-63.5, -63, -62.5, -62, -61.5, 30, 31, 31.5, 31.75, 32]).reshape(2, 5)
+    c.append({"op": "qnn.dequantize", "source": f"{DEQUANT}:95-111", "name": "channelwise_axis_1",
+              "inputs": {"data": arr(codes.T, "uint8")},
+              "attrs": {"input_scale": [0.5, 0.25], "input_zero_point": [127, 123], "axis": -1},
+              "expected": arr(vals.T, "float32")})
+    c.append({"op": "qnn.dequantize", "source": f"{DEQUANT}:114-128", "name": "channelwise_axis_0",
+              "inputs": {"data": arr(codes, "uint8")},
+              "attrs": {"input_scale": [0.5, 0.25], "input_zero_point": [127, 123], "axis": 0},
+              "expected": arr(vals, "float32")})
+    c.append({"op": "qnn.dequantize", "source": f"{DEQUANT}:131-142", "name": "per_tensor_vector_args",
+              "inputs": {"data": arr(np.array([0, 1, 2, 3, 4, 251, 252, 253, 254, 255]), "uint8")},
+              "attrs": {"input_scale": [0.5], "input_zero_point": [127], "axis": -1},
+              "expected": arr(f, "float32")})
+    return c
+
+
+def concatenate_cases():
+    """test_op_qnn_concatenate.py: int32 ramps; the goldens are the test's own expressions."""
+    c = []
+    x = np.arange(-32, 32, 1).reshape(1, 64)
+    y = np.arange(-64, 64, 2).reshape(1, 64)
+    s = float(np.float32((62 + 64) / (np.power(2, 32) - 1.0)))
+    for name, src, zps, ozp, gold in (
+            ("same_io_qnn_params", f"{CONCAT}:26-57", (0, 0), 0, np.concatenate((x, y), axis=0)),
+            ("different_io_qnn_params", f"{CONCAT}:60-93", (3, 4), 1, np.concatenate((x - 2, y - 3), axis=0)),
+            ("few_same_io_qnn_params", f"{CONCAT}:96-129", (0, 1), 1, np.concatenate((x + 1, y), axis=0)),
+            ("same_i_qnn_params", f"{CONCAT}:132-165", (0, 0), 1, np.concatenate((x + 1, y + 1), axis=0))):
+        c.append({"op": "qnn.concatenate", "source": src, "name": name,
+                  "inputs": {"data": [arr(x, "int32"), arr(y, "int32")]},
+                  "attrs": {"input_scales": [s, s], "input_zero_points": list(zps), "output_scale": s,
+                            "output_zero_point": ozp, "axis": 0},
+                  "expected": arr(gold, "int32")})
+    # test_call_input (:168-191): the two halves of a uint8 split, same params -> the input back
+    ones = np.ones(64, dtype="uint8")
+    c.append({"op": "qnn.concatenate", "source": f"{CONCAT}:168-191", "name": "call_input_split_halves",
+              "inputs": {"data": [arr(ones[:32], "uint8"), arr(ones[32:], "uint8")]},
+              "attrs": {"input_scales": [1.0, 1.0], "input_zero_points": [0, 0], "output_scale": 1.0,
+                        "output_zero_point": 0, "axis": 0},
+              "expected": arr(ones, "uint8")})
+    return c
+
+
+def _binary_case(op, src, name, x, y, ls, lz, rs, rz, os_, oz, expect):
+    return {"op": op, "source": src, "name": name,
+            "inputs": {"lhs": arr(np.array(x).reshape(1, 4), "uint8"), "rhs": arr(np.array(y).reshape(1, 4), "uint8")},
+            "attrs": {"lhs_scale": ls, "lhs_zero_point": lz, "rhs_scale": rs, "rhs_zero_point": rz,
+                      "output_scale": os_, "output_zero_point": oz},
+            "expected": arr(np.array(expect).reshape(1, 4), "uint8")}
+
+
+def mul_cases():
+    """test_op_qnn_mul.py: the test's golden is its own float64 expression (recover both operands,
+    multiply, np.around(v / s_out + zp_out), clip to uint8), evaluated here on its literal data."""
+    def golden(x, y, ls, lz, rs, rz, os_, oz):
+        xr = ls * (np.asarray(x) - lz)
+        yr = rs * (np.asarray(y) - rz)
+        return np.clip(np.around(xr * yr / os_ + oz), 0, 255).astype("uint8")
+
+    c = []
+    groups = [
+        (f"{MUL}:39-87", "same_io_qnn_params", (0.00784314, 127, 0.00784314, 127, 0.00784314, 127),
+         [(1, 153, 2, 178), (25, 1, 178, 216), (25, 153, 1, 165)],
+         [(204, 178, 1, 8), (204, 178, 191, 1), (204, 178, 1, 191)]),
+        (f"{MUL}:90-141", "different_io_qnn_params", (0.0156863, 127, 0.0117647, 85, 0.0235294, 128),
+         [(76, 140, 153, 172), (133, 140, 146, 153), (76, 140, 172, 146)],
+         [(136, 119, 128, 17), (136, 119, 111, 94), (136, 119, 17, 128)]),
+        (f"{MUL}:144-180", "saturation_same", (0.125, 0, 0.125, 0, 0.125, 0), [(255, 1, 1, 0)], [(255, 255, 128, 0)]),
+        (f"{MUL}:182-215", "saturation_out_scale", (0.125, 0, 0.125, 0, 0.25, 0), [(255, 1, 1, 0)],
+         [(255, 255, 127, 0)]),
+        (f"{MUL}:217-251", "saturation_all_diff", (0.5, 0, 0.25, 0, 0.125, 0), [(255, 0, 1, 0)], [(0, 128, 64, 0)]),
+    ]
+    for src, name, p, xs, ys in groups:
+        for i, (x, y) in enumerate(zip(xs, ys)):
+            c.append(_binary_case("qnn.mul", src, f"{name}_{i}", x, y, *p, golden(x, y, *p)))
+    return c
+
+
+def subtract_cases():
+    """test_op_qnn_subtract.py: literal operands and goldens."""
+    c = []
+    groups = [
+        (f"{SUB}:61-85", "same_io_qnn_params", (0.00784314, 127, 0.00784314, 127, 0.00784314, 127),
+         [(140, 153, 165, 178), (25, 153, 178, 216), (25, 153, 216, 165)],
+         [(204, 178, 165, 140), (204, 178, 191, 25), (204, 178, 25, 191)],
+         [(63, 102, 127, 165), (0, 102, 114, 255), (0, 102, 255, 101)]),
+        (f"{SUB}:88-112", "different_io_qnn_params", (0.0156863, 127, 0.0117647, 85, 0.0235294, 128),
+         [(76, 140, 153, 172), (133, 140, 146, 153), (76, 140, 172, 146)],
+         [(136, 119, 128, 17), (136, 119, 111, 94), (136, 119, 17, 128)],
+         [(68, 120, 123, 192), (106, 120, 128, 140), (68, 120, 192, 119)]),
+        (f"{SUB}:115-128", "saturation_same", (0.125, 0, 0.125, 0, 0.125, 0), [(255, 1, 1, 0)], [(255, 255, 128, 0)],
+         [(0, 0, 0, 0)]),
+        (f"{SUB}:130-142", "saturation_out_scale", (0.125, 0, 0.125, 0, 0.25, 0), [(255, 1, 200, 0)],
+         [(255, 255, 127, 0)], [(0, 0, 36, 0)]),
+        (f"{SUB}:144-156", "saturation_all_diff", (0.5, 0, 0.25, 0, 0.125, 0), [(255, 0, 1, 0)], [(0, 128, 64, 0)],
+         [(255, 0, 0, 0)]),
+    ]
+    for src, name, p, xs, ys, gs in groups:
+        for i, (x, y, g) in enumerate(zip(xs, ys, gs)):
+            c.append(_binary_case("qnn.subtract", src, f"{name}_{i}", x, y, *p, g))
+    return c
+
+
 def main():
     doc = {
         "about": "Literal known-answer vectors transcribed from the reference's unit tests "
                  "(CortexFoundation/tachikoma @ /root/reference). Generated by make_golden.py.",
         "pinned_config": {"target": "llvm (no -mcpu)", "compute_dtype": "int64", "rounding_default": "UPWARD"},
-        "cases": requantize_cases() + dense_cases() + conv_cases() + add_cases(),
+        "cases": requantize_cases() + dense_cases() + conv_cases() + add_cases() + quantize_cases() +
+                 dequantize_cases() + concatenate_cases() + mul_cases() + subtract_cases(),
     }
     path = os.path.join(HERE, "qnn_kats.json")
     with open(path, "w") as f:

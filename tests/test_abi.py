@@ -46,6 +46,9 @@ int main(void) {
   O(tk_tensor, shape) O(tk_tensor, byte_offset) O(tk_node, inputs) O(tk_node, n_outputs) O(tk_node, outputs) O(tk_node, ext)
   O(tk_node, attrs) O(tk_qnn_add_attrs, rhs) O(tk_qnn_add_attrs, lhs_upcast) O(tk_requantize_attrs, output_zero_point)
   O(tk_conv2d_attrs, kernel_zero_points) O(tk_array_meta, dtype)
+  P(tk_qparams_attrs) P(tk_qnn_binary_attrs) P(tk_concat_attrs) P(tk_transpose_attrs)
+  O(tk_qparams_attrs, zero_points) O(tk_qnn_binary_attrs, out) O(tk_qnn_binary_attrs, output_zero_point)
+  O(tk_concat_attrs, rq)
   return 0;
 }
 """
@@ -75,6 +78,14 @@ def test_ctypes_layout_matches_c(tmp_path):
         "tk_requantize_attrs.output_zero_point": _lib.tk_requantize_attrs.output_zero_point.offset,
         "tk_conv2d_attrs.kernel_zero_points": _lib.tk_conv2d_attrs.kernel_zero_points.offset,
         "tk_array_meta.dtype": _lib.tk_array_meta.dtype.offset,
+        "tk_qparams_attrs": ctypes.sizeof(_lib.tk_qparams_attrs),
+        "tk_qnn_binary_attrs": ctypes.sizeof(_lib.tk_qnn_binary_attrs),
+        "tk_concat_attrs": ctypes.sizeof(_lib.tk_concat_attrs),
+        "tk_transpose_attrs": ctypes.sizeof(_lib.tk_transpose_attrs),
+        "tk_qparams_attrs.zero_points": _lib.tk_qparams_attrs.zero_points.offset,
+        "tk_qnn_binary_attrs.out": _lib.tk_qnn_binary_attrs.out.offset,
+        "tk_qnn_binary_attrs.output_zero_point": _lib.tk_qnn_binary_attrs.output_zero_point.offset,
+        "tk_concat_attrs.rq": _lib.tk_concat_attrs.rq.offset,
     }
     for k, v in py.items():
         assert int(got[k]) == v, (k, got[k], v)

@@ -43,7 +43,26 @@ def test_launcher_gloo_rendezvous(tmp_path):
 def test_world_size_must_match_gpus(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "2")
     with pytest.raises(SystemExit, match="WORLD_SIZE=2 but --gpus 4"):
-        bench.main(["--gpus", "4"])
+        bench.main(["--gpus", "4", "--dist-backend", "gloo"])
+
+
+def test_more_gpus_than_visible_fails_before_any_rank(monkeypatch):
+    """--gpus N over RCCL with fewer visible GPUs stops at once with a clear message, before the
+    launcher starts ranks or init_process_group("nccl") could wait for a missing one."""
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    started = []
+    monkeypatch.setattr(bench, "launch_ranks", lambda n, cmd: started.append(n) or 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    with pytest.raises(SystemExit, match="--gpus 8 needs 8 visible GPUs.*shows 1"):
+        bench.main(["--gpus", "8"])
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    with pytest.raises(SystemExit, match="needs 8 visible GPUs"):
+        bench.main(["--gpus", "8"])
+    assert started == []
+    # gloo rehearses N ranks on one GPU: the launcher runs
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert bench.main(["--gpus", "2", "--dist-backend", "gloo"]) == 0 and started == [2]
 
 
 def test_parity_checker():

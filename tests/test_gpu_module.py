@@ -78,14 +78,23 @@ def test_graph_replay_equals_plain_run(device):
             images.append(bytes(m.trace_capture().bytes()))
     assert images[:3] == images[3:]
     assert images[0] != images[1]
-    # copy kernels, and memcpy nodes over 2 chains / 1 chain (the default spreads them over 4)
-    for mode in (1, 2, 5):
+    # copy kernels, memcpy nodes over 2 / 3 / 4 chains and 1 chain (the default packs the image)
+    for mode in (1, 2, 3, 4, 5):
         _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, mode), "tk_module_set_graph_copies")
         m.set_input("data", xs[1])
         m.run(trace=True)
         m.trace_capture().synchronize()
         assert bytes(m.trace_capture().bytes()) == images[1], mode
     _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, 0), "tk_module_set_graph_copies")
+    # packed capture with 1, 3 and more chunks than nodes; back-to-back runs (the two mirrors
+    # alternate, kernels of run k+1 overlap the copies of run k)
+    for chunks in (1, 3, 500, 8):
+        _lib.check(m.module.lib.tk_module_set_trace_chunks(m.module.handle, chunks), "tk_module_set_trace_chunks")
+        m.set_input("data", xs[2])
+        for _ in range(3):
+            m.run(trace=True)
+        m.trace_capture().synchronize()
+        assert bytes(m.trace_capture().bytes()) == images[2], chunks
     # a second image: its own graph; both images hold their own run
     cap2 = graph_executor.TraceCapture(m.module, m._meta)
     stream = torch.cuda.current_stream()
@@ -183,3 +192,32 @@ def test_export_library_reload_in_fresh_process(device, tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     exp = graph_ref.calibrate(model.mod, model.params, {"data": x}, backend="c")
     _compare(read_trace(out).records, exp)
+
+
+@pytest.mark.parametrize("mode", [0, 2, 4])
+def test_graph_mode_small_modules(device, mode):
+    """Graph runs of modules with 1-3 traced nodes (fewer than the copy chains): packed
+    and memcpy-node captures give the host-issued run's image."""
+    import numpy as np
+    from tachikoma_amd.relay import qnn
+    rng = np.random.default_rng(8)
+    x = relay.var("x", (3, 40), "int32")
+    e1 = qnn.op.requantize(x, relay.const(0.02), relay.const(1, "int32"), relay.const(0.5), relay.const(2, "int32"),
+                           out_dtype="int8")
+    e2 = relay.clip(e1, -20.0, 100.0)
+    e3 = relay.cast(e2, "int32")
+    for body in (e1, e2, e3):
+        lib = relay.build(relay.IRModule.from_expr(body), target="mi355x", params={})
+        m = graph_executor.GraphModule(lib["default"]())
+        _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, mode), "tk_module_set_graph_copies")
+        xv = rng.integers(-5000, 5000, (3, 40)).astype(np.int32)
+        m.set_input("x", xv)
+        m.module.use_graph = False
+        m.run(trace=True)
+        m.trace_capture().synchronize()
+        want = bytes(m.trace_capture().bytes())
+        m.module.use_graph = True
+        for _ in range(2):
+            m.run(trace=True)
+        m.trace_capture().synchronize()
+        assert bytes(m.trace_capture().bytes()) == want

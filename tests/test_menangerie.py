@@ -114,6 +114,42 @@ def test_fold_scale_axis_backward():
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4)
 
 
+def test_fold_scale_axis_add_constant_must_broadcast_on_channels():
+    """add(conv, b) * s[c] with b of shape (W,) on an NCHW output where W == C: b broadcasts along
+    W, not along channels, so the multiply must stay (MatchBroadcastToLeftAxes); b of shape
+    (C, 1, 1) folds."""
+    c = 6
+    x = relay.var("x", (1, 4, c, c))
+    rng = np.random.default_rng(7)
+    s = relay.const(rng.uniform(0.5, 1.5, (c, 1, 1)).astype(np.float32))
+    xv = rng.standard_normal((1, 4, c, c)).astype(np.float32)
+    for bshape, folds in (((c,), False), ((c, 1, 1), True), ((1, c, 1, 1), True)):
+        b = relay.const(rng.uniform(-1, 1, bshape).astype(np.float32))
+        mod = relay.IRModule.from_expr(relay.multiply(relay.add(_conv(x, c, 3, 4), b), s))
+        out = transform.fold_constant(transform.fold_scale_axis(mod))
+        assert ("multiply" not in _ops(out)) == folds, bshape
+        ref = list(graph_ref.calibrate(transform.fold_constant(mod), {}, {"x": xv}).values())[-1]
+        got = list(graph_ref.calibrate(out, {}, {"x": xv}).values())[-1]
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("groups,depthwise", [(1, False), (2, False), (8, True)])
+def test_fold_scale_axis_grouped_conv(groups, depthwise):
+    """ConvBackwardPrep folds only into groups == 1 or depthwise convs (fold_scale_axis.cc:986-987)."""
+    rng = np.random.default_rng(11)
+    x = relay.var("x", (1, 8, 5, 5))
+    w = rng.standard_normal((8, 8 // groups, 3, 3)).astype(np.float32)
+    conv = relay.nn.conv2d(x, relay.const(w), padding=(1, 1, 1, 1), groups=groups)
+    s = relay.const(rng.uniform(0.5, 1.5, (8, 1, 1)).astype(np.float32))
+    mod = relay.IRModule.from_expr(relay.multiply(conv, s))
+    out = transform.fold_constant(transform.fold_scale_axis(mod))
+    assert ("multiply" not in _ops(out)) == (groups == 1 or depthwise)
+    xv = rng.standard_normal((1, 8, 5, 5)).astype(np.float32)
+    ref = list(graph_ref.calibrate(transform.fold_constant(mod), {}, {"x": xv}).values())[-1]
+    got = list(graph_ref.calibrate(out, {}, {"x": xv}).values())[-1]
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("name", ["mnist", "mobilenet"])
 def test_quantize_menangerie(name):
     """relay.quantize of a parsed reference model: every batch norm of a conv -> bn chain is

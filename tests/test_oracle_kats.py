@@ -72,3 +72,87 @@ def test_power_of_two_int32_path_wraps():
     assert out[0] == ((2**31 - 1 + 8 - 2**32) >> 4)
     assert out[1] == ((2**31 - 8 + 8 - 2**32) >> 4)
     assert out[2] == ((-2**31 + 8) >> 4)
+
+
+# ---- the pre-quantized QNN ops
+
+def _p(v, dtype):
+    return np.array(v, dtype=dtype) if isinstance(v, list) else np.dtype(dtype).type(v)
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.quantize"), ids=lambda c: c["name"])
+def test_quantize_kat(case):
+    a = case["attrs"]
+    out = ref.quantize(load_array(case["inputs"]["data"]), _p(a["output_scale"], "float32"),
+                       _p(a["output_zero_point"], "int32"), axis=a["axis"], out_dtype=a["out_dtype"])
+    np.testing.assert_array_equal(out, load_array(case["expected"]))
+    assert out.dtype == np.dtype(a["out_dtype"])
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.dequantize"), ids=lambda c: c["name"])
+def test_dequantize_kat(case):
+    a = case["attrs"]
+    out = ref.dequantize(load_array(case["inputs"]["data"]), _p(a["input_scale"], "float32"),
+                         _p(a["input_zero_point"], "int32"), axis=a["axis"])
+    exp = load_array(case["expected"])
+    assert out.dtype == np.float32 and out.shape == exp.shape
+    np.testing.assert_array_equal(out, exp)
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.concatenate"), ids=lambda c: c["name"])
+def test_concatenate_kat(case):
+    a = case["attrs"]
+    out = ref.qnn_concatenate([load_array(d) for d in case["inputs"]["data"]],
+                              [np.float32(s) for s in a["input_scales"]],
+                              [np.int32(z) for z in a["input_zero_points"]], np.float32(a["output_scale"]),
+                              np.int32(a["output_zero_point"]), axis=a["axis"])
+    np.testing.assert_array_equal(out, load_array(case["expected"]))
+
+
+@pytest.mark.parametrize("op", ["qnn.mul", "qnn.subtract"])
+def test_binary_kats(op):
+    fn = ref.qnn_mul if op == "qnn.mul" else ref.qnn_subtract
+    cases = load_cases(op)
+    assert len(cases) == 9
+    for case in cases:
+        a = case["attrs"]
+        out = fn(load_array(case["inputs"]["lhs"]), load_array(case["inputs"]["rhs"]), np.float32(a["lhs_scale"]),
+                 np.int32(a["lhs_zero_point"]), np.float32(a["rhs_scale"]), np.int32(a["rhs_zero_point"]),
+                 np.float32(a["output_scale"]), np.int32(a["output_zero_point"]))
+        np.testing.assert_array_equal(out, load_array(case["expected"]), err_msg=case["name"])
+
+
+def test_quantize_rounding_and_int32_edges():
+    """llvm.round halves away from zero (0.5 -> 1, -0.5 -> -1, 2.5 -> 3), the division is one float32
+    rounding, and an int32 output clips at float32(2^31 - 1) = 2^31, which x86's cvttss2si turns
+    into INT32_MIN."""
+    x = np.array([0.25, 0.5, -0.5, 1.25, 2.5, -2.5, 3e9, -3e9], np.float32)
+    q = ref.quantize(x, np.float32(0.5), np.int32(0), out_dtype="int32")
+    assert q.tolist() == [1, 1, -1, 3, 5, -5, -2 ** 31, -2 ** 31]
+    # a value whose float32 quotient is not the float64 one: x / s rounded once in float32
+    x = np.array([0.1], np.float32)
+    s = np.float32(0.3)
+    assert ref.quantize(x, s, np.int32(0), out_dtype="int8")[0] == int(np.round(np.float32(x[0] / s)))
+
+
+def test_binary_broadcast_and_per_axis():
+    """qnn.add / subtract / mul broadcast like numpy (BroadcastRel) and take per-axis parameters
+    along each operand's axis (RequantizeOrUpcast / mul.cc per-channel branch)."""
+    rng = np.random.default_rng(0)
+    a = rng.integers(-128, 128, (2, 3, 4, 5)).astype(np.int8)
+    b = rng.integers(-128, 128, (3, 1, 1)).astype(np.int8)
+    out = ref.qnn_subtract(a, b, np.float32(0.02), np.int32(1), np.float32(0.03), np.int32(-2), np.float32(0.04),
+                           np.int32(3))
+    ra = ref.requantize(a, np.float32(0.02), np.int32(1), np.float32(0.04), np.int32(3), out_dtype="int32")
+    rb = ref.requantize(b, np.float32(0.03), np.int32(-2), np.float32(0.04), np.int32(3), out_dtype="int32")
+    exp = np.clip(ra.astype(np.int64) - rb + 3, -128, 127).astype(np.int8)
+    np.testing.assert_array_equal(out, exp)
+    # per-channel mul: scales along axis 1 of both operands
+    ls = np.array([0.01, 0.02, 0.03], np.float32)
+    rs = np.array([0.5, 0.25, 0.125], np.float32)
+    c = rng.integers(-128, 128, (2, 3, 4, 5)).astype(np.int8)
+    out = ref.qnn_mul(a, c, ls, np.int32(0), rs, np.int32(0), np.float32(0.05), np.int32(0), lhs_axis=1, rhs_axis=1)
+    prod = a.astype(np.int64) * c
+    sc = np.array([np.float32(np.float64(x) * np.float64(y)) for x, y in zip(ls, rs)], np.float32)
+    exp = ref.requantize(prod, sc, np.int32(0), np.float32(0.05), np.int32(0), axis=1, out_dtype="int8")
+    np.testing.assert_array_equal(out, exp)

@@ -1,0 +1,71 @@
+#!/bin/bash
+# One launcher for every GPU-box session (replaces the per-session tools/gpu_r0*.sh scripts).
+# usage (through gpurun):  bash tools/gpu.sh <tag> <recipe> [recipe ...]
+# Each recipe runs under its own time limit; the first failure ends the call (no retries).
+# Outputs go under gpurun_out/<tag>/.
+#   suite      pytest -m gpu (one process)          smoke     __graft_entry__.smoke()
+#   bench      default bench line (20/5 steps)      host      same, --run-mode host
+#   findstep   the find step on this GPU, written as a tune table (commit it as profiles/<tag>_tune_table.json)
+#   copytrace  rocprofv3 memory-copy trace of 3 traced steps, graph then host-issued
+#   copyprobe  the step's 233 record copies isolated: host-issued, graph chains, packed chunks (tools/probe_copies)
+#   prof       rocprofv3 kernel-trace --stats of the default bench (compute + traced steps)
+#   pmc        the PMC HBM-traffic / stall passes (tools/pmc.sh)
+#   layers     rocprofv3 kernel trace of compute-only steps (per-layer durations)
+#   filesink   bench --sink file
+#   realized   realized relay.quantize ResNet-50 trace rate (tools/realized_times.py)
+#   hostmem    host DRAM write / read bandwidth of the GPU's NUMA node, alone and beside a traced bench
+#   tests:<k>  pytest -m gpu -k <k>
+set -o pipefail
+export TMPDIR=/tmp
+T=${1:?tag}
+shift
+O=gpurun_out/$T
+mkdir -p "$O"
+run() {  # run <seconds> <log> <cmd...>
+  local secs=$1 log=$2
+  shift 2
+  echo "[$(date +%T)] $*" | tee -a "$O/steps.log"
+  timeout -k 10 "$secs" "$@" > "$O/$log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] rc=$rc" | tee -a "$O/steps.log"
+  if [ $rc -ne 0 ]; then tail -30 "$O/$log"; exit $rc; fi
+}
+for r in "$@"; do
+  case "$r" in
+    suite) run 900 suite.log python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    smoke) run 300 smoke.log python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run 400 bench.json python3 -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    findstep) run 400 bench_find.json python3 -u bench.py --gpus 1 --steps 5 --warmup 2 --skip-cpu \
+        --tune-table none --write-tune-table "$O/tune_table.json" --tune-report "$O/find_step.json" ;;
+    host) run 400 bench_host.json python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --run-mode host ;;
+    copytrace)
+      run 400 copytrace_graph.log rocprofv3 --memory-copy-trace --output-format csv -d "$O/copy_graph" -o run -- \
+        python3 -u bench.py --steps 3 --warmup 1 --skip-cpu
+      run 400 copytrace_host.log rocprofv3 --memory-copy-trace --output-format csv -d "$O/copy_host" -o run -- \
+        python3 -u bench.py --steps 3 --warmup 1 --skip-cpu --run-mode host ;;
+    copyprobe) run 300 copyprobe.jsonl ./tools/probe_copies tools/resnet50_b64_record_sizes.txt 3 ;;
+    prof) run 400 prof.log rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
+        python3 -u bench.py --skip-cpu ;;
+    pmc) run 900 pmc.log bash tools/pmc.sh "$O/pmc" "$O/pmc/summary.json" ;;
+    layers) run 400 layers.log rocprofv3 --kernel-trace --output-format csv -d "$O/layers" -o run -- \
+        python3 -u bench.py --steps 3 --warmup 1 --skip-cpu --no-trace ;;
+    filesink) run 600 bench_file.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file --out-dir /tmp ;;
+    realized) run 600 realized.log python3 -u tools/realized_times.py ;;
+    hostmem)
+      # host DRAM bandwidth of the GPU's NUMA node, alone and while a traced bench writes its image
+      node=$(python3 -c 'import sys; sys.path.insert(0, "."); from tachikoma_amd import shard; print(shard.pci_numa_node(shard.gpu_pci_address(0)))')
+      echo "gpu numa node $node" | tee -a "$O/steps.log"
+      run 120 hostmem_alone8.jsonl ./tools/probe_hostmem "$node" 8 3 256
+      run 120 hostmem_alone14.jsonl ./tools/probe_hostmem "$node" 14 3 256
+      (timeout -k 10 400 python3 -u bench.py --steps 40 --warmup 3 --skip-cpu > "$O/bench_beside_probe.json" \
+        2> "$O/bench_beside_probe.err"; echo "bench rc=$?" >> "$O/steps.log") &
+      bpid=$!
+      for i in $(seq 1 120); do grep -q "trace image" "$O/bench_beside_probe.err" 2>/dev/null && break; sleep 1; done
+      sleep 8
+      run 120 hostmem_beside_bench.jsonl ./tools/probe_hostmem "$node" 8 4 256
+      wait $bpid ;;
+    tests:*) run 900 "tests_${r#tests:}.log" python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
+        --timeout-method thread -k "${r#tests:}" ;;
+    *) echo "unknown recipe $r"; exit 2 ;;
+  esac
+done

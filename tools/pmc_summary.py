@@ -110,6 +110,21 @@ def main():
     # which kernels these counters belong to: bench.py takes the traffic from the summary whose
     # library digest equals the loaded library's (else the newest by this UTC stamp)
     s["created_utc"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+    # and which kernel mix: the tune table the passes replayed (bench --tune-table), by digest
+    s["tune_table"] = wl[wl.index("--tune-table") + 1] if "--tune-table" in wl else "auto"
+    s["tune_table_digest"] = None
+    if s["tune_table"] == "auto":  # what bench.py's default resolves to
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        s["tune_table"] = bench.find_tune_table(model, batch)
+    if s["tune_table"] and s["tune_table"] != "none":
+        try:
+            sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            from tachikoma_amd.relay.device_module import tune_table_digest
+            with open(s["tune_table"]) as f:
+                s["tune_table_digest"] = tune_table_digest(json.load(f)["entries"])
+        except Exception as e:  # noqa: BLE001
+            print(f"  (tune table digest unavailable: {e})")
     try:
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from tachikoma_amd import _lib
