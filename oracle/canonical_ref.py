@@ -54,6 +54,10 @@ def eval_op(op, args):
         if "vector" in op.consts:
             return _wrap(x.astype(np.int64) - _axis_vec(op.consts["vector"], x.ndim, a["axis"]), dt)
         return _wrap(x.astype(np.int64) - a["scalar"], dt)
+    if op.op == "add" and len(args) == 2 and dt == "int64":
+        with np.errstate(over="ignore"):
+            return (np.asarray(x, np.int64).astype(np.uint64) + np.asarray(args[1], np.int64).astype(np.uint64)
+                    ).astype(np.int64)
     if op.op == "add":
         if "scalar" in a:
             return _wrap(x.astype(np.int64) + a["scalar"], dt)
@@ -67,6 +71,27 @@ def eval_op(op, args):
         m = _axis_vec(op.consts["multipliers"], x.ndim, a["axis"])
         s = _axis_vec(op.consts["shifts"], x.ndim, a["axis"])
         return _qms_general(x, np.broadcast_to(m, x.shape), np.broadcast_to(s, x.shape))
+    if op.op in ("left_shift", "right_shift", "multiply"):
+        # int64 steps of FixedPointMultiplyToNearest (src/relay/qnn/utils.cc:59-216), wrapping
+        v = np.int64(a["scalar"]) if "scalar" in a else _axis_vec(op.consts["vector"], x.ndim, a["axis"])
+        x64 = np.asarray(x, np.int64)
+        with np.errstate(over="ignore"):
+            if op.op == "left_shift":
+                y = (x64.astype(np.uint64) << np.asarray(v).astype(np.uint64)).astype(np.int64)
+            elif op.op == "right_shift":
+                y = x64 >> np.asarray(v).astype(np.int64)
+            else:
+                y = (x64.astype(np.uint64) * np.asarray(v).astype(np.int64).astype(np.uint64)).astype(np.int64)
+        return _wrap(y, dt)
+    if op.op == "greater_equal":
+        return np.asarray(x) >= a["scalar"]
+    if op.op == "where":
+        pos, neg = op.consts["pos"], op.consts["neg"]
+        if "axis" in a:
+            pos, neg = _axis_vec(pos, x.ndim, a["axis"]), _axis_vec(neg, x.ndim, a["axis"])
+        else:
+            pos, neg = pos.reshape(()), neg.reshape(())
+        return np.where(x, pos, neg).astype(dt)
     if op.op == "clip":
         return np.clip(x, a["a_min"], a["a_max"]).astype(x.dtype)
     if op.op == "nn.relu":

@@ -27,8 +27,9 @@ debug executor dumps are those of that canonical graph.  This module rebuilds it
 
 Every canonical op keeps the plan record its value equals, where there is one (the contraction,
 the requantize / add / clip outputs), so that only the intermediates (int16 shifts, int32 partial
-requantize results) need computing when the dump is made.  TONEAREST requantize (lowered by the
-reference to multiply / add / shift sequences) is outside what this module rebuilds.
+requantize results) need computing when the dump is made.  TONEAREST requantize is lowered like
+the reference's FixedPointMultiplyToNearest (int64 cast, left_shift, multiply, greater_equal /
+where rounding constant, add, right_shift, cast).
 """
 from __future__ import annotations
 
@@ -166,8 +167,6 @@ class _Builder:
     def requantize_lower(self, x: str, attrs: Dict[str, Any], consts: Dict[str, np.ndarray], axis: int,
                          out_dtype: str) -> str:
         """RequantizeLowerInt (requantize.cc:195-273) on canonical tensor x."""
-        if attrs.get("rounding", "UPWARD") != "UPWARD":
-            raise UnsupportedError("canonical graph: TONEAREST requantize (multiply / add / shift lowering)")
         t = self.cast(x, "int32")
         if "input_zero_points" in consts:
             zp = consts["input_zero_points"]
@@ -175,7 +174,12 @@ class _Builder:
                           {"vector": np.asarray(zp, np.int32)}) if np.any(zp) else t
         else:
             t = self.subtract_scalar(t, attrs.get("input_zero_point", 0))
-        if "multipliers" in consts:
+        if attrs.get("rounding", "UPWARD") == "TONEAREST":
+            if "multipliers" in consts:
+                t = self.to_nearest(t, np.asarray(consts["multipliers"]), np.asarray(consts["shifts"]), axis)
+            elif attrs.get("mode", 3) != 0:
+                t = self.to_nearest(t, np.array([attrs["multiplier"]]), np.array([attrs["shift"]]), None)
+        elif "multipliers" in consts:
             t = self.emit("fixed_point_multiply_per_axis", [t], {"axis": axis}, self.t(t).shape, "int32",
                           {"multipliers": consts["multipliers"], "shifts": consts["shifts"]})
         elif attrs.get("mode", 2) != 0:  # identity: equal scales skip the multiply (requantize.cc:226)
@@ -190,6 +194,35 @@ class _Builder:
             lo, hi = _RANGE[out_dtype]
             t = self.cast(self.clip(t, lo, hi), out_dtype)
         return t
+
+    def to_nearest(self, t: str, ms: np.ndarray, ss: np.ndarray, axis: Optional[int]) -> str:
+        """FixedPointMultiplyToNearest (src/relay/qnn/utils.cc:59-109; per channel :137-216, axis not
+        None): in int64, [left_shift], multiply, add where(x >= 0, 2^(30+rs), 2^(30+rs) - 1),
+        right_shift by 31 + rs, cast to int32.  The zeros / full / broadcast_to operands are constants
+        after FoldConstant."""
+        shape = self.t(t).shape
+        ls = np.maximum(ss, 0).astype(np.int64)
+        rs = np.maximum(-ss, 0).astype(np.int64)
+        total = rs + 31
+        pos = (np.int64(1) << (total - 1)).astype(np.int64)
+        x = self.cast(t, "int64")
+
+        def operand(v: np.ndarray):
+            # scalar constant (per-tensor) or an axis-expanded vector (per-channel)
+            return ({"scalar": int(v[0])}, {}) if axis is None else ({"axis": axis}, {"vector": v.astype(np.int64)})
+
+        if np.any(ls):
+            a, c = operand(ls)
+            x = self.emit("left_shift", [x], a, shape, "int64", c)
+        a, c = operand(np.asarray(ms, np.int64))
+        x = self.emit("multiply", [x], a, shape, "int64", c)
+        ge = self.emit("greater_equal", [x], {"scalar": 0}, shape, "bool")
+        wa = {} if axis is None else {"axis": axis}
+        r = self.emit("where", [ge], wa, shape, "int64", {"pos": pos, "neg": pos - 1})
+        x = self.emit("add", [x, r], {}, shape, "int64")
+        a, c = operand(total)
+        x = self.emit("right_shift", [x], a, shape, "int64", c)
+        return self.cast(x, "int32")
 
     def lower(self, p) -> None:
         self.origin, self.k = p.name, 0

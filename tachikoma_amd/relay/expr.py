@@ -100,8 +100,14 @@ class Function:
 
 
 class IRModule:
-    def __init__(self, main: Function):
-        self.functions = {"main": main}
+    def __init__(self, main: Function, functions: Optional[Dict[str, Function]] = None):
+        """``functions``: further global functions beside ``main`` (relay.quantize's
+        partition_conversions adds quantize_inputs / quantized_main / dequantize_outputs)."""
+        self.functions = dict(functions or {})
+        self.functions["main"] = main
+
+    def get_global_vars(self) -> List[str]:
+        return list(self.functions)
 
     @staticmethod
     def from_expr(expr) -> "IRModule":

@@ -90,12 +90,18 @@ def eval_const_call(call: Call, args) -> np.ndarray:
 
 
 def rebuild(body: Expr, fn: Callable[[Call, list], Expr]) -> Expr:
-    """Post-order mutator: ``fn(call, new_args)`` returns the replacement of each call."""
+    """Post-order mutator: ``fn(call, new_args)`` returns the replacement of each call (tuples are
+    rebuilt around rewritten fields)."""
+    from .expr import Tuple
     new: Dict[int, Expr] = {}
     for n in post_order(body):
         if isinstance(n, Call):
             args = [new.get(id(x), x) for x in n.args]
             new[id(n)] = fn(n, args)
+        elif isinstance(n, Tuple):
+            fields = [new.get(id(x), x) for x in n.fields]
+            if any(x is not y for x, y in zip(fields, n.fields)):
+                new[id(n)] = Tuple(fields)
     return new.get(id(body), body)
 
 

@@ -46,6 +46,7 @@ _PATTERNS = {
     "nn.bias_add": kBroadcast, "qnn.add": kBroadcast, "add": kBroadcast, "multiply": kBroadcast,
     "left_shift": kBroadcast, "right_shift": kBroadcast, "subtract": kBroadcast,
     "fixed_point_multiply_per_axis": kBroadcast,  # transform.cc:4421-4432
+    "greater_equal": kBroadcast, "where": kBroadcast,  # TONEAREST requantize (FixedPointMultiplyToNearest)
     "nn.batch_flatten": kInjective, "reshape": kInjective, "nn.pad": kInjective,
     # pre-quantized graphs: the pattern of each op's canonical form (divide / round / add / clip /
     # cast; cast / subtract / multiply; requantizes + subtract / multiply; requantizes + concatenate)

@@ -723,12 +723,18 @@ def quantize(mod, params=None, dataset=None) -> IRModule:
     """quantize.py:330-379: prerequisite_optimize -> partition -> annotate -> calibrate ->
     [realize] -> FoldConstant, under the current ``qconfig``."""
     cfg = current_qconfig()
-    if cfg.partition_conversions != "disabled":
-        raise UnsupportedError("quantize: partition_conversions is not implemented")
+    if cfg.partition_conversions not in ("disabled", "enabled", "fully_integral"):
+        raise ValueError(f"partition_conversions={cfg.partition_conversions!r}")
     mod = prerequisite_optimize(mod, params)
     mod = partition(mod)
     mod = annotate(mod, _QuantizeContext())
     mod = calibrate(mod, dataset)
     if not cfg.do_simulation:
         mod = realize(mod)
-    return fold_constant(mod)
+    mod = fold_constant(mod)
+    if cfg.partition_conversions != "disabled":
+        # quantize.py:373-377
+        from .partition_conversions import partition_conversions
+        qd = {cfg.dtype_input, cfg.dtype_weight, cfg.dtype_activation}
+        return partition_conversions(mod, qd, cfg.partition_conversions == "fully_integral")
+    return mod

@@ -118,3 +118,28 @@ def test_canonical_values_equal_their_records(name):
     nodes = fused_nodes(canon)
     assert sum(len(n.ops) for n in nodes) == len(canon.ops)
     assert all(n.func_name.startswith("tvmgen_default_fused_") for n in nodes)
+
+
+def test_tonearest_requantize_lowering():
+    """TONEAREST requantize lowers like FixedPointMultiplyToNearest (src/relay/qnn/utils.cc:59-216):
+    int64 cast, multiply, greater_equal / where rounding constant, add, right_shift, cast -- per
+    tensor and per channel; the values still equal the plan's records and the ops fuse into the
+    producer's function (its name lists them)."""
+    from tachikoma_amd.relay import qnn
+    with qnn.op.requantize_config(rounding="TONEAREST"):
+        m = zoo.lenet5(batch=2)
+    plan = lower(m.mod, m.params)
+    assert all(o.attrs["rounding"] == "TONEAREST" for o in plan.ops if o.op == "qnn.requantize")
+    canon = canonicalize(plan)
+    kinds = [o.op for o in canon.ops]
+    assert "fixed_point_multiply" not in kinds and "fixed_point_multiply_per_axis" not in kinds
+    assert {"greater_equal", "where", "right_shift", "multiply"} <= set(kinds)
+    x = m.random_input()
+    vals = canonical_ref.evaluate(canon, {m.input_name: x, **{k: np.asarray(v) for k, v in m.params.items()}})
+    rec = graph_ref.calibrate(m.mod, m.params, {m.input_name: x})
+    checked = [op for op in canon.ops if op.record is not None]
+    for op in checked:
+        assert np.array_equal(vals[op.name], rec[op.record]), (op.name, op.op, op.record)
+    assert any(r.op == "qnn.requantize" for r in plan.ops if r.name in {o.record for o in checked})
+    names = [n.func_name for n in fused_nodes(canon)]
+    assert any("greater_equal_where" in n for n in names), names

@@ -162,7 +162,7 @@ def test_canonical_graph_json_layout():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,batch", [("resnet18", 2), ("mobilenet_v2", 1)])
+@pytest.mark.parametrize("name,batch", [("resnet18", 2), ("mobilenet_v2", 1), ("lenet5_tonearest", 2)])
 def test_canonical_debug_dump_matches_oracle(device, tmp_path, name, batch):
     """Every canonical fused node's dumped tensor -- plan records and the device-computed
     intermediates (int16 operand shifts, int32 partial requantize / add results) -- equals the
@@ -172,7 +172,12 @@ def test_canonical_debug_dump_matches_oracle(device, tmp_path, name, batch):
     from tachikoma_amd import relay, trace_format as tf
     from tachikoma_amd.contrib.debugger import debug_executor
 
-    model = zoo.MODELS[name](batch=batch)
+    if name.endswith("_tonearest"):
+        from tachikoma_amd.relay import qnn
+        with qnn.op.requantize_config(rounding="TONEAREST"):
+            model = zoo.MODELS[name.rsplit("_", 1)[0]](batch=batch)
+    else:
+        model = zoo.MODELS[name](batch=batch)
     x = model.random_input()
     lib = relay.build(model.mod, target="mi355x", params=model.params)
     mod = debug_executor.create(lib, tachikoma_amd.rocm(0), dump_root=str(tmp_path / "dbg"), granularity="canonical")

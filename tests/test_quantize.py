@@ -169,11 +169,96 @@ def test_unsupported_modes_fail_loudly():
     with pytest.raises(ValueError):
         with qconfig(calibrate_mode="kl_divergence"):
             quantize(relay.IRModule.from_expr(y), params)  # needs a dataset
-    with pytest.raises(UnsupportedError):
-        with qconfig(partition_conversions="enabled"):
+    with pytest.raises(ValueError):
+        with qconfig(partition_conversions="sometimes"):
             quantize(relay.IRModule.from_expr(y), params)
     with pytest.raises(AttributeError):
         qconfig(no_such_field=1)
+
+
+# ---- partition_conversions (python/tvm/relay/quantize/_partition_conversions.py), the structure
+# and the partitioned-vs-unpartitioned agreement of test_pass_auto_quantize.py:178-330
+
+BASE_CFG = {"skip_conv_layers": [], "skip_dense_layer": False, "dtype_input": "int8", "dtype_weight": "int8",
+            "dtype_activation": "int32"}
+
+
+def _eval(expr, params, inputs):
+    """The value of ``expr`` over graph inputs / params (oracle walker); tuples field by field."""
+    from tachikoma_amd.relay.expr import Tuple
+    if isinstance(expr, Tuple):
+        return [_eval(f, params, inputs) for f in expr.fields]
+    if isinstance(expr, relay.Var):
+        return inputs[expr.name_hint] if expr.name_hint in inputs else params[expr.name_hint]
+    mod = relay.IRModule.from_expr(expr)
+    names = {v.name_hint for v in mod["main"].params}
+    recs = graph_ref.calibrate(mod, {k: v for k, v in params.items() if k in names},
+                               {k: v for k, v in inputs.items() if k in names})
+    return list(recs.values())[-1]
+
+
+def _verify_partition(mod, params, inputs):
+    from tachikoma_amd.relay.expr import Tuple
+    with qconfig(**BASE_CFG, partition_conversions="disabled"):
+        un = quantize(mod, params)
+    assert un.get_global_vars() == ["main"]
+    with qconfig(**BASE_CFG, partition_conversions="fully_integral"):
+        part = quantize(mod, params)
+    assert set(part.get_global_vars()) == {"main", "quantize_inputs", "quantized_main", "dequantize_outputs"}
+    pre, mid, post = part["quantize_inputs"], part["quantized_main"], part["dequantize_outputs"]
+    assert isinstance(pre.body, Tuple) and len(pre.body.fields) == len(mid.params)
+    ops = lambda f: {n.op for n in relay.post_order(f.body) if isinstance(n, relay.Call)}  # noqa: E731
+    assert ops(pre) <= {"add", "multiply", "right_shift", "clip", "round", "cast"}
+    assert ops(post) <= {"add", "multiply", "right_shift", "clip", "round", "cast"}
+    assert {n.dtype for n in relay.post_order(mid.body) if isinstance(n, (relay.Call, relay.Var))} <= \
+        {"int8", "int32"}
+    want = _eval(un["main"].body, params, inputs)
+    # main (the composition) and the three partitions run one after another agree with the
+    # unpartitioned result
+    np.testing.assert_array_equal(_eval(part["main"].body, params, inputs), want)
+    staged = dict(zip([p.name_hint for p in mid.params], _eval(pre.body, params, inputs)))
+    core = _eval(mid.body, params, staged)
+    np.testing.assert_array_equal(_eval(post.body, params, {post.params[0].name_hint: core}), want)
+    return part
+
+
+def test_partition_conversions_conv2d():
+    rng = np.random.default_rng(21)
+    x = relay.var("x", (1, 4, 16, 16), "float32")
+    w = relay.var("w", (4, 4, 3, 3), "float32")
+    y = relay.nn.conv2d(x, w, padding=(1, 1, 1, 1), channels=4, kernel_size=(3, 3))
+    params = {"w": rng.uniform(0, 1, (4, 4, 3, 3)).astype(np.float32)}
+    part = _verify_partition(relay.IRModule.from_expr(y), params,
+                             {"x": rng.uniform(0, 1, (1, 4, 16, 16)).astype(np.float32)})
+    # the partitioned main builds like any quantized graph
+    from tachikoma_amd.relay.build_module import build
+    assert build(part, params={}).plan.ops
+
+
+def test_partition_conversions_multiple_args():
+    rng = np.random.default_rng(22)
+    xs = [relay.var(f"x{i}", (1, 4, 16, 16), "float32") for i in (1, 2)]
+    ws = [relay.var(f"w{i}", (4, 4, 3, 3), "float32") for i in (1, 2)]
+    convs = [relay.nn.conv2d(x, w, padding=(1, 1, 1, 1), channels=4, kernel_size=(3, 3)) for x, w in zip(xs, ws)]
+    y = relay.add(*convs)
+    params = {f"w{i}": rng.uniform(0, 1, (4, 4, 3, 3)).astype(np.float32) for i in (1, 2)}
+    part = _verify_partition(relay.IRModule.from_expr(y), params,
+                             {f"x{i}": rng.uniform(0, 1, (1, 4, 16, 16)).astype(np.float32) for i in (1, 2)})
+    assert len(part["quantized_main"].params) == 2
+
+
+def test_partition_conversions_fails_when_not_integral():
+    """verify_partition_fails (test_pass_auto_quantize.py:198-209): 'enabled' always partitions;
+    'fully_integral' asserts when a partition is not a pure conversion / integer one."""
+    x = relay.var("x", (10, 10), "float32")
+    y = relay.var("y", (10, 10), "float32")
+    mod = relay.IRModule.from_expr(relay.add(x, y))
+    with qconfig(**BASE_CFG, partition_conversions="enabled"):
+        part = quantize(mod, {})
+    assert "quantized_main" in part.get_global_vars()
+    with pytest.raises(AssertionError):
+        with qconfig(**BASE_CFG, partition_conversions="fully_integral"):
+            quantize(mod, {})
 
 
 def test_round_away_and_oracle_agree_on_ties():

@@ -14,7 +14,7 @@
 #   filesink   bench --sink file
 #   realized   realized relay.quantize ResNet-50 trace rate (tools/realized_times.py)
 #   hostmem    host DRAM write / read bandwidth of the GPU's NUMA node, alone and beside a traced bench
-#   tests:<k>  pytest -m gpu -k <k>
+#   tests:<k>  pytest -m gpu -k <k>               file:<path>  pytest -m gpu of one test file
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:?tag}
@@ -64,6 +64,8 @@ for r in "$@"; do
       sleep 8
       run 120 hostmem_beside_bench.jsonl ./tools/probe_hostmem "$node" 8 4 256
       wait $bpid ;;
+    file:*) f=${r#file:}; run 900 "pytest_$(basename "$f" .py).log" python3 -u -m pytest "$f" -m gpu -x -v --timeout 300 \
+        --timeout-method thread ;;
     tests:*) run 900 "tests_${r#tests:}.log" python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
         --timeout-method thread -k "${r#tests:}" ;;
     *) echo "unknown recipe $r"; exit 2 ;;
