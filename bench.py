@@ -58,6 +58,9 @@ def parse(argv=None):
                    help="memory: trace image complete in pinned host RAM; file: also write every step's image "
                         "to trace.rank<r>.tkt, overlapped with the next step (two pinned images, writer thread)")
     p.add_argument("--out-dir", default="/tmp")
+    p.add_argument("--file-overlap", choices=["on", "off"], default="on",
+                   help="file sink: write image i while step i+1 runs (on) or finish each write before the next "
+                        "step starts (off: no D2H / writer concurrency, the contention check)")
     p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
     p.add_argument("--tune-report", default=None, help="write the find step's per-node kernel timings (JSON) here")
     p.add_argument("--tune-table", default="auto",
@@ -301,6 +304,21 @@ def check_gpu_count(args) -> None:
                          f"RCCL), this host shows {have}; use --dist-backend gloo to rehearse N ranks on one GPU")
 
 
+def mount_of(path: str):
+    """(mount point, filesystem type, device) of the mount holding `path` (/proc/mounts)."""
+    best = None
+    real = os.path.realpath(path)
+    try:
+        with open("/proc/mounts") as f:
+            for line in f:
+                dev, mnt, fstype = line.split()[:3]
+                if (real == mnt or real.startswith(mnt.rstrip("/") + "/")) and (best is None or len(mnt) > len(best[0])):
+                    best = (mnt, fstype, dev)
+    except OSError:
+        return None
+    return None if best is None else {"mount": best[0], "type": best[1], "device": best[2]}
+
+
 def main(argv=None) -> int:
     args = parse(argv)
     check_gpu_count(args)
@@ -420,6 +438,8 @@ def main(argv=None) -> int:
             d2h_ev[i][1].record(cap.capture_stream)
         if writer is not None:
             pending[k] = writer.submit(write_image, cap)
+            if args.file_overlap == "off":
+                pending[k].result()
 
     def drain():
         for k, f in enumerate(pending):
@@ -547,7 +567,8 @@ def main(argv=None) -> int:
         # the file on disk must carry exactly the records the device digested
         from tachikoma_amd.trace_format import trace_file_digest
         fd = trace_file_digest(path)
-        file_check = {"path": path, "file_digest": shard.hex64(fd), "device_digest": shard.hex64(digests[rank]),
+        file_check = {"path": path, "filesystem": mount_of(path), "overlap": args.file_overlap,
+                      "file_digest": shard.hex64(fd), "device_digest": shard.hex64(digests[rank]),
                       "equal": fd == (digests[rank] & 0xFFFFFFFFFFFFFFFF)}
         entries = [shard.ShardEntry(r, *shard.shard_range(B * world, world, r), shard.hex64(d),
                                     shard.shard_file(args.out_dir, r)) for r, d in enumerate(digests)]
@@ -688,7 +709,8 @@ def main(argv=None) -> int:
             "cpu_baseline": cpu,
             "parity": par,
             "file_sink": None if args.sink != "file" else
-            {k: ranks[0]["file_sink"].get(k) for k in ("achieved_GBps", "probe_GBps", "frac", "equal")},
+            {k: ranks[0]["file_sink"].get(k) for k in ("achieved_GBps", "probe_GBps", "frac", "equal", "overlap",
+                                                      "filesystem")},
             "ranks": ranks,
             "extra": {
                 "compute_only_ms_per_step": round(compute_ms, 3),

@@ -174,8 +174,8 @@ static int run_node(Node& n, hipStream_t s) {
 // Packed trace capture for tk_module_run_graph (the default graph copy mode): the node outputs that
 // have host destinations are gathered, chunk by chunk, into a device mirror of the host image range
 // they span (header bytes included, loaded once from the host image), and each chunk is copied to
-// host memory by ONE host-issued hipMemcpyAsync gated on an external event-record node after the
-// chunk's pack kernel.  Two mirrors alternate between runs, so a run's kernels overlap the previous
+// host memory by ONE host-issued hipMemcpyAsync gated on an event recorded after the graph that
+// ends with the chunk's pack kernel (one graph per chunk).  Two mirrors alternate between runs, so a run's kernels overlap the previous
 // run's copies (only the pack into a mirror waits for that mirror's last copies).
 struct PackRecHost {
   const void* src;
@@ -195,16 +195,16 @@ struct PackPlan {
   };
   std::vector<Chunk> chunks;
   void* table = nullptr;          // device PackRec entries of every chunk
-  std::vector<hipEvent_t> ev[2];  // per chunk, external event-record nodes of graph[m]
+  std::vector<hipEvent_t> ev[2];  // per chunk, recorded after its graph
   hipEvent_t mirror_done[2] = {nullptr, nullptr};
   bool mirror_used[2] = {false, false};
-  hipGraph_t g[2] = {nullptr, nullptr};
-  hipGraphExec_t ge[2] = {nullptr, nullptr};
+  std::vector<hipGraph_t> g[2];   // per mirror: one graph per chunk (+ a tail graph)
+  std::vector<hipGraphExec_t> ge[2];
   int next = 0;
   ~PackPlan() {
     for (int m = 0; m < 2; ++m) {
-      if (ge[m]) (void)hipGraphExecDestroy(ge[m]);
-      if (g[m]) (void)hipGraphDestroy(g[m]);
+      for (auto x : ge[m]) (void)hipGraphExecDestroy(x);
+      for (auto x : g[m]) (void)hipGraphDestroy(x);
       for (auto e : ev[m]) (void)hipEventDestroy(e);
       if (mirror_done[m]) (void)hipEventDestroy(mirror_done[m]);
       if (mirror[m]) (void)hipFree(mirror[m]);
@@ -665,52 +665,55 @@ static int build_pack_plan(tk_module* mod, const std::vector<void*>& dst, PackPl
     for (auto& e : plan->ev[m]) TK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   if (!mod->cap_s) TK_HIP(hipStreamCreateWithFlags(&mod->cap_s, hipStreamNonBlocking));
+  // one graph per chunk: the nodes up to the chunk's last producer and its pack kernel (a tail
+  // graph holds the nodes after the last chunk).  The copy of chunk c waits on an event recorded
+  // between graph launches c and c + 1; external event-record nodes inside one graph would do the
+  // same in one launch, but torch's bundled HIP runtime (7.0) refuses them in capture.
+  const int nseg = (int)plan->chunks.size() + (plan->chunks.back().after_node < nn - 1 ? 1 : 0);
   for (int m = 0; m < 2; ++m) {
     hipStream_t qs = mod->cap_s;
-    TK_HIP(hipStreamBeginCapture(qs, hipStreamCaptureModeThreadLocal));
-    int rc = TK_OK;
-    size_t c = 0;
-    for (int i = 0; i < nn && rc == TK_OK; ++i) {
-      rc = tk::run_node(mod->nodes[i], qs);
-      if (rc) {
-        tk::set_error("node " + std::to_string(i) + ": " + tk_last_error());
-        break;
+    int i = 0;
+    for (int seg = 0; seg < nseg; ++seg) {
+      const bool has_chunk = seg < (int)plan->chunks.size();
+      const int last = has_chunk ? plan->chunks[seg].after_node : nn - 1;
+      TK_HIP(hipStreamBeginCapture(qs, hipStreamCaptureModeThreadLocal));
+      int rc = TK_OK;
+      for (; i <= last && rc == TK_OK; ++i) {
+        rc = tk::run_node(mod->nodes[i], qs);
+        if (rc) tk::set_error("node " + std::to_string(i) + ": " + tk_last_error());
       }
-      while (c < plan->chunks.size() && plan->chunks[c].after_node == i && rc == TK_OK) {
-        const PackPlan::Chunk& ch = plan->chunks[c];
+      if (rc == TK_OK && has_chunk) {
+        const PackPlan::Chunk& ch = plan->chunks[seg];
         rc = tk::pack_records_impl((const char*)plan->table + ch.table_off * sizeof(PackRecHost), ch.n_rec, ch.blocks,
                                    plan->mirror[m], qs);
-        if (rc == TK_OK && hipEventRecordWithFlags(plan->ev[m][c], qs, hipEventRecordExternal) != hipSuccess) {
-          tk::set_error("tk_module_run_graph: event record in capture failed");
-          rc = TK_ERR_HIP;
-        }
-        ++c;
       }
-    }
-    hipGraph_t g = nullptr;
-    hipError_t e = hipStreamEndCapture(qs, &g);
-    if (rc) {
-      if (g) (void)hipGraphDestroy(g);
-      return rc;
-    }
-    if (e != hipSuccess || !g) {
-      (void)hipGetLastError();
-      tk::set_error(std::string("tk_module_run_graph: stream capture failed: ") + hipGetErrorString(e));
-      return TK_ERR_HIP;
-    }
-    plan->g[m] = g;
-    e = hipGraphInstantiate(&plan->ge[m], g, nullptr, nullptr, 0);
-    if (e != hipSuccess) {
-      tk::set_error(std::string("tk_module_run_graph: instantiate failed: ") + hipGetErrorString(e));
-      return TK_ERR_HIP;
+      hipGraph_t g = nullptr;
+      hipError_t e = hipStreamEndCapture(qs, &g);
+      if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+      }
+      if (e != hipSuccess || !g) {
+        (void)hipGetLastError();
+        tk::set_error(std::string("tk_module_run_graph: stream capture failed: ") + hipGetErrorString(e));
+        return TK_ERR_HIP;
+      }
+      plan->g[m].push_back(g);
+      hipGraphExec_t ge = nullptr;
+      e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+      if (e != hipSuccess) {
+        tk::set_error(std::string("tk_module_run_graph: instantiate failed: ") + hipGetErrorString(e));
+        return TK_ERR_HIP;
+      }
+      plan->ge[m].push_back(ge);
     }
   }
   *out = plan.release();
   return TK_OK;
 }
 
-// One packed traced run: the graph of mirror m (kernels, pack kernels, event records) on s, then the
-// chunk copies on cs, each after its event.
+// One packed traced run: the chunk graphs of mirror m (kernels, pack kernel) on s, each followed by
+// an event, and the chunk copies on cs, each after its event.
 static int run_packed(tk_module* mod, hipStream_t s, hipStream_t cs, void* const* host_dst) {
   const size_t nd = mod->nodes.size() * TK_MAX_NODE_OUTPUTS;
   std::vector<void*> dst(host_dst, host_dst + nd);
@@ -736,9 +739,11 @@ static int run_packed(tk_module* mod, hipStream_t s, hipStream_t cs, void* const
   // the pack into mirror m waits for that mirror's last copies (two runs ago); the records the
   // kernels overwrite are only read by the packs of the previous launch on the same stream
   if (plan->mirror_used[m]) TK_HIP(hipStreamWaitEvent(s, plan->mirror_done[m], 0));
-  TK_HIP(hipGraphLaunch(plan->ge[m], s));
-  for (size_t c = 0; c < plan->chunks.size(); ++c) {
+  for (size_t c = 0; c < plan->ge[m].size(); ++c) {
+    TK_HIP(hipGraphLaunch(plan->ge[m][c], s));
+    if (c >= plan->chunks.size()) break;  // the tail graph
     const PackPlan::Chunk& ch = plan->chunks[c];
+    TK_HIP(hipEventRecord(plan->ev[m][c], s));
     TK_HIP(hipStreamWaitEvent(cs, plan->ev[m][c], 0));
     TK_HIP(hipMemcpyAsync(plan->host_lo + ch.off, (char*)plan->mirror[m] + ch.off, (size_t)ch.len,
                           hipMemcpyDeviceToHost, cs));

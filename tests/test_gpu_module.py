@@ -88,7 +88,7 @@ def test_graph_replay_equals_plain_run(device):
     _lib.check(m.module.lib.tk_module_set_graph_copies(m.module.handle, 0), "tk_module_set_graph_copies")
     # packed capture with 1, 3 and more chunks than nodes; back-to-back runs (the two mirrors
     # alternate, kernels of run k+1 overlap the copies of run k)
-    for chunks in (1, 3, 500, 8):
+    for chunks in (1, 3, 200, 8):
         _lib.check(m.module.lib.tk_module_set_trace_chunks(m.module.handle, chunks), "tk_module_set_trace_chunks")
         m.set_input("data", xs[2])
         for _ in range(3):

@@ -240,7 +240,7 @@ def test_conv_layouts(device, tmp_path, data_layout, kernel_layout, c, o, k, gro
     # the NCHW / OIHW contraction of the same operands, in the data layout (the reference's own
     # layout test compares against nn.conv2d of the shifted operands in each layout)
     zw = e.args[3].data
-    nchw = ref.qnn_conv2d(x, wt, e.args[2].data, zw, padding=(1, 1, 1, 1) if k > 1 else (0, 0, 0, 0),
+    nchw = ref.qnn_conv2d(x, wt, e.args[2].data, zw, padding=(1, 1, 1, 1),
                           groups=groups) if k != 5 else None
     if nchw is not None:
         got = rec["%0"] if data_layout == "NCHW" else rec["%0"].transpose(0, 3, 1, 2)

@@ -7,6 +7,7 @@
 #   bench      default bench line (20/5 steps)      host      same, --run-mode host
 #   findstep   the find step on this GPU, written as a tune table (commit it as profiles/<tag>_tune_table.json)
 #   copytrace  rocprofv3 memory-copy trace of 3 traced steps, graph then host-issued
+#   copytraceprobe  rocprofv3 memory-copy trace of tools/probe_copies (torch-free; bench under it crashes at exit)
 #   copyprobe  the step's 233 record copies isolated: host-issued, graph chains, packed chunks (tools/probe_copies)
 #   prof       rocprofv3 kernel-trace --stats of the default bench (compute + traced steps)
 #   pmc        the PMC HBM-traffic / stall passes (tools/pmc.sh)
@@ -43,13 +44,19 @@ for r in "$@"; do
         python3 -u bench.py --steps 3 --warmup 1 --skip-cpu
       run 400 copytrace_host.log rocprofv3 --memory-copy-trace --output-format csv -d "$O/copy_host" -o run -- \
         python3 -u bench.py --steps 3 --warmup 1 --skip-cpu --run-mode host ;;
+    copytraceprobe) run 300 copytrace_probe.log rocprofv3 --memory-copy-trace --stats --output-format csv \
+        -d "$O/copy_probe" -o run -- ./tools/probe_copies tools/resnet50_b64_record_sizes.txt 1 ;;
     copyprobe) run 300 copyprobe.jsonl ./tools/probe_copies tools/resnet50_b64_record_sizes.txt 3 ;;
     prof) run 400 prof.log rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
         python3 -u bench.py --skip-cpu ;;
     pmc) run 900 pmc.log bash tools/pmc.sh "$O/pmc" "$O/pmc/summary.json" ;;
     layers) run 400 layers.log rocprofv3 --kernel-trace --output-format csv -d "$O/layers" -o run -- \
         python3 -u bench.py --steps 3 --warmup 1 --skip-cpu --no-trace ;;
-    filesink) run 600 bench_file.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file --out-dir /tmp ;;
+    filesink)
+      (df -hT /tmp . ; cat /proc/mounts) > "$O/mounts.txt" 2>&1
+      run 600 bench_file.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file --out-dir /tmp
+      run 600 bench_file_serial.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file \
+        --out-dir /tmp --file-overlap off ;;
     realized) run 600 realized.log python3 -u tools/realized_times.py ;;
     hostmem)
       # host DRAM bandwidth of the GPU's NUMA node, alone and while a traced bench writes its image
