@@ -568,6 +568,8 @@ def main(argv=None) -> int:
         from tachikoma_amd.trace_format import trace_file_digest
         fd = trace_file_digest(path)
         file_check = {"path": path, "filesystem": mount_of(path), "overlap": args.file_overlap,
+                      "writer": {k: os.environ[k] for k in ("TK_WRITE_THREADS", "TK_WRITE_PIECE_MB", "TK_WRITE_BUFFERED")
+                                 if os.environ.get(k)} or "default (O_DIRECT, 64 MiB pieces, 4 threads)",
                       "file_digest": shard.hex64(fd), "device_digest": shard.hex64(digests[rank]),
                       "equal": fd == (digests[rank] & 0xFFFFFFFFFFFFFFFF)}
         entries = [shard.ShardEntry(r, *shard.shard_range(B * world, world, r), shard.hex64(d),
@@ -710,7 +712,7 @@ def main(argv=None) -> int:
             "parity": par,
             "file_sink": None if args.sink != "file" else
             {k: ranks[0]["file_sink"].get(k) for k in ("achieved_GBps", "probe_GBps", "frac", "equal", "overlap",
-                                                      "filesystem")},
+                                                      "filesystem", "writer")},
             "ranks": ranks,
             "extra": {
                 "compute_only_ms_per_step": round(compute_ms, 3),

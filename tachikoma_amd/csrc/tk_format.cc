@@ -13,6 +13,7 @@
 #include <atomic>
 #include <cerrno>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -280,12 +281,20 @@ int tk_write_file(const char* path, const void* image, int64_t size) {
     return TK_ERR_INVALID_ARG;
   }
   const uint8_t* p = static_cast<const uint8_t*>(image);
-  constexpr int64_t kAlign = 4096, kDirectChunk = (int64_t)64 << 20, kBufChunk = (int64_t)256 << 20;
+  // the writer's shape can be overridden for sink experiments: TK_WRITE_THREADS (direct writers,
+  // default 4), TK_WRITE_PIECE_MB (direct piece, default 64), TK_WRITE_BUFFERED=1 (no O_DIRECT)
+  auto env = [](const char* k, int64_t d) {
+    const char* v = std::getenv(k);
+    return v && *v ? (int64_t)std::atoll(v) : d;
+  };
+  const int direct_threads = (int)std::max<int64_t>(1, std::min<int64_t>(64, env("TK_WRITE_THREADS", 4)));
+  const int64_t kDirectChunk = std::max<int64_t>(1, env("TK_WRITE_PIECE_MB", 64)) << 20;
+  constexpr int64_t kAlign = 4096, kBufChunk = (int64_t)256 << 20;
   const int64_t aligned = size / kAlign * kAlign;
   int e = 0;
   int fd = -1;
   bool direct = false;
-  if (aligned >= kDirectChunk && ((uintptr_t)p % kAlign) == 0) {
+  if (!env("TK_WRITE_BUFFERED", 0) && aligned >= kDirectChunk && ((uintptr_t)p % kAlign) == 0) {
     fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC | O_DIRECT, 0644);
     direct = fd >= 0;
   }
@@ -296,7 +305,7 @@ int tk_write_file(const char* path, const void* image, int64_t size) {
   }
   if (size > 0 && ::ftruncate(fd, (off_t)size) != 0) e = errno;
   if (!e && direct) {
-    e = write_range(fd, p, 0, aligned, kDirectChunk, 4);
+    e = write_range(fd, p, 0, aligned, kDirectChunk, direct_threads);
     if (e == EINVAL) {  // the filesystem refused direct I/O after all: everything buffered
       ::close(fd);
       direct = false;

@@ -12,7 +12,7 @@
 #   prof       rocprofv3 kernel-trace --stats of the default bench (compute + traced steps)
 #   pmc        the PMC HBM-traffic / stall passes (tools/pmc.sh)
 #   layers     rocprofv3 kernel trace of compute-only steps (per-layer durations)
-#   filesink   bench --sink file
+#   filesink   bench --sink file, overlapped and serial     filesweep  file sink writer shapes
 #   realized   realized relay.quantize ResNet-50 trace rate (tools/realized_times.py)
 #   hostmem    host DRAM write / read bandwidth of the GPU's NUMA node, alone and beside a traced bench
 #   tests:<k>  pytest -m gpu -k <k>               file:<path>  pytest -m gpu of one test file
@@ -57,6 +57,14 @@ for r in "$@"; do
       run 600 bench_file.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file --out-dir /tmp
       run 600 bench_file_serial.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file \
         --out-dir /tmp --file-overlap off ;;
+    filesweep)
+      # writer shapes with the overlapped sink: threads, piece size, buffered
+      for v in "TK_WRITE_THREADS=1" "TK_WRITE_THREADS=2" "TK_WRITE_THREADS=8" "TK_WRITE_PIECE_MB=256" \
+               "TK_WRITE_THREADS=2 TK_WRITE_PIECE_MB=256" "TK_WRITE_BUFFERED=1"; do
+        tag=$(echo "$v" | tr ' =' '__')
+        run 300 "bench_file_$tag.json" env $v python3 -u bench.py --gpus 1 --steps 8 --warmup 2 --skip-cpu \
+          --sink file --out-dir /tmp
+      done ;;
     realized) run 600 realized.log python3 -u tools/realized_times.py ;;
     hostmem)
       # host DRAM bandwidth of the GPU's NUMA node, alone and while a traced bench writes its image
@@ -64,12 +72,13 @@ for r in "$@"; do
       echo "gpu numa node $node" | tee -a "$O/steps.log"
       run 120 hostmem_alone8.jsonl ./tools/probe_hostmem "$node" 8 3 256
       run 120 hostmem_alone14.jsonl ./tools/probe_hostmem "$node" 14 3 256
-      (timeout -k 10 400 python3 -u bench.py --steps 40 --warmup 3 --skip-cpu > "$O/bench_beside_probe.json" \
+      # the bench's timed region (250 steps, ~33 s) starts a few seconds after its "trace image" line
+      (timeout -k 10 400 python3 -u bench.py --steps 250 --warmup 3 --skip-cpu > "$O/bench_beside_probe.json" \
         2> "$O/bench_beside_probe.err"; echo "bench rc=$?" >> "$O/steps.log") &
       bpid=$!
       for i in $(seq 1 120); do grep -q "trace image" "$O/bench_beside_probe.err" 2>/dev/null && break; sleep 1; done
-      sleep 8
-      run 120 hostmem_beside_bench.jsonl ./tools/probe_hostmem "$node" 8 4 256
+      sleep 5
+      run 120 hostmem_beside_bench.jsonl ./tools/probe_hostmem "$node" 8 6 256
       wait $bpid ;;
     file:*) f=${r#file:}; run 900 "pytest_$(basename "$f" .py).log" python3 -u -m pytest "$f" -m gpu -x -v --timeout 300 \
         --timeout-method thread ;;
