@@ -569,7 +569,7 @@ def main(argv=None) -> int:
         fd = trace_file_digest(path)
         file_check = {"path": path, "filesystem": mount_of(path), "overlap": args.file_overlap,
                       "writer": {k: os.environ[k] for k in ("TK_WRITE_THREADS", "TK_WRITE_PIECE_MB", "TK_WRITE_BUFFERED")
-                                 if os.environ.get(k)} or "default (O_DIRECT, 64 MiB pieces, 4 threads)",
+                                 if os.environ.get(k)} or "default (O_DIRECT, 256 MiB pieces, 2 threads)",
                       "file_digest": shard.hex64(fd), "device_digest": shard.hex64(digests[rank]),
                       "equal": fd == (digests[rank] & 0xFFFFFFFFFFFFFFFF)}
         entries = [shard.ShardEntry(r, *shard.shard_range(B * world, world, r), shard.hex64(d),
@@ -628,8 +628,8 @@ def main(argv=None) -> int:
                  "parity": parity.summary() if parity is not None else None,
                  "file_sink": file_check}
     if file_check is not None:
-        # disk-write probe on the same filesystem, same writer (tk_write_file: O_DIRECT, 64 MiB
-        # pieces, 4 threads), no GPU work beside it: the sink's ceiling on this box
+        # disk-write probe on the same filesystem, same writer (tk_write_file: O_DIRECT, 256 MiB
+        # pieces, 2 threads), no GPU work beside it: the sink's ceiling on this box
         probe_path = path + ".probe"
         best = float("inf")
         for _ in range(2):

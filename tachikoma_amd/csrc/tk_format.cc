@@ -271,9 +271,11 @@ static int write_range(int fd, const uint8_t* p, int64_t base, int64_t size, int
 }
 
 // A shard image is GBs, produced into pinned memory at the PCIe rate: it is written with O_DIRECT
-// (no page-cache copy on the writer's cores, no dirty-page writeback storm later) in 64 MiB
-// pieces by 4 threads -- every piece 4 KiB aligned in memory, on disk and in length -- and the
-// unaligned tail (< 4 KiB) through the page cache.  Filesystems without O_DIRECT (tmpfs) and
+// (no page-cache copy on the writer's cores, no dirty-page writeback storm later) in 256 MiB
+// pieces by 2 threads -- every piece 4 KiB aligned in memory, on disk and in length -- and the
+// unaligned tail (< 4 KiB) through the page cache.  Written while the next step's D2H copies land
+// in the other image, 2 x 256 MiB wrote 14.1 GB/s against 10.1 for 4 x 64 MiB (the round-3 shape)
+// on the same box (profiles/r04j_file_sink_writer_sweep.txt); alone both write ~14.5-15.  Filesystems without O_DIRECT (tmpfs) and
 // unaligned images take buffered pwrites of 256 MiB pieces from up to 8 threads.
 int tk_write_file(const char* path, const void* image, int64_t size) {
   if (!path || (!image && size) || size < 0) {
@@ -282,13 +284,13 @@ int tk_write_file(const char* path, const void* image, int64_t size) {
   }
   const uint8_t* p = static_cast<const uint8_t*>(image);
   // the writer's shape can be overridden for sink experiments: TK_WRITE_THREADS (direct writers,
-  // default 4), TK_WRITE_PIECE_MB (direct piece, default 64), TK_WRITE_BUFFERED=1 (no O_DIRECT)
+  // default 2), TK_WRITE_PIECE_MB (direct piece, default 256), TK_WRITE_BUFFERED=1 (no O_DIRECT)
   auto env = [](const char* k, int64_t d) {
     const char* v = std::getenv(k);
     return v && *v ? (int64_t)std::atoll(v) : d;
   };
-  const int direct_threads = (int)std::max<int64_t>(1, std::min<int64_t>(64, env("TK_WRITE_THREADS", 4)));
-  const int64_t kDirectChunk = std::max<int64_t>(1, env("TK_WRITE_PIECE_MB", 64)) << 20;
+  const int direct_threads = (int)std::max<int64_t>(1, std::min<int64_t>(64, env("TK_WRITE_THREADS", 2)));
+  const int64_t kDirectChunk = std::max<int64_t>(1, env("TK_WRITE_PIECE_MB", 256)) << 20;
   constexpr int64_t kAlign = 4096, kBufChunk = (int64_t)256 << 20;
   const int64_t aligned = size / kAlign * kAlign;
   int e = 0;

@@ -80,6 +80,32 @@ def summarise(d, launches=None, runs=None, model="resnet50", batch=64):
             if c != "_meta":
                 tot[c] += v
     n = len(steps)
+    # per kernel (template instance) and per dispatch of the step: where the LDS bank conflicts,
+    # VALU and HBM bytes are (attribute the conflict ratio per kernel)
+    fam = defaultdict(lambda: defaultdict(float))
+    disp = []
+    for i in sorted(steps):
+        m = steps[i]["_meta"]
+        name = m["kernel"].split("(")[0].replace("void ", "").replace("tk::", "").strip()
+        f = fam[name]
+        f["dispatches"] += 1
+        for c, v in steps[i].items():
+            if c != "_meta":
+                f[c] += v
+        lds_i = steps[i].get("SQ_INSTS_LDS", 0.0)
+        disp.append({"i": i, "kernel": name, "grid": m["grid"], "lds_bytes": m["lds"],
+                     "lds_conflict_per_inst": round(steps[i].get("SQ_LDS_BANK_CONFLICT", 0.0) / lds_i, 3) if lds_i else None,
+                     "SQ_INSTS_LDS": lds_i, "SQ_LDS_BANK_CONFLICT": steps[i].get("SQ_LDS_BANK_CONFLICT"),
+                     "hbm_bytes": steps[i].get("FETCH_SIZE", 0.0) * KIB * 2 + steps[i].get("WRITE_SIZE", 0.0) * KIB})
+    per_kernel = {}
+    for name, f in sorted(fam.items(), key=lambda kv: -kv[1].get("SQ_LDS_BANK_CONFLICT", 0.0)):
+        li = f.get("SQ_INSTS_LDS", 0.0)
+        per_kernel[name] = {"dispatches": int(f["dispatches"]), "SQ_INSTS_LDS": li,
+                            "SQ_LDS_BANK_CONFLICT": f.get("SQ_LDS_BANK_CONFLICT", 0.0),
+                            "conflict_per_lds_inst": round(f.get("SQ_LDS_BANK_CONFLICT", 0.0) / li, 3) if li else None,
+                            "share_of_conflicts": round(f.get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                                                        max(tot.get("SQ_LDS_BANK_CONFLICT", 0.0), 1.0), 3),
+                            "SQ_INSTS_VALU": f.get("SQ_INSTS_VALU", 0.0)}
     fetch = tot.get("FETCH_SIZE", 0.0) * KIB * 2
     write = tot.get("WRITE_SIZE", 0.0) * KIB
     out = {"launches_per_step": n,
@@ -88,7 +114,10 @@ def summarise(d, launches=None, runs=None, model="resnet50", batch=64):
            "hbm_bytes_per_launch": (fetch + write) / max(n, 1),
            "correction": "FETCH_SIZE x2 (gfx950 wide reads), KiB -> bytes",
            "counters_per_step": {c: v for c, v in sorted(tot.items())},
-           "example_dispatch": steps[0]["_meta"] if n else None}
+           "example_dispatch": steps[0]["_meta"] if n else None,
+           "lds_conflict_per_lds_inst": round(tot.get("SQ_LDS_BANK_CONFLICT", 0.0) / tot["SQ_INSTS_LDS"], 3)
+           if tot.get("SQ_INSTS_LDS") else None,
+           "per_kernel": per_kernel, "per_dispatch": disp}
     return out
 
 
@@ -137,6 +166,10 @@ def main():
           f"{s['write_bytes_per_step'] / 1e9:.3f} GB, per launch {s['hbm_bytes_per_launch'] / 1e6:.2f} MB")
     for c, v in s["counters_per_step"].items():
         print(f"  {c:24s} {v:16.0f}")
+    print(f"LDS bank conflicts per LDS instruction: {s['lds_conflict_per_lds_inst']}; per kernel:")
+    for k, v in s["per_kernel"].items():
+        print(f"  {v['share_of_conflicts']:6.3f} of conflicts, {v['conflict_per_lds_inst']} per inst, "
+              f"{v['dispatches']:3d} x {k}")
     if a.json:
         with open(a.json, "w") as f:
             json.dump(s, f, indent=1)

@@ -20,7 +20,7 @@ from collections import defaultdict
 def main(d, runs=18):
     path = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    fams = ("gemm_i8_kernel", "conv_img_kernel", "direct_conv_kernel", "conv_pf_kernel")
+    fams = ("gemm_i8_kernel", "conv_img_kernel", "direct_conv_kernel", "conv_pf_kernel", "dense_tile_kernel")
     gemm = [r for r in rows if any(f in r["Kernel_Name"] for f in fams)]
     # launches per step = the period of the kernel-name sequence (the module's find step launches
     # candidate kernels first: drop everything before the first whole period from the end)
@@ -31,14 +31,18 @@ def main(d, runs=18):
             names[-(n_steps + 1) * launches:-n_steps * launches] == names[-launches:]:
         n_steps += 1
     gemm = gemm[len(gemm) - n_steps * launches:]
-    copies = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if "copyBuffer" in r["Kernel_Name"]]
+    # traced steps: blit copy kernels (per-record copies under the profiler) or the packed capture's
+    # gather kernels (pack_records_kernel, one per image chunk)
+    copies = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
+              if "copyBuffer" in r["Kernel_Name"] or "pack_records_kernel" in r["Kernel_Name"]]
     phases = defaultdict(lambda: defaultdict(list))
     steps = defaultdict(int)
     for i in range(0, len(gemm) - launches + 1, launches):
         step = gemm[i:i + launches]
         t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
-        # a traced step overlaps its ~150 record copies; stray single copies do not count
-        traced = sum(1 for s, e in copies if s < t1 and e > t0) >= 10
+        # a traced step overlaps its ~150 record copies (or its 8 chunk gathers); stray single
+        # copies do not count
+        traced = sum(1 for s, e in copies if s < t1 and e > t0) >= 4
         ph = "traced" if traced else "compute-only"
         steps[ph] += 1
         for r in step:
