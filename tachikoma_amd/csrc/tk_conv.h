@@ -262,8 +262,10 @@ constexpr int kAlgoIm2col = 1, kAlgoImg = 2, kAlgoPf2 = 3, kAlgoPf3 = 4, kAlgoDe
 // Runs the conv block on the image-tile kernel when its plan applies (returns 1 and sets *rc;
 // algo 0: the cheapest plan by the planner's estimate), else returns 0 (im2col path).
 // `chunked`: the chunked weight image (NULL for 1x1 convs, whose packed weight has that layout).
-int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked, int algo,
-                 hipStream_t s, int* rc);
+int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked, void* scratch,
+                 int algo, hipStream_t s, int* rc);
+// scratch a 3x3 block's split-K image-tile plans need (their partial records), 0 if none apply
+int64_t conv_img_split_scratch_bytes(const ConvGeom& g);
 // The image-tile plans as algo values (16 + i), cheapest estimate first; returns how many exist.
 int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked,
                    int32_t* algos, int max_algos);

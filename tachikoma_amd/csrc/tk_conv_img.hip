@@ -39,7 +39,8 @@ struct ImgArgs {
   const int8_t* wimg;          // weight rows: chunked packing (3x3) or the plain one (1x1)
   int32_t ldw;                 // bytes per weight row
   int32_t nimg, ipt;           // images of the batch; whole images per workgroup
-  int32_t hr, hc, pl;          // patch rows / cols per image; patch pixels per channel group (ipt*hr*hc)
+  int32_t hr, hc, pl;          // patch rows / cols per image; slots per channel group (lead + ipt*hr*hc)
+  int32_t lead;                // 3x3: slots ahead of each channel group's pixels (the taps' reach, W + 1)
   int32_t ih0, iw0, ls;        // input pixel of patch (0, 0); input pixels per patch pixel (strided 1x1)
   int32_t ps;                  // patch pixels per output pixel (the stride of a 3x3)
   int32_t hw, p, nct;          // output pixels per image and per workgroup; 32-column tiles
@@ -55,13 +56,22 @@ struct ImgArgs {
   int32_t npass, cw;           // epilogue passes over the tile's columns (npass > 1: one image per
                                // workgroup, cw = hw / npass pixels per pass), or 1 pass of cw = hw
   int32_t skew;                // profiling: first-round workgroups start up to 3 x skew x s_sleep(8) late
+  // split K (3x3): MODE 1 workgroups reduce stages [z * stages / ksplit, (z + 1) * stages / ksplit)
+  // of their tile and store the raw sums as partial record z (NCHW int32, the conv record's layout,
+  // part + z * part_stride); MODE 2 workgroups (their own tiling) sum the ksplit partial records
+  // into their accumulators and run the block epilogue
+  int32_t ksplit;
+  int64_t part_stride;
+  int32_t* part;
 };
 
 // KT: 1 or 3 taps per axis; WM: 32-row wave groups (R = 32 * WM); CT: 32-column tiles per wave
 // (the waves of a row group take columns wn, wn + WN, ...); CC: input channels per K stage (32 or
 // 64 for 3x3 -- 64 halves the barrier-separated stages of the 7x7 / 14x14 layers' long K loops;
 // 32, 64 or 128 for 1x1: smaller stages for larger planes or two workgroups per CU).
-template <int KT, int WM, int CT, int CC>
+// MODE: 0 = the whole block; 1 = split-K partial sums (no epilogue); 2 = sum the partials + the
+// block epilogue (no K loop).
+template <int KT, int WM, int CT, int CC, int MODE = 0>
 __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, ImgArgs h) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   __shared__ int s_fast;
@@ -86,8 +96,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   if (h.skew && L < 8 * 256)
     for (int k = 0; k < ((L >> 3) & 3) * h.skew; ++k) __builtin_amdgcn_s_sleep(8);
 #endif
-  const int mt = w % h.mtiles;
-  const int img0 = (w / h.mtiles) * h.ipt;
+  // split K: the ksplit workgroups of a tile are adjacent (same XCD, same input patch in its L2)
+  const int S = MODE == 1 ? h.ksplit : 1;
+  const int tw = MODE == 1 ? w / S : w;
+  const int zs = w - tw * S;
+  const int mt = tw % h.mtiles;
+  const int img0 = (tw / h.mtiles) * h.ipt;
   const int nimg = min(h.ipt, h.nimg - img0);
   const int m0 = mt * R;
   const int hw = h.hw;
@@ -143,14 +157,17 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     if (k < ni) {
       const uint32_t q = (uint32_t)((wave + 4 * k) * 64 + lane);
       if (q < (uint32_t)h.pslots) {
-        const uint32_t grp = fdiv40(q, h.mg_pl), pix = q - grp * h.pl;
-        const uint32_t kk = fdiv40(pix, h.mg_img), r = pix - kk * (h.hr * h.hc);
-        const uint32_t hrow = fdiv40(r, h.mg_hc), hcol = r - hrow * h.hc;
-        const int ih = h.ih0 + (int)hrow * h.ls, iw = h.iw0 + (int)hcol * h.ls;
-        const int img = img0 + (int)kk;
-        if (img < h.nimg && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
-          srcs[k] = g.B + ((int64_t)grp * g.in_pix + ((int64_t)img * g.H + ih) * g.W + iw) * 16;
-          steps[k] = (uint32_t)h.pstep;
+        const uint32_t grp = fdiv40(q, h.mg_pl), pix0 = q - grp * h.pl;
+        if (grp < (uint32_t)(CC / 16) && pix0 >= (uint32_t)h.lead) {  // else lead / trailing slack: fill
+          const uint32_t pix = pix0 - h.lead;
+          const uint32_t kk = fdiv40(pix, h.mg_img), r = pix - kk * (h.hr * h.hc);
+          const uint32_t hrow = fdiv40(r, h.mg_hc), hcol = r - hrow * h.hc;
+          const int ih = h.ih0 + (int)hrow * h.ls, iw = h.iw0 + (int)hcol * h.ls;
+          const int img = img0 + (int)kk;
+          if (img < h.nimg && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
+            srcs[k] = g.B + ((int64_t)grp * g.in_pix + ((int64_t)img * g.H + ih) * g.W + iw) * 16;
+            steps[k] = (uint32_t)h.pstep;
+          }
         }
       } else if (q < (uint32_t)h.sslots) {
         const uint32_t wq = q - h.pslots;
@@ -161,6 +178,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
         }
       }
     }
+  }
+  // this split's first stage
+  const int st_lo = MODE == 1 ? (int)((int64_t)zs * h.stages / S) : 0;
+  if (MODE == 1 && st_lo) {
+#pragma unroll
+    for (int k = 0; k < kImgNI; ++k) srcs[k] += (int64_t)steps[k] * st_lo;
   }
   auto issue = [&](int slot) __attribute__((always_inline)) {
     int8_t* dst = smem + slot * h.stage_bytes + wave * 1024;
@@ -177,14 +200,31 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   int jn = 0;  // column tiles of this wave (wave-uniform)
 #pragma unroll
   for (int j = 0; j < CT; ++j) jn += (wn + WN * j < h.nct) ? 1 : 0;
+  // 3x3: the patch holds each image's input pixels densely (no halo): lane l's B chunk for tap
+  // (kh, kw) sits (kh - 1) * W + kw - 1 slots from its centre pixel, a uniform shift, so the 16
+  // lanes of a ds_read_b128 group -- 16 distinct residues of the output column mod 16 -- hit 16
+  // distinct 16-byte bank slots (the halo layout cost 3.4-6.5 extra LDS cycles per read,
+  // SQ_LDS_BANK_CONFLICT in profiles/r04j_pmc_block.json); taps that fall outside the image take
+  // the input zero point in registers (bit t of msk[j])
   int boff[CT];
+  [[maybe_unused]] uint32_t msk[CT];
 #pragma unroll
   for (int j = 0; j < CT; ++j) {
     const uint32_t c = (uint32_t)min((wn + WN * j) * 32 + (lane & 31), h.p - 1);
     const uint32_t kk = fdiv40(c, h.mg_hw), r = c - kk * hw;
     const uint32_t oh = fdiv40(r, h.mg_ow), ow = r - oh * g.OW;
-    boff[j] = (int)(((lane >> 5) * h.pl + kk * (h.hr * h.hc) + (oh * h.hc + ow) * h.ps) * 16);
+    boff[j] = (int)(((lane >> 5) * h.pl + h.lead + kk * (h.hr * h.hc) + (oh * h.hc + ow) * h.ps) * 16);
+    if constexpr (KT == 3) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ih = (int)oh * h.ps + t / 3 - 1, iw = (int)ow * h.ps + t % 3 - 1;
+        m |= (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) ? 1u << t : 0u;
+      }
+      msk[j] = m;
+    }
   }
+  [[maybe_unused]] const v4i fillv = {(int)g.fill, (int)g.fill, (int)g.fill, (int)g.fill};
   const int aoff = h.pslots * 16 + (wm * 32 + (lane & 31)) * WROW + (lane >> 5) * 16;
   const int hc = h.hc, pl16 = h.pl * 16;
 
@@ -198,10 +238,15 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       // weight row of the stage: [SUB][TAPS][32] (3x3: CC / 32 consecutive chunks of the chunked
       // packing; 1x1: TAPS = 1, the plain packing's CC channels)
       a[u] = *reinterpret_cast<const v4i*>(base + aoff + (s * TAPS + t) * 32);
-      const int bo = 2 * s * pl16 + (kh * hc + kw) * 16;
+      const int bo = 2 * s * pl16 + ((kh - KT / 2) * hc + (kw - KT / 2)) * 16;
 #pragma unroll
       for (int j = 0; j < CT; ++j)
-        if (j < jn) b[u][j] = *reinterpret_cast<const v4i*>(base + boff[j] + bo);
+        if (j < jn) {
+          b[u][j] = *reinterpret_cast<const v4i*>(base + boff[j] + bo);
+          if constexpr (KT == 3) {
+            if ((msk[j] >> t) & 1u) b[u][j] = fillv;
+          }
+        }
     };
     rd(0, 0);
 #pragma unroll
@@ -219,19 +264,60 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   // the LDS holds, since one workgroup per CU has nothing else to hide the L2 -> LDS latency
   // with); after the barrier of stage it, the slot read in step it - 1 is free for stage
   // it + ns - 1
-  const int nst = h.stages, ns = h.ns;
-  for (int st = 0; st < ns - 1 && st < nst; ++st) issue(st);
-  int cur = 0, nxt = ns - 1;
-  for (int it = 0; it < nst; ++it) {
-    wait_vm_any(min(ns - 2, nst - 1 - it) * ni);
-    lds_barrier();
-    if (it + ns - 1 < nst) {
-      issue(nxt);
-      nxt = nxt == ns - 1 ? 0 : nxt + 1;
+  if constexpr (MODE != 2) {
+    const int nst = MODE == 1 ? (int)((int64_t)(zs + 1) * h.stages / S) - st_lo : h.stages, ns = h.ns;
+    for (int st = 0; st < ns - 1 && st < nst; ++st) issue(st);
+    int cur = 0, nxt = ns - 1;
+    for (int it = 0; it < nst; ++it) {
+      wait_vm_any(min(ns - 2, nst - 1 - it) * ni);
+      lds_barrier();
+      if (it + ns - 1 < nst) {
+        issue(nxt);
+        nxt = nxt == ns - 1 ? 0 : nxt + 1;
+      }
+      if (MODE == 0 && has_add && it == nst - 1 && !TK_ABL(65536)) issue_residual(0);
+      compute(smem + cur * h.stage_bytes);
+      cur = cur == ns - 1 ? 0 : cur + 1;
     }
-    if (has_add && it == nst - 1 && !TK_ABL(65536)) issue_residual(0);
-    compute(smem + cur * h.stage_bytes);
-    cur = cur == ns - 1 ? 0 : cur + 1;
+  }
+  // the accumulator element (j, q) of this lane: channel row wm * 32 + (q & 3) + 8 (q >> 2) + 4 h
+  // of the tile, column (wn + WN j) * 32 + lane % 32 (an image pixel of the tile)
+  auto part_ptr = [&](int j, int32_t* base) __attribute__((always_inline)) -> int32_t* {
+    const int col = min((wn + WN * j) * 32 + (lane & 31), h.p - 1);
+    const uint32_t kk = fdiv40((uint32_t)col, h.mg_hw);
+    const int pix = col - (int)kk * hw;
+    const int img = min(img0 + (int)kk, h.nimg - 1);
+    return base + ((int64_t)img * g.M + m0 + wm * 32 + 4 * (lane >> 5)) * hw + pix;
+  };
+  if constexpr (MODE == 1) {
+    // raw sums of this split's stages -> partial record zs (every tile column stored once: columns
+    // past the tile's images are skipped)
+    int32_t* base = h.part + (int64_t)zs * h.part_stride;
+#pragma unroll
+    for (int j = 0; j < CT; ++j)
+      if (j < jn) {
+        const int col = (wn + WN * j) * 32 + (lane & 31);
+        const int kk = (int)fdiv40((uint32_t)min(col, h.p - 1), h.mg_hw);
+        if (col < h.p && img0 + kk < h.nimg) {
+          int32_t* o = part_ptr(j, base);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) o[((q & 3) + 8 * (q >> 2)) * hw] = acc[j][q];
+        }
+      }
+    return;
+  }
+  if constexpr (MODE == 2) {
+    if (has_add && !TK_ABL(65536)) issue_residual(0);
+#pragma unroll
+    for (int j = 0; j < CT; ++j)
+      if (j < jn) {
+        const int32_t* o = part_ptr(j, h.part);
+        for (int z = 0; z < h.ksplit; ++z) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            acc[j][q] = (int32_t)((uint32_t)acc[j][q] + (uint32_t)o[(int64_t)z * h.part_stride + ((q & 3) + 8 * (q >> 2)) * hw]);
+        }
+      }
   }
   wait_vm(0);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler
@@ -491,7 +577,7 @@ using ImgKernel = void (*)(GemmArgs, ImgArgs);
 
 template <int KT, int WM, int CC>
 ImgKernel img_kernel_cc(int ct) {
-  if constexpr (WM == 1) {
+  if constexpr (WM == 1 && KT == 1) {  // (3x3 with 7 column tiles per wave spills: not planned)
     if (ct == 7) return conv_img_kernel<KT, WM, 7, CC>;
   }
   return ct == 2 ? conv_img_kernel<KT, WM, 2, CC> : conv_img_kernel<KT, WM, 4, CC>;
@@ -506,22 +592,42 @@ ImgKernel img_kernel(int ct, int cc) {
   }
 }
 
+// 3x3 split-K kernels: the partial pass (MODE 1) and the epilogue pass (MODE 2, one 32-row
+// tiling, the stage width does not matter there)
+template <int WM, int MODE>
+ImgKernel img_kernel3(int ct, int cc) {
+  if constexpr (MODE == 2) {
+    return ct == 2 ? conv_img_kernel<3, WM, 2, 32, 2> : conv_img_kernel<3, WM, 4, 32, 2>;
+  } else {
+    if (cc == 64) return ct == 2 ? conv_img_kernel<3, WM, 2, 64, MODE> : conv_img_kernel<3, WM, 4, 64, MODE>;
+    return ct == 2 ? conv_img_kernel<3, WM, 2, 32, MODE> : conv_img_kernel<3, WM, 4, 32, MODE>;
+  }
+}
+
 struct ImgPlan {
   ImgArgs a;
   size_t lds;
   int kt, wm, ct, cc, occ;
   double cost;
+  // split K (ksplit > 1): `a` is the partial pass, `b` the epilogue pass
+  int ksplit;
+  ImgArgs b;
+  size_t lds_b;
+  int wm_b, ct_b;
 };
 
 uint64_t magic40(uint64_t d) { return ((1ull << 40) + d - 1) / d; }
 
 // Most output columns a workgroup holds: 4 waves x 7 column tiles (R = 32), 2 x 4 (R = 64).
 constexpr int kImgMaxCols = 4 * 7 * 32;
+constexpr int kImgMaxSplit = 4;  // split-K partial records a 3x3 block may need (scratch)
 
 // One candidate tiling (R rows, ipt images per workgroup, CC channels per stage, one or two
 // workgroups per CU, the epilogue in npass column passes); false if it does not fit.
+// mode: 0 the whole block, 1 / 2 the partial / epilogue pass of a split-K plan over ksplit splits
+// (mode 1 needs no epilogue staging, mode 2 no ring)
 bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R, int ipt, int CC, bool two,
-                   int npass, ImgPlan* out) {
+                   int npass, ImgPlan* out, int mode = 0, int ksplit = 1) {
   const int taps = kt * kt;
   const int hw = g.OH * g.OW;
   // several passes: one image per workgroup, each pass a whole number of 4-pixel groups per row
@@ -532,15 +638,19 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   const int wm = R / 32, wn = 4 / wm;
   const int ct_need = (nct + wn - 1) / wn;
   const int ct = ct_need <= 2 ? 2 : ct_need <= 4 ? 4 : ct_need <= 7 ? 7 : 0;
-  if (!ct || (ct == 7 && wm != 1)) return false;
+  if (!ct || (ct == 7 && (wm != 1 || kt == 3))) return false;
   ImgArgs x{};
   x.nimg = g.N;
   x.ipt = ipt;
-  x.hr = kt == 3 ? (g.OH - 1) * st + 3 : g.OH;
-  x.hc = kt == 3 ? (g.OW - 1) * st + 3 : g.OW;
-  x.pl = ipt * x.hr * x.hc;
-  x.ih0 = kt == 3 ? -1 : 0;
-  x.iw0 = kt == 3 ? -1 : 0;
+  // 3x3: the images' input pixels, dense, after `lead` slots of slack (reads up to W + 1 slots
+  // either side of a pixel land in the slack or a neighbour, and are replaced by the zero point);
+  // 1x1: the input pixels the (strided) outputs read
+  x.hr = kt == 3 ? g.H : g.OH;
+  x.hc = kt == 3 ? g.W : g.OW;
+  x.lead = kt == 3 ? g.W + 1 : 0;
+  x.pl = x.lead + ipt * x.hr * x.hc;
+  x.ih0 = 0;
+  x.iw0 = 0;
   x.ls = kt == 3 ? 1 : st;
   x.ps = kt == 3 ? st : 1;
   x.hw = hw;
@@ -550,7 +660,9 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   x.wgs = (int32_t)(((int64_t)g.N + ipt - 1) / ipt * x.mtiles);
   x.wgs8 = (x.wgs + 7) / 8 * 8;
   x.stages = g.cin_pad / CC;
-  x.pslots = CC / 16 * x.pl;
+  x.ksplit = ksplit;
+  if (mode == 1 && x.stages < ksplit) return false;
+  x.pslots = CC / 16 * x.pl + x.lead;  // + trailing slack after the last channel group
   x.wslot = taps * CC / 16 + 1;
   x.sslots = x.pslots + R * x.wslot;
   x.ni = ((x.sslots + 63) / 64 + 3) / 4;
@@ -566,20 +678,24 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   // ring depth: every slot the LDS budget holds (up to 8, no more than the stages need), at least
   // 3 where there are more than 2 stages and one workgroup per CU.  The budget is the CU's 160 KB, or half of it for two
   // resident workgroups (one's epilogue stores then overlap the other's K loop).
-  const size_t res_bytes = ga.has_add ? ((size_t)(npass > 1 ? cw : p) * R + 255) / 256 * 256 : 0;
-  const size_t extra = (size_t)R * sizeof(EpiRow) + 2048 + res_bytes;
-  const size_t tile = (size_t)R * x.tstride * 4;
+  const size_t res_bytes = ga.has_add && mode != 1 ? ((size_t)(npass > 1 ? cw : p) * R + 255) / 256 * 256 : 0;
+  const size_t extra = mode == 1 ? 0 : (size_t)R * sizeof(EpiRow) + 2048 + res_bytes;
+  const size_t tile = mode == 1 ? 0 : (size_t)R * x.tstride * 4;
   const int cap = env_int("TK_IMG_NS", 8);
   const size_t budget = (two ? 80 : 160) * 1024 - 64 - extra;
   if (tile > budget) return false;
-  x.ns = (int)std::min<size_t>({(size_t)cap, budget / x.stage_bytes, (size_t)x.stages + 1});
-  // one workgroup per CU needs a stage in flight while it computes; two may double-buffer (the
-  // other workgroup computes while this one waits)
-  if (x.ns < (x.stages > 2 && !two ? 3 : 2)) return false;
-  const size_t ring = (size_t)x.ns * x.stage_bytes;
+  size_t ring = 0;
+  if (mode != 2) {
+    const int kst = mode == 1 ? (x.stages + ksplit - 1) / ksplit : x.stages;  // a split's stages
+    x.ns = (int)std::min<size_t>({(size_t)cap, budget / x.stage_bytes, (size_t)kst + 1});
+    // one workgroup per CU needs a stage in flight while it computes; two may double-buffer (the
+    // other workgroup computes while this one waits)
+    if (x.ns < (kst > 2 && !two ? 3 : 2)) return false;
+    ring = (size_t)x.ns * x.stage_bytes;
+  }
   x.rowc_off = (int32_t)std::max(ring, tile);
-  x.lut_off = x.rowc_off + R * (int)sizeof(EpiRow);
-  x.res_off = x.lut_off + 2048;
+  x.lut_off = x.rowc_off + (mode == 1 ? 0 : R * (int)sizeof(EpiRow));  // (the partial pass has no epilogue)
+  x.res_off = x.lut_off + (mode == 1 ? 0 : 2048);
   const size_t lds = (size_t)x.res_off + res_bytes;
   if (lds > (two ? 80 : 160) * 1024 - 64) return false;
   x.runq = R * cw / 4;
@@ -602,15 +718,51 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   // the busiest wave's MFMA cycles at ~2.1 GHz) and epilogue = its record bytes at ~22 GB/s per CU
   // (~5.6 TB/s over 256 CUs), plus ~2 us of load latency per round.  One workgroup per CU runs
   // them back to back; two overlap one's epilogue with the other's K loop.
-  const double K = (double)taps * g.cin_pad;
-  const double bytes = R * K + (double)x.pl * g.cin_pad;
-  const double main_ns = std::max(bytes / 55.0, ct_need * K / 2.1);
-  const double epi_ns = (double)R * p * (ga.has_add ? 12.0 : 10.0) / 22.0;
+  const double K = (double)taps * g.cin_pad / (mode == 1 ? ksplit : 1);
+  const double bytes = R * K + (double)x.pl * g.cin_pad / (mode == 1 ? ksplit : 1);
+  // (mode 2: reading the ksplit partial tiles instead of the K loop; mode 1: storing one)
+  const double main_ns = mode == 2 ? (double)ksplit * R * p * 4 / 55.0 : std::max(bytes / 55.0, ct_need * K / 2.1);
+  const double epi_ns = mode == 1 ? (double)R * p * 4 / 22.0 : (double)R * p * (ga.has_add ? 12.0 : 10.0) / 22.0;
   const double per_cu = std::ceil(x.wgs / 256.0);
   const double lat = 2000.0;
   out->cost = two && per_cu >= 2 ? per_cu * std::max(main_ns, epi_ns) + lat + std::min(main_ns, epi_ns)
                                  : per_cu * (lat + main_ns + epi_ns);
   out->cost += per_cu * (npass - 1) * 1000.0;  // a store drain + barrier per extra pass
+  out->ksplit = 1;
+  return true;
+}
+
+// The 3x3 layers on small planes (7x7, 14x14) are bound by their L2 -> LDS bytes: every workgroup
+// streams its R weight rows of all K plus its images' patch, so wide tiles (more images, R = 64)
+// re-read less but leave CUs idle.  Split K keeps them: ksplit workgroups per wide tile each reduce
+// a share of the stages into a partial record (NCHW int32), and a second pass with small tiles
+// (R = 32, enough workgroups for the chip) sums the partials and runs the block epilogue.
+bool img_split_candidate(const ConvGeom& g, const GemmArgs& ga, int st, int R, int ipt, int CC, bool two, int ksplit,
+                         ImgPlan* out) {
+  ImgPlan pa{}, pb{}, best_b{};
+  if (!img_candidate(g, ga, 3, st, R, ipt, CC, two, 1, &pa, 1, ksplit)) return false;
+  const int tiles = pa.a.wgs, wgs = tiles * ksplit;
+  if (tiles >= 256 || wgs > 2048) return false;  // the plain plans already fill the chip
+  pa.a.wgs = wgs;
+  pa.a.wgs8 = (wgs + 63) / 64 * 64;  // (a multiple of 8 * ksplit: a tile's splits share an XCD)
+  // the epilogue pass: 32-row tiles of as many images as keep >= 512 workgroups
+  const int hw = g.OH * g.OW;
+  bool have_b = false;
+  for (int ipt_b = std::max(1, std::min(kImgMaxCols / hw, g.N)); ipt_b >= 1; --ipt_b)
+    for (int two_b = 1; two_b >= 0; --two_b)
+      if (g.O % 32 == 0 && img_candidate(g, ga, 3, st, 32, ipt_b, 32, two_b, 1, &pb, 2, ksplit) && pb.ct <= 4 &&
+          (!have_b || pb.cost < best_b.cost)) {
+        best_b = pb;
+        have_b = true;
+      }
+  *out = pa;
+  // (pa.cost counted rounds of `tiles` workgroups per CU; the pass runs ksplit times as many)
+  out->cost = pa.cost * std::ceil(wgs / 256.0) / std::ceil(tiles / 256.0) + best_b.cost + 1000.0;
+  out->ksplit = ksplit;
+  out->b = best_b.a;
+  out->lds_b = best_b.lds;
+  out->wm_b = best_b.wm;
+  out->ct_b = best_b.ct;
   return true;
 }
 
@@ -657,6 +809,19 @@ std::vector<ImgPlan> img_plans(const ConvGeom& g, const tk_conv2d_attrs* a, cons
       }
     }
   }
+  // split-K plans (3x3), after the plain ones so that the plain plans' algo numbers stay put
+  if (kt == 3 && env_int("TK_IMG_SPLIT", 1) && g.N * (int64_t)g.O * hw * 4 * kImgMaxSplit <= ((int64_t)1 << 31))
+    for (int S : {2, 4})
+      for (int R : {64, 32}) {
+        if (g.O % R || (force_r && R != force_r)) continue;
+        const int maxcols = R == 32 ? kImgMaxCols : 256;
+        for (int CC : {64, 32}) {
+          if (g.cin_pad % CC || (force_cc && CC != force_cc)) continue;
+          for (int ipt = std::min(maxcols / hw, g.N); ipt >= 1; --ipt)
+            for (int two = 0; two < 2; ++two)
+              if (img_split_candidate(g, ga, st, R, ipt, CC, two, S, &c)) out.push_back(c);
+        }
+      }
   return out;
 }
 
@@ -668,12 +833,46 @@ int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& 
   std::vector<int> order(plans.size());
   for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return plans[x].cost < plans[y].cost; });
+  // the find step times the first candidates only: give the split-K plans (whose two-pass cost the
+  // model knows least well) 5 of the first 14 places, the plain plans the other 9
+  {
+    std::vector<int> plain, split, head, rest;
+    for (int i : order) (plans[i].ksplit > 1 ? split : plain).push_back(i);
+    const size_t ns = std::min<size_t>(split.size(), 5), np = std::min<size_t>(plain.size(), 14 - ns);
+    for (size_t i = 0; i < plain.size(); ++i) (i < np ? head : rest).push_back(plain[i]);
+    for (size_t i = 0; i < split.size(); ++i) (i < ns ? head : rest).push_back(split[i]);
+    std::stable_sort(head.begin(), head.end(), [&](int x, int y) { return plans[x].cost < plans[y].cost; });
+    std::stable_sort(rest.begin(), rest.end(), [&](int x, int y) { return plans[x].cost < plans[y].cost; });
+    order = head;
+    order.insert(order.end(), rest.begin(), rest.end());
+  }
   for (int k = 0; k < (int)order.size() && k < max_algos; ++k) algos[k] = kAlgoImg0 + order[k];
   return (int)plans.size();
 }
 
-int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked, int algo,
-                 hipStream_t s, int* rc) {
+int64_t conv_img_split_scratch_bytes(const ConvGeom& g) {
+  // the partial records of a 3x3 split-K plan (img_plans lists them only for 3x3 blocks)
+  if (g.KH != 3 || g.KW != 3 || !env_int("TK_IMG_SPLIT", 1)) return 0;
+  const int64_t rec = (int64_t)g.N * g.O * g.OH * g.OW * 4;
+  return rec * kImgMaxSplit <= ((int64_t)1 << 31) && g.OH * g.OW <= kImgMaxCols ? rec * kImgMaxSplit : 0;
+}
+
+static int set_lds(ImgKernel kern, size_t lds, int* rc) {
+  if (lds <= 64 * 1024) return 0;
+  // dynamic LDS beyond 64 KiB must be allowed per kernel (the static s_fast word counts too)
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error(std::string("conv image-tile kernel: LDS attribute failed: ") + hipGetErrorString(e));
+    *rc = TK_ERR_HIP;
+    return 1;
+  }
+  return 0;
+}
+
+int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked, void* scratch,
+                 int algo, hipStream_t s, int* rc) {
   if (algo == kAlgoIm2col || algo == kAlgoPf2 || algo == kAlgoPf3) return 0;
   const std::vector<ImgPlan> plans = img_plans(g, a, ga, chunked != nullptr);
   if (plans.empty() && algo == 0) return 0;
@@ -688,26 +887,40 @@ int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga
   if (algo >= kAlgoImg0) {
     best = plans[algo - kAlgoImg0];
   } else {
+    // the library's own choice: the cheapest plain plan (split plans are the find step's to pick)
     for (const ImgPlan& p : plans)
-      if (p.cost < best.cost) best = p;
+      if (p.ksplit == 1 && p.cost < best.cost) best = p;
   }
   const int kt = best.kt;
   best.a.wimg = kt == 3 ? chunked : ga.A;
   best.a.ldw = kt == 3 ? 9 * g.cin_pad : ga.lda;
-  ImgKernel kern = kt == 3 ? (best.wm == 2 ? img_kernel<3, 2>(best.ct, best.cc) : img_kernel<3, 1>(best.ct, best.cc))
-                           : (best.wm == 2 ? img_kernel<1, 2>(best.ct, best.cc) : img_kernel<1, 1>(best.ct, best.cc));
-  if (best.lds > 64 * 1024) {
-    // dynamic LDS beyond 64 KiB must be allowed per kernel (the static s_fast word counts too)
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)best.lds);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      set_error(std::string("conv image-tile kernel: LDS attribute failed: ") + hipGetErrorString(e));
-      *rc = TK_ERR_HIP;
+  if (best.ksplit > 1) {
+    if (!scratch) {
+      set_error("tk_qnn_conv2d_block: split-K image-tile plan needs scratch (tk_conv2d_scratch_bytes)");
+      *rc = TK_ERR_INVALID_ARG;
       return 1;
     }
+    const int64_t stride = (int64_t)g.N * g.O * g.OH * g.OW;
+    best.a.part = best.b.part = static_cast<int32_t*>(scratch);
+    best.a.part_stride = best.b.part_stride = stride;
+    best.a.ksplit = best.b.ksplit = best.ksplit;
+    ImgKernel ka = best.wm == 2 ? img_kernel3<2, 1>(best.ct, best.cc) : img_kernel3<1, 1>(best.ct, best.cc);
+    ImgKernel kb = img_kernel3<1, 2>(best.ct_b, 32);
+    if (best.wm_b != 1) {
+      set_error("conv image-tile split-K: epilogue pass must use 32-row tiles");
+      *rc = TK_ERR_INVALID_ARG;
+      return 1;
+    }
+    if (set_lds(ka, best.lds, rc) || set_lds(kb, best.lds_b, rc)) return 1;
+    hipLaunchKernelGGL(ka, dim3((unsigned)best.a.wgs8), dim3(kGemmThreads), best.lds, s, ga, best.a);
+    hipLaunchKernelGGL(kb, dim3((unsigned)best.b.wgs8), dim3(kGemmThreads), best.lds_b, s, ga, best.b);
+  } else {
+    best.a.ksplit = 1;
+    ImgKernel kern = kt == 3 ? (best.wm == 2 ? img_kernel<3, 2>(best.ct, best.cc) : img_kernel<3, 1>(best.ct, best.cc))
+                             : (best.wm == 2 ? img_kernel<1, 2>(best.ct, best.cc) : img_kernel<1, 1>(best.ct, best.cc));
+    if (set_lds(kern, best.lds, rc)) return 1;
+    hipLaunchKernelGGL(kern, dim3((unsigned)best.a.wgs8), dim3(kGemmThreads), best.lds, s, ga, best.a);
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)best.a.wgs8), dim3(kGemmThreads), best.lds, s, ga, best.a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error(std::string("conv image-tile kernel: launch failed: ") + hipGetErrorString(e));

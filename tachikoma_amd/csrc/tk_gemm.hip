@@ -1696,8 +1696,10 @@ int64_t conv_scratch_bytes(const tk_tensor* data, const tk_tensor* weight, const
   const int ipt = mt1 ? conv_image_tiles(g, block, conv_needs_patch(weight, a)) : 0;
   const bool wide = mt1 && conv_wide(g, block, ipt);
   const SplitPlan sp = conv_split_plan(g, mt1, ipt, wide ? 2 * kBK : kBK);
-  if (sp.splits > 1) bytes += al256(sp.tiles * sp.splits * (int64_t)(2 * 16 * kGemmThreads) * 4);
-  return bytes;
+  int64_t split = sp.splits > 1 ? al256(sp.tiles * sp.splits * (int64_t)(2 * 16 * kGemmThreads) * 4) : 0;
+  // a conv block's split-K image-tile plans (3x3) use the same space for their partial records
+  if (block && !conv_needs_patch(weight, a)) split = std::max(split, al256(conv_img_split_scratch_bytes(g)));
+  return bytes + split;
 }
 
 static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor* weight, const void* packed,
@@ -1861,7 +1863,7 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
                                 ? (const int8_t*)packed + (int64_t)g.rows_pad * g.k_pad
                                 : nullptr;
     int irc = TK_OK;
-    if (conv_img_try(g, a, ga, chunked, blk->attrs->algo, s, &irc)) return irc;
+    if (conv_img_try(g, a, ga, chunked, sc, blk->attrs->algo, s, &irc)) return irc;
     const int algo = blk->attrs->algo;
     if (algo == kAlgoPf2 || algo == kAlgoPf3) {
       if (!conv_pf_applies(g, ga)) {
