@@ -742,7 +742,7 @@ bool img_split_candidate(const ConvGeom& g, const GemmArgs& ga, int st, int R, i
   ImgPlan pa{}, pb{}, best_b{};
   if (!img_candidate(g, ga, 3, st, R, ipt, CC, two, 1, &pa, 1, ksplit)) return false;
   const int tiles = pa.a.wgs, wgs = tiles * ksplit;
-  if (tiles >= 256 || wgs > 2048) return false;  // the plain plans already fill the chip
+  if (tiles > 256 || wgs > 2048) return false;  // the plain plans already fill the chip
   pa.a.wgs = wgs;
   pa.a.wgs8 = (wgs + 63) / 64 * 64;  // (a multiple of 8 * ksplit: a tile's splits share an XCD)
   // the epilogue pass: 32-row tiles of as many images as keep >= 512 workgroups
