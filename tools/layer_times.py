@@ -1,6 +1,7 @@
 """Per-layer kernel durations from a rocprofv3 kernel-trace CSV of `bench.py --no-trace`
 (maps the k-th launch of each kernel family per step onto the plan's exec groups)."""
 import csv
+import re
 import sys
 from collections import defaultdict
 
@@ -31,7 +32,7 @@ def main(path, model="resnet50", batch=64):
     # launches per step: the smallest period >= n of the kernel-name sequence (a split-K block
     # launches its partial tiles, then the reduce that runs the epilogue)
     names = [r["Kernel_Name"] for r in g_rows]
-    L = next(p for p in range(n, n + 8) if names[-p:] == names[-2 * p:-p])
+    L = next(p for p in range(n, n + 24) if names[-p:] == names[-2 * p:-p])
     # whole steps from the end (the module's find step launches candidate kernels first)
     k = 1
     while (k + 1) * L <= len(names) and names[-(k + 1) * L:-k * L] == names[-L:]:
@@ -47,14 +48,17 @@ def main(path, model="resnet50", batch=64):
         pending = 0.0
         for r in step:
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-            if "true, false, 1," in r["Kernel_Name"] and L > n:  # split-K partials: + the reduce
+            # split-K partial passes (im2col tiles' partials, image tiles' partial records): their
+            # time goes to the block's second launch (the reduce / epilogue pass)
+            if L > n and ("true, false, 1," in r["Kernel_Name"] or re.search(r"conv_img_kernel<\d+, \d+, \d+, \d+, 1>",
+                                                                             r["Kernel_Name"])):
                 pending += d
                 continue
             dur[i].append(d + pending)
             pending = 0.0
             if id(r) in prev_end:
                 gap[i].append((int(r["Start_Timestamp"]) - prev_end[id(r)]) / 1e3)
-            kname[i] = r["Kernel_Name"].split("(")[0].replace("void tk::", "")
+            kname[i] = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("tk::", "")
             i += 1
     print(f"{'layer':34s} {'us':>8s} {'GB/s':>8s} {'TOPS':>7s} {'gap us':>7s}  kernel")
     tot = tgap = 0
