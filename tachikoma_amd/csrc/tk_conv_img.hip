@@ -205,9 +205,10 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   // lanes of a ds_read_b128 group -- 16 distinct residues of the output column mod 16 -- hit 16
   // distinct 16-byte bank slots (the halo layout cost 3.4-6.5 extra LDS cycles per read,
   // SQ_LDS_BANK_CONFLICT in profiles/r04j_pmc_block.json); taps that fall outside the image take
-  // the input zero point in registers (bit t of msk[j])
+  // the input zero point: their reads are redirected to the channel group's first lead slot, which
+  // the ring fills with it (flg[j]: the column's image edges, bit 0 top, 1 bottom, 2 left, 3 right)
   int boff[CT];
-  [[maybe_unused]] uint32_t msk[CT];
+  [[maybe_unused]] uint32_t flg[CT];
 #pragma unroll
   for (int j = 0; j < CT; ++j) {
     const uint32_t c = (uint32_t)min((wn + WN * j) * 32 + (lane & 31), h.p - 1);
@@ -215,16 +216,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     const uint32_t oh = fdiv40(r, h.mg_ow), ow = r - oh * g.OW;
     boff[j] = (int)(((lane >> 5) * h.pl + h.lead + kk * (h.hr * h.hc) + (oh * h.hc + ow) * h.ps) * 16);
     if constexpr (KT == 3) {
-      uint32_t m = 0;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int ih = (int)oh * h.ps + t / 3 - 1, iw = (int)ow * h.ps + t % 3 - 1;
-        m |= (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) ? 1u << t : 0u;
-      }
-      msk[j] = m;
+      const int ih = (int)oh * h.ps, iw = (int)ow * h.ps;  // the centre tap's input pixel
+      flg[j] = (ih == 0 ? 1u : 0u) | (ih + 1 >= g.H ? 2u : 0u) | (iw == 0 ? 4u : 0u) | (iw + 1 >= g.W ? 8u : 0u);
     }
   }
-  [[maybe_unused]] const v4i fillv = {(int)g.fill, (int)g.fill, (int)g.fill, (int)g.fill};
+  [[maybe_unused]] const int hb = (lane >> 5) * h.pl * 16;  // lead slot 0 of this lane's channel group
   const int aoff = h.pslots * 16 + (wm * 32 + (lane & 31)) * WROW + (lane >> 5) * 16;
   const int hc = h.hc, pl16 = h.pl * 16;
 
@@ -238,14 +234,18 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       // weight row of the stage: [SUB][TAPS][32] (3x3: CC / 32 consecutive chunks of the chunked
       // packing; 1x1: TAPS = 1, the plain packing's CC channels)
       a[u] = *reinterpret_cast<const v4i*>(base + aoff + (s * TAPS + t) * 32);
-      const int bo = 2 * s * pl16 + ((kh - KT / 2) * hc + (kw - KT / 2)) * 16;
+      const int gs = 2 * s * pl16, bo = ((kh - KT / 2) * hc + (kw - KT / 2)) * 16;
+      // the image edges this tap crosses (a constant once the K loop is unrolled)
+      [[maybe_unused]] const uint32_t me =
+          KT == 3 ? (kh == 0 ? 1u : 0u) | (kh == 2 ? 2u : 0u) | (kw == 0 ? 4u : 0u) | (kw == 2 ? 8u : 0u) : 0u;
 #pragma unroll
       for (int j = 0; j < CT; ++j)
         if (j < jn) {
-          b[u][j] = *reinterpret_cast<const v4i*>(base + boff[j] + bo);
+          int off = boff[j] + bo;
           if constexpr (KT == 3) {
-            if ((msk[j] >> t) & 1u) b[u][j] = fillv;
+            if (me && (flg[j] & me)) off = hb;
           }
+          b[u][j] = *reinterpret_cast<const v4i*>(base + gs + off);
         }
     };
     rd(0, 0);
@@ -255,7 +255,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       if (!TK_ABL(512)) {
 #pragma unroll
         for (int j = 0; j < CT; ++j)
-          if (j < jn) acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1], b[ks & 1][j], acc[j], 0, 0, 0);
+          if (j < jn) {
+            acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks & 1], b[ks & 1][j], acc[j], 0, 0, 0);
+          }
       }
     }
   };
