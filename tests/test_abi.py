@@ -191,3 +191,25 @@ def test_conv_block_3x3_stage_widths():
 
     n512, n480 = count(512), count(480)
     assert n480 > 1 and n512 > n480, (n512, n480)
+
+
+def test_conv_block_scratch_holds_split_partials():
+    # a 3x3 block's scratch holds the four partial records its split-K image-tile plans may write
+    # (tk_conv_img.hip MODE 1 / 2); a 1x1 block reserves none of that
+    lib = _lib.load()
+
+    def scratch(c, h, o, k):
+        keep = []
+        x = _host_tensor((64, c, h, h), 0, 8, keep)
+        w = _host_tensor((o, c, k, k), 0, 8, keep)
+        a = _lib.tk_conv2d_attrs()
+        a.strides[:] = [1, 1]
+        p = k // 2
+        a.padding[:] = [p, p, p, p]
+        a.dilation[:] = [1, 1]
+        a.groups = 1
+        return lib.tk_conv2d_scratch_bytes(ctypes.byref(x), ctypes.byref(w), ctypes.byref(a), 1)
+
+    assert scratch(512, 7, 512, 3) >= 4 * 64 * 512 * 49 * 4
+    assert scratch(256, 14, 256, 3) >= 4 * 64 * 256 * 196 * 4
+    assert scratch(1024, 14, 256, 1) < 64 * 256 * 196 * 4
