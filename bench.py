@@ -693,8 +693,10 @@ def main(argv=None) -> int:
                          "traffic_bytes_per_step": None if pmc is None else int(pmc["per_step"]),
                          "launches_per_step": None if pmc is None else pmc["launches"],
                          "algorithmic_bytes_per_node": int(blk_bytes / max(n_launch, 1)),
-                         "kernel": "fused conv/dense layer blocks: conv_img_kernel (whole-image tiles, 7x7/14x14 "
-                                   "planes) and gemm_i8_kernel<*,*,block> (im2col tiles), v_mfma_i32_32x32x32_i8",
+                         "kernel": "fused conv/dense layer blocks, the find step's pick per node: conv_img_kernel "
+                                   "(whole-image tiles on 28x28/14x14/7x7 planes, 3x3 split-K as a partial and an "
+                                   "epilogue pass), gemm_i8_kernel<*,*,block> (im2col tiles), conv_pf_kernel "
+                                   "(persistent im2col), dense_tile_kernel (classifier); v_mfma_i32_32x32x32_i8",
                          "nodes_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
                          "algorithmic_bytes_per_step": int(blk_bytes),
                          "mfma_tops": round(achieved_ops / 1e12, 1),
