@@ -212,7 +212,8 @@ int64_t tk_conv2d_shadow_bytes(const tk_tensor* data);
 int tk_conv2d_make_shadow(const tk_tensor* data, void* shadow, void* stream);
 /* Device scratch of a prepared conv (tk_qnn_conv2d_prepared: block = 0; tk_qnn_conv2d_block:
  * block = 1): per-pixel patch sums when the kernel zero point is non-zero, plus split-K
- * partial tiles for layers whose tile grid cannot fill the GPU.  0 = no scratch needed. */
+ * partial tiles for layers whose tile grid cannot fill the GPU, or (3x3 blocks) up to four
+ * partial records of a split-K image-tile plan (tk_conv2d_block_algos).  0 = no scratch needed. */
 int64_t tk_conv2d_scratch_bytes(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* attrs,
                                 int block);
 /* qnn.conv2d on a prepared shadow + packed weight (what the executor runs).
