@@ -40,7 +40,9 @@ struct ImgArgs {
   int32_t ldw;                 // bytes per weight row
   int32_t nimg, ipt;           // images of the batch; whole images per workgroup
   int32_t hr, hc, pl;          // patch rows / cols per image; slots per channel group (lead + ipt*hr*hc)
-  int32_t lead;                // 3x3: slots ahead of each channel group's pixels (the taps' reach, W + 1)
+  int32_t lead;                // 3x3: slots ahead of each channel group's pixels (the taps' reach)
+  int32_t half;                // 3x3 stride 2 (even W): a row holds its even columns, then its odd ones
+                               // (half = W / 2), so a tap's lanes read consecutive slots; 0 = in order
   int32_t ih0, iw0, ls;        // input pixel of patch (0, 0); input pixels per patch pixel (strided 1x1)
   int32_t ps;                  // patch pixels per output pixel (the stride of a 3x3)
   int32_t hw, p, nct;          // output pixels per image and per workgroup; 32-column tiles
@@ -162,7 +164,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
           const uint32_t pix = pix0 - h.lead;
           const uint32_t kk = fdiv40(pix, h.mg_img), r = pix - kk * (h.hr * h.hc);
           const uint32_t hrow = fdiv40(r, h.mg_hc), hcol = r - hrow * h.hc;
-          const int ih = h.ih0 + (int)hrow * h.ls, iw = h.iw0 + (int)hcol * h.ls;
+          const int ih = h.ih0 + (int)hrow * h.ls;
+          const int iw = h.half ? ((int)hcol < h.half ? 2 * (int)hcol : 2 * ((int)hcol - h.half) + 1)
+                                : h.iw0 + (int)hcol * h.ls;
           const int img = img0 + (int)kk;
           if (img < h.nimg && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
             srcs[k] = g.B + ((int64_t)grp * g.in_pix + ((int64_t)img * g.H + ih) * g.W + iw) * 16;
@@ -214,7 +218,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     const uint32_t c = (uint32_t)min((wn + WN * j) * 32 + (lane & 31), h.p - 1);
     const uint32_t kk = fdiv40(c, h.mg_hw), r = c - kk * hw;
     const uint32_t oh = fdiv40(r, h.mg_ow), ow = r - oh * g.OW;
-    boff[j] = (int)(((lane >> 5) * h.pl + h.lead + kk * (h.hr * h.hc) + (oh * h.hc + ow) * h.ps) * 16);
+    boff[j] = (int)(((lane >> 5) * h.pl + h.lead + kk * (h.hr * h.hc) + oh * h.hc * h.ps + ow * (h.half ? 1 : h.ps)) * 16);
     if constexpr (KT == 3) {
       const int ih = (int)oh * h.ps, iw = (int)ow * h.ps;  // the centre tap's input pixel
       flg[j] = (ih == 0 ? 1u : 0u) | (ih + 1 >= g.H ? 2u : 0u) | (iw == 0 ? 4u : 0u) | (iw + 1 >= g.W ? 8u : 0u);
@@ -234,7 +238,10 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       // weight row of the stage: [SUB][TAPS][32] (3x3: CC / 32 consecutive chunks of the chunked
       // packing; 1x1: TAPS = 1, the plain packing's CC channels)
       a[u] = *reinterpret_cast<const v4i*>(base + aoff + (s * TAPS + t) * 32);
-      const int gs = 2 * s * pl16, bo = ((kh - KT / 2) * hc + (kw - KT / 2)) * 16;
+      // (stride-2 rows split by column parity: the centre column 2 ow is even slot ow, 2 ow - 1 odd
+      // slot half + ow - 1, 2 ow + 1 odd slot half + ow)
+      const int dx = KT == 3 && h.half ? (kw == 1 ? 0 : kw == 0 ? h.half - 1 : h.half) : kw - KT / 2;
+      const int gs = 2 * s * pl16, bo = ((kh - KT / 2) * hc + dx) * 16;
       // the image edges this tap crosses (a constant once the K loop is unrolled)
       [[maybe_unused]] const uint32_t me =
           KT == 3 ? (kh == 0 ? 1u : 0u) | (kh == 2 ? 2u : 0u) | (kw == 0 ? 4u : 0u) | (kw == 2 ? 8u : 0u) : 0u;
@@ -649,6 +656,7 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   // 1x1: the input pixels the (strided) outputs read
   x.hr = kt == 3 ? g.H : g.OH;
   x.hc = kt == 3 ? g.W : g.OW;
+  x.half = kt == 3 && st == 2 && g.W % 2 == 0 ? g.W / 2 : 0;
   x.lead = kt == 3 ? g.W + 1 : 0;
   x.pl = x.lead + ipt * x.hr * x.hc;
   x.ih0 = 0;
