@@ -425,6 +425,10 @@ ALGO_CASES = [
     # and 5 stages of a uint8 block with a residual join on a 7x7 plane
     (3, 192, 14, 64, 3, 2, "int8", 0, None, (0, 127)),
     (2, 320, 7, 64, 3, 1, "uint8", 129, (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
+    # round 4: split-K image plans over a stage count no split divides (5 stages of 32 channels),
+    # and a stride-2 3x3 on an odd input width (no column-parity patch), uint8 with a residual join
+    (4, 160, 7, 64, 3, 1, "int8", -3, None, (0, 127)),
+    (2, 64, 13, 64, 3, 2, "uint8", 131, (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
 ]
 
 
