@@ -601,15 +601,18 @@ ImgKernel img_kernel(int ct, int cc) {
   }
 }
 
-// 3x3 split-K kernels: the partial pass (MODE 1) and the epilogue pass (MODE 2, one 32-row
-// tiling, the stage width does not matter there)
-template <int WM, int MODE>
-ImgKernel img_kernel3(int ct, int cc) {
+// Split-K kernels: the partial pass (MODE 1) and the epilogue pass (MODE 2: one 32-row tiling for
+// 1x1 and 3x3 alike -- it has no K loop, so neither the taps nor the stage width matter there)
+template <int KT, int WM, int MODE>
+ImgKernel img_kernel_split(int ct, int cc) {
   if constexpr (MODE == 2) {
     return ct == 2 ? conv_img_kernel<3, WM, 2, 32, 2> : conv_img_kernel<3, WM, 4, 32, 2>;
   } else {
-    if (cc == 64) return ct == 2 ? conv_img_kernel<3, WM, 2, 64, MODE> : conv_img_kernel<3, WM, 4, 64, MODE>;
-    return ct == 2 ? conv_img_kernel<3, WM, 2, 32, MODE> : conv_img_kernel<3, WM, 4, 32, MODE>;
+    if constexpr (KT == 1) {
+      if (cc == 128) return ct == 2 ? conv_img_kernel<1, WM, 2, 128, MODE> : conv_img_kernel<1, WM, 4, 128, MODE>;
+    }
+    if (cc == 64) return ct == 2 ? conv_img_kernel<KT, WM, 2, 64, MODE> : conv_img_kernel<KT, WM, 4, 64, MODE>;
+    return ct == 2 ? conv_img_kernel<KT, WM, 2, 32, MODE> : conv_img_kernel<KT, WM, 4, 32, MODE>;
   }
 }
 
@@ -742,15 +745,16 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   return true;
 }
 
-// The 3x3 layers on small planes (7x7, 14x14) are bound by their L2 -> LDS bytes: every workgroup
-// streams its R weight rows of all K plus its images' patch, so wide tiles (more images, R = 64)
-// re-read less but leave CUs idle.  Split K keeps them: ksplit workgroups per wide tile each reduce
-// a share of the stages into a partial record (NCHW int32), and a second pass with small tiles
-// (R = 32, enough workgroups for the chip) sums the partials and runs the block epilogue.
-bool img_split_candidate(const ConvGeom& g, const GemmArgs& ga, int st, int R, int ipt, int CC, bool two, int ksplit,
-                         ImgPlan* out) {
+// The long-K layers on small planes (7x7, 14x14: 3x3, and the 1x1 reduces over 1024-2048 channels)
+// are bound by their L2 -> LDS bytes: every workgroup streams its R weight rows of all K plus its
+// images' patch, so wide tiles (more images, R = 64) re-read less but leave CUs idle.  Split K
+// keeps them: ksplit workgroups per wide tile each reduce a share of the stages into a partial
+// record (NCHW int32), and a second pass with small tiles (R = 32, enough workgroups for the
+// chip) sums the partials and runs the block epilogue.
+bool img_split_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R, int ipt, int CC, bool two,
+                         int ksplit, ImgPlan* out) {
   ImgPlan pa{}, pb{}, best_b{};
-  if (!img_candidate(g, ga, 3, st, R, ipt, CC, two, 1, &pa, 1, ksplit)) return false;
+  if (!img_candidate(g, ga, kt, st, R, ipt, CC, two, 1, &pa, 1, ksplit)) return false;
   const int tiles = pa.a.wgs, wgs = tiles * ksplit;
   if (tiles > 256 || wgs > 2048) return false;  // the plain plans already fill the chip
   pa.a.wgs = wgs;
@@ -760,7 +764,7 @@ bool img_split_candidate(const ConvGeom& g, const GemmArgs& ga, int st, int R, i
   bool have_b = false;
   for (int ipt_b = std::max(1, std::min(kImgMaxCols / hw, g.N)); ipt_b >= 1; --ipt_b)
     for (int two_b = 1; two_b >= 0; --two_b)
-      if (g.O % 32 == 0 && img_candidate(g, ga, 3, st, 32, ipt_b, 32, two_b, 1, &pb, 2, ksplit) && pb.ct <= 4 &&
+      if (g.O % 32 == 0 && img_candidate(g, ga, kt, st, 32, ipt_b, 32, two_b, 1, &pb, 2, ksplit) && pb.ct <= 4 &&
           (!have_b || pb.cost < best_b.cost)) {
         best_b = pb;
         have_b = true;
@@ -819,17 +823,17 @@ std::vector<ImgPlan> img_plans(const ConvGeom& g, const tk_conv2d_attrs* a, cons
       }
     }
   }
-  // split-K plans (3x3), after the plain ones so that the plain plans' algo numbers stay put
-  if (kt == 3 && env_int("TK_IMG_SPLIT", 1) && g.N * (int64_t)g.O * hw * 4 * kImgMaxSplit <= ((int64_t)1 << 31))
+  // split-K plans, after the plain ones so that the plain plans' algo numbers stay put
+  if (env_int("TK_IMG_SPLIT", 1) && g.N * (int64_t)g.O * hw * 4 * kImgMaxSplit <= ((int64_t)1 << 31))
     for (int S : {2, 4})
       for (int R : {64, 32}) {
         if (g.O % R || (force_r && R != force_r)) continue;
         const int maxcols = R == 32 ? kImgMaxCols : 256;
-        for (int CC : {64, 32}) {
-          if (g.cin_pad % CC || (force_cc && CC != force_cc)) continue;
+        for (int CC : {128, 64, 32}) {
+          if ((kt == 3 && CC > 64) || g.cin_pad % CC || (force_cc && CC != force_cc)) continue;
           for (int ipt = std::min(maxcols / hw, g.N); ipt >= 1; --ipt)
             for (int two = 0; two < 2; ++two)
-              if (img_split_candidate(g, ga, st, R, ipt, CC, two, S, &c)) out.push_back(c);
+              if (img_split_candidate(g, ga, kt, st, R, ipt, CC, two, S, &c)) out.push_back(c);
         }
       }
   return out;
@@ -861,8 +865,8 @@ int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& 
 }
 
 int64_t conv_img_split_scratch_bytes(const ConvGeom& g) {
-  // the partial records of a 3x3 split-K plan (img_plans lists them only for 3x3 blocks)
-  if (g.KH != 3 || g.KW != 3 || !env_int("TK_IMG_SPLIT", 1)) return 0;
+  // the partial records of a split-K image-tile plan (1x1 and 3x3 blocks)
+  if (g.KH != g.KW || (g.KH != 1 && g.KH != 3) || !env_int("TK_IMG_SPLIT", 1)) return 0;
   const int64_t rec = (int64_t)g.N * g.O * g.OH * g.OW * 4;
   return rec * kImgMaxSplit <= ((int64_t)1 << 31) && g.OH * g.OW <= kImgMaxCols ? rec * kImgMaxSplit : 0;
 }
@@ -914,8 +918,11 @@ int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga
     best.a.part = best.b.part = static_cast<int32_t*>(scratch);
     best.a.part_stride = best.b.part_stride = stride;
     best.a.ksplit = best.b.ksplit = best.ksplit;
-    ImgKernel ka = best.wm == 2 ? img_kernel3<2, 1>(best.ct, best.cc) : img_kernel3<1, 1>(best.ct, best.cc);
-    ImgKernel kb = img_kernel3<1, 2>(best.ct_b, 32);
+    ImgKernel ka = kt == 3 ? (best.wm == 2 ? img_kernel_split<3, 2, 1>(best.ct, best.cc)
+                                           : img_kernel_split<3, 1, 1>(best.ct, best.cc))
+                           : (best.wm == 2 ? img_kernel_split<1, 2, 1>(best.ct, best.cc)
+                                           : img_kernel_split<1, 1, 1>(best.ct, best.cc));
+    ImgKernel kb = img_kernel_split<3, 1, 2>(best.ct_b, 32);
     if (best.wm_b != 1) {
       set_error("conv image-tile split-K: epilogue pass must use 32-row tiles");
       *rc = TK_ERR_INVALID_ARG;

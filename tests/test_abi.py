@@ -194,8 +194,8 @@ def test_conv_block_3x3_stage_widths():
 
 
 def test_conv_block_scratch_holds_split_partials():
-    # a 3x3 block's scratch holds the four partial records its split-K image-tile plans may write
-    # (tk_conv_img.hip MODE 1 / 2); a 1x1 block reserves none of that
+    # a block's scratch holds the four partial records its split-K image-tile plans may write
+    # (tk_conv_img.hip MODE 1 / 2); planes too large for image tiles reserve none of that
     lib = _lib.load()
 
     def scratch(c, h, o, k):
@@ -212,4 +212,5 @@ def test_conv_block_scratch_holds_split_partials():
 
     assert scratch(512, 7, 512, 3) >= 4 * 64 * 512 * 49 * 4
     assert scratch(256, 14, 256, 3) >= 4 * 64 * 256 * 196 * 4
-    assert scratch(1024, 14, 256, 1) < 64 * 256 * 196 * 4
+    assert scratch(1024, 7, 512, 1) >= 4 * 64 * 512 * 49 * 4
+    assert scratch(64, 56, 256, 1) < 64 * 256 * 3136 * 4
