@@ -769,6 +769,7 @@ bool img_split_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, 
         best_b = pb;
         have_b = true;
       }
+  if (!have_b) return false;
   *out = pa;
   // (pa.cost counted rounds of `tiles` workgroups per CU; the pass runs ksplit times as many)
   out->cost = pa.cost * std::ceil(wgs / 256.0) / std::ceil(tiles / 256.0) + best_b.cost + 1000.0;
