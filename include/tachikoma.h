@@ -171,14 +171,21 @@ typedef struct {
                                    Every algo gives bit-identical records; only time differs. */
 } tk_block_attrs;
 
-/* The kernels an MFMA conv block can run on, as tk_block_attrs.algo values: 1 (im2col tiles,
- * always), then 16 + i for each image-tile plan that applies, in the planner's estimated-time
- * order, then 3 and 4 where the persistent im2col kernel applies (planes of more than 64 pixels,
- * pixel count a multiple of 4, UPWARD requantize, no kernel zero point).  Writes at most max_algos entries; returns how many exist (0: not an MFMA conv, the
- * block has a single kernel) or a negative tk_status.  The reference has one CPU kernel per op
- * (its TOPI schedules are chosen at compile time); this is the MI355X find step's search space. */
+/* The kernels an MFMA conv block can run on, as tk_block_attrs.algo values: 5 (dense tiles, for
+ * [B, K] x [U, K]^T heads with a zero weight zero point), 1 (im2col tiles, always), then 16 + i for
+ * each image-tile plan that applies (plain plans, then split-K plans), in the planner's
+ * estimated-time order, then 3 and 4 where the persistent im2col kernel applies (planes of more
+ * than 64 pixels, pixel count a multiple of 4, UPWARD requantize, no kernel zero point).  Writes at
+ * most max_algos entries; returns how many exist (0: not an MFMA conv, the block has a single
+ * kernel) or a negative tk_status.  The reference has one CPU kernel per op (its TOPI schedules are
+ * chosen at compile time); this is the MI355X find step's search space. */
 int tk_conv2d_block_algos(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
                           int32_t* algos, int max_algos);
+/* A one-line description of one of those kernels (tile shape, stage width, ring, split) into buf
+ * (NUL-terminated, truncated to len): for reports of what the find step picked.  TK_ERR_INVALID_ARG
+ * for an algo the block does not list. */
+int tk_conv2d_block_algo_info(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs, int algo,
+                              char* buf, int len);
 
 /* A fused residual join: qnn.add [→ clip].  One kernel writes both records and,
  * optionally, the int8 shadow (tk_conv2d_make_shadow layout) of the last output for the next MFMA conv. */

@@ -333,6 +333,8 @@ SIGNATURES = {
     "tk_module_set_node_algo": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int]),
     "tk_conv2d_block_algos": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_block_attrs), ctypes.POINTER(ctypes.c_int32),
                                              ctypes.c_int]),
+    "tk_conv2d_block_algo_info": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_block_attrs), ctypes.c_int,
+                                                  ctypes.c_char_p, ctypes.c_int]),
     "tk_ndlist_layout": (_I64, [ctypes.POINTER(tk_array_meta), ctypes.c_int, ctypes.POINTER(_I64)]),
     "tk_ndlist_write_headers": (ctypes.c_int, [ctypes.POINTER(tk_array_meta), ctypes.c_int, _VP, _I64]),
     "tk_ndlist_parse": (ctypes.c_int, [_VP, _I64, ctypes.c_int, ctypes.POINTER(tk_array_meta), ctypes.POINTER(_I64),

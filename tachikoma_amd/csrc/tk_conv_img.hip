@@ -24,6 +24,7 @@
 // (python/tvm/topi/math.py:615-640) as the other conv-block kernels; parity: tests/test_gpu_ops.py.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -863,6 +864,23 @@ int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& 
   }
   for (int k = 0; k < (int)order.size() && k < max_algos; ++k) algos[k] = kAlgoImg0 + order[k];
   return (int)plans.size();
+}
+
+int conv_img_describe(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked, int algo,
+                      char* buf, int len) {
+  const std::vector<ImgPlan> plans = img_plans(g, a, ga, have_chunked);
+  const int i = algo - kAlgoImg0;
+  if (i < 0 || i >= (int)plans.size()) return TK_ERR_INVALID_ARG;
+  const ImgPlan& p = plans[i];
+  const ImgArgs& x = p.a;
+  int n = std::snprintf(buf, (size_t)len, "image tiles %dx%d: %d rows x %d image%s (%d columns), %d-channel stages, "
+                        "%d-slot ring, %d workgroup%s per CU, %d epilogue pass%s, %.1f KB LDS",
+                        p.kt, p.kt, 32 * p.wm, x.ipt, x.ipt > 1 ? "s" : "", x.p, p.cc, x.ns, p.occ, p.occ > 1 ? "s" : "",
+                        x.npass, x.npass > 1 ? "es" : "", p.lds / 1024.0);
+  if (p.ksplit > 1 && n >= 0 && n < len)
+    std::snprintf(buf + n, (size_t)(len - n), "; split K %d ways (%d workgroups), then an epilogue pass of %d rows x %d "
+                  "image%s (%d workgroups)", p.ksplit, x.wgs, 32 * p.wm_b, p.b.ipt, p.b.ipt > 1 ? "s" : "", p.b.wgs);
+  return TK_OK;
 }
 
 int64_t conv_img_split_scratch_bytes(const ConvGeom& g) {

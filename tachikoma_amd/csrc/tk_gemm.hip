@@ -15,6 +15,7 @@
 // python/tvm/relay/qnn/op/legalizations.py:195-226 pads with zeros after the shift).
 // The epilogue writes int32 NCHW directly (lanes run along pixels: coalesced).
 #include <algorithm>
+#include <cstdio>
 #include <mutex>
 #include <type_traits>
 #include <climits>
@@ -1945,6 +1946,47 @@ int conv2d_block_impl(const tk_tensor* data, const void* shadow, const tk_tensor
   return conv2d_run(data, shadow, weight, packed, sums, outs[0], attrs ? &attrs->conv : nullptr, patch, &b, s);
 }
 
+// what the image-tile planner reads of a block's launch arguments (see conv2d_run)
+static GemmArgs planner_args(const ConvGeom& g, const tk_tensor* weight, const tk_block_attrs* attrs) {
+  static int32_t marker;
+  GemmArgs ga{};
+  ga.bias_out = &marker;
+  ga.has_add = attrs->has_add;
+  ga.in_pix = (int64_t)g.N * g.H * g.W;
+  ga.zA = attrs->conv.kernel_zero_point - (is_uint(weight, 8) ? 128 : 0);
+  ga.zA_vec = attrs->conv.kernel_zero_points;
+  ga.RB = conv_needs_patch(weight, &attrs->conv) ? &marker : nullptr;
+  return ga;
+}
+
+int conv_img_describe(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked, int algo,
+                      char* buf, int len);
+
+int conv2d_block_algo_info_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs, int algo,
+                                char* buf, int len) {
+  TK_CHECK_ARG(data && weight && attrs && buf && len > 0, "null argument");
+  ConvGeom g;
+  if (conv_geom(data, weight, &attrs->conv, &g) != TK_OK) {
+    set_error("tk_conv2d_block_algo_info: bad shapes");
+    return TK_ERR_SHAPE;
+  }
+  const GemmArgs ga = planner_args(g, weight, attrs);
+  const char* fixed = algo == kAlgoIm2col ? "im2col tiles (64 or 128 rows x 128 or 256 columns, the library's own shape)"
+                      : algo == kAlgoPf2  ? "persistent im2col tiles, 2 workgroups per CU"
+                      : algo == kAlgoPf3  ? "persistent im2col tiles, 1 workgroup per CU (3-slot ring)"
+                      : algo == kAlgoDense ? "dense tiles: 32 units x 64 samples, K split over 8 waves"
+                                           : nullptr;
+  if (fixed) {
+    std::snprintf(buf, (size_t)len, "%s", fixed);
+    return TK_OK;
+  }
+  const int rc = conv_img_describe(g, &attrs->conv, ga,
+                                   g.KH * g.KW == 1 || conv_img_chunked_bytes(g.rows_pad, g.cin_pad, g.KH * g.KW), algo,
+                                   buf, len);
+  if (rc) set_error("tk_conv2d_block_algo_info: algo " + std::to_string(algo) + " is not listed for this block");
+  return rc;
+}
+
 int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
                             int32_t* algos, int max_algos) {
   TK_CHECK_ARG(data && weight && attrs && (algos || max_algos <= 0), "null argument");
@@ -1954,15 +1996,7 @@ int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, cons
     return TK_ERR_SHAPE;
   }
   if (!use_mfma_conv(g, attrs->conv.groups) || !is_int8ish(data) || !is_int8ish(weight)) return 0;
-  // what the image-tile planner reads of the launch arguments (see conv2d_run)
-  static int32_t marker;
-  GemmArgs ga{};
-  ga.bias_out = &marker;
-  ga.has_add = attrs->has_add;
-  ga.in_pix = (int64_t)g.N * g.H * g.W;
-  ga.zA = attrs->conv.kernel_zero_point - (is_uint(weight, 8) ? 128 : 0);
-  ga.zA_vec = attrs->conv.kernel_zero_points;
-  ga.RB = conv_needs_patch(weight, &attrs->conv) ? &marker : nullptr;
+  const GemmArgs ga = planner_args(g, weight, attrs);
   int n = 0;
   // dense blocks (1x1 over [B, K, 1, 1]) with a zero weight zero point: the dense tile kernel first
   if (conv_dense_applies(g, ga)) {

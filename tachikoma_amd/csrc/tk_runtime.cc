@@ -66,6 +66,8 @@ int qnn_concatenate_impl(const tk_tensor* const* xs, int n_in, tk_tensor* y, con
 int transpose_impl(const tk_tensor* x, tk_tensor* y, const tk_transpose_attrs* a, hipStream_t s);
 int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
                             int32_t* algos, int max_algos);
+int conv2d_block_algo_info_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs, int algo,
+                                char* buf, int len);
 
 // run_packed's "nothing to capture, run the plain graph" answer (not an error code)
 constexpr int TK_OK_RUN = 1;
@@ -325,6 +327,10 @@ int tk_qnn_conv2d_block(const tk_tensor* data, const void* shadow, const tk_tens
 int tk_conv2d_block_algos(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
                           int32_t* algos, int max_algos) {
   return tk::conv2d_block_algos_impl(data, weight, attrs, algos, max_algos);
+}
+int tk_conv2d_block_algo_info(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs, int algo,
+                              char* buf, int len) {
+  return tk::conv2d_block_algo_info_impl(data, weight, attrs, algo, buf, len);
 }
 int tk_qnn_dense_block(const tk_tensor* data, const tk_tensor* weight, const tk_tensor* bias, tk_tensor* const* outs,
                        int n_outs, const tk_block_attrs* attrs, void* workspace, void* stream) {

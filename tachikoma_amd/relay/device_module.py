@@ -420,6 +420,7 @@ class DeviceModule:
             emit(n, g.kind, [o.name for o in g.ops])
         torch.cuda.current_stream().synchronize()
         self._node_kind_codes = [int(n.kind) for n in nodes]
+        self._nodes = nodes  # (their tensors and attrs describe a node's kernels: algo_info)
         arr = (_lib.tk_node * max(1, len(nodes)))(*nodes)
         handle = ctypes.c_void_p()
         _lib.check(self.lib.tk_module_create(arr, len(nodes), ctypes.byref(handle)), "tk_module_create")
@@ -723,7 +724,8 @@ class DeviceModule:
             cands = [(int(algos[i * w + 1 + c]), round(float(us[i * w + 1 + c]), 2)) for c in range(max_candidates)
                      if algos[i * w + 1 + c] >= 0]
             out.append({"node": i, "records": list(self.node_records[i]), "algo": int(algos[i * w]),
-                        "us": round(float(us[i * w]), 2), "candidates": cands})
+                        "us": round(float(us[i * w]), 2), "kernel": self.algo_info(i, int(algos[i * w])),
+                        "candidates": cands})
         self.tuning = out
         self.tune_table_digest = tune_table_digest(out)
         return out
@@ -754,10 +756,18 @@ class DeviceModule:
                 raise _lib.TachikomaError(f"tune table has no entry for the conv block writing {recs}")
             _lib.check(self.lib.tk_module_set_node_algo(self.handle, i, int(e["algo"])), "tk_module_set_node_algo")
             applied.append({"node": i, "records": list(recs), "algo": int(e["algo"]), "us": e.get("us"),
-                            "candidates": []})
+                            "kernel": self.algo_info(i, int(e["algo"])), "candidates": []})
         self.tuning = applied
         self.tune_table_digest = tune_table_digest(applied)
         return applied
+
+    def algo_info(self, node: int, algo: int) -> str:
+        """tk_conv2d_block_algo_info: what kernel `algo` is on conv-block node `node`."""
+        n = self._nodes[node]
+        buf = ctypes.create_string_buffer(256)
+        rc = self.lib.tk_conv2d_block_algo_info(n.inputs[0], n.inputs[1], ctypes.byref(n.attrs.block), int(algo), buf,
+                                               len(buf))
+        return buf.value.decode() if rc == 0 else f"algo {algo} (not listed)"
 
     def _node_kind(self, i: int) -> int:
         return self._node_kind_codes[i]

@@ -214,3 +214,30 @@ def test_conv_block_scratch_holds_split_partials():
     assert scratch(256, 14, 256, 3) >= 4 * 64 * 256 * 196 * 4
     assert scratch(1024, 7, 512, 1) >= 4 * 64 * 512 * 49 * 4
     assert scratch(64, 56, 256, 1) < 64 * 256 * 3136 * 4
+
+
+def test_conv_block_algo_info():
+    # every listed kernel has a description (the find step's report names its picks); unlisted fail
+    lib = _lib.load()
+    keep = []
+    x = _host_tensor((64, 512, 7, 7), 0, 8, keep)
+    w = _host_tensor((512, 512, 3, 3), 0, 8, keep)
+    a = _lib.tk_block_attrs()
+    a.conv.strides[:] = [1, 1]
+    a.conv.padding[:] = [1, 1, 1, 1]
+    a.conv.dilation[:] = [1, 1]
+    a.conv.groups = 1
+    a.requantize.mode = _lib.TK_RQ_AXIS_UPWARD
+    a.requantize.axis = 1
+    buf = (ctypes.c_int32 * 512)()
+    cnt = lib.tk_conv2d_block_algos(ctypes.byref(x), ctypes.byref(w), ctypes.byref(a), buf, 512)
+    descs = []
+    for algo in list(buf)[:cnt]:
+        s = ctypes.create_string_buffer(256)
+        assert lib.tk_conv2d_block_algo_info(ctypes.byref(x), ctypes.byref(w), ctypes.byref(a), algo, s, 256) == 0
+        descs.append(s.value.decode())
+    assert descs[0].startswith("im2col")
+    assert any(d.startswith("image tiles 3x3") and "split K" in d for d in descs), descs[:20]
+    assert any(d.startswith("image tiles 3x3") and "split K" not in d for d in descs)
+    s = ctypes.create_string_buffer(256)
+    assert lib.tk_conv2d_block_algo_info(ctypes.byref(x), ctypes.byref(w), ctypes.byref(a), 16 + cnt + 5, s, 256) < 0
