@@ -279,6 +279,8 @@ int conv_pf_run(const ConvGeom& g, GemmArgs ga, int ring, hipStream_t s);
 // ---------------------------------------------------------------- small-batch dense blocks
 // (tk_dense.hip) [B, K] x [U, K]^T on 32 x 32 tiles with K split over the four waves, one launch.
 bool conv_dense_applies(const ConvGeom& g, const GemmArgs& ga);
-int conv_dense_run(const ConvGeom& g, const GemmArgs& ga, hipStream_t s);
+// scratch: conv_dense_scratch_bytes(g) bytes for a K-sliced run (NULL: one launch, no slices)
+int conv_dense_run(const ConvGeom& g, const GemmArgs& ga, void* scratch, hipStream_t s);
+int64_t conv_dense_scratch_bytes(const ConvGeom& g);
 
 }  // namespace tk

@@ -2,16 +2,17 @@
 // qnn.requantize [-> clip] of [B, K] x [U, K]^T with B <= a few hundred (the classifier heads;
 // dense blocks run as 1x1 conv blocks over [B, K, 1, 1], device_module._dense_as_conv).
 //
-// The im2col conv tiles (64 rows x 128 columns) leave such a layer 16 tiles for 256 CUs and need
-// split-K with a second reduce launch: ResNet-50's 2048 -> 1000 classifier took 23.7 us for 2 MB of
-// weights (profiles/r03fin3_layers_rocprof.txt).  Here one launch covers it: a workgroup owns a
-// 32-unit x 64-sample tile, its eight waves split K eight ways and stream their A (packed weight)
-// and B (input shadow) fragments straight from global memory into registers -- all of a wave's
-// loads in one batch for ResNet-50's K = 2048, so the launch costs about one memory round trip --
-// (every byte feeds MFMAs directly, LDS staging buys nothing), the partial tiles meet in LDS and the
-// workgroup writes every record of the block from there: 32 tiles for ResNet-50's head.  (Four
-// waves over two 32-sample tiles each measured 9.0 us in the network, profiles/r04j_layers_rocprof.txt.)
-// Bound: the weight bytes (HBM) and the per-CU load rate; v_mfma_i32_32x32x32_i8.
+// The im2col conv tiles (64 rows x 128 columns) leave such a layer 16 tiles for 256 CUs: round 3's
+// split-K im2col run took ResNet-50's 2048 -> 1000 classifier 23.7 us for 2 MB of weights
+// (profiles/r03fin3_layers_rocprof.txt).  Here a workgroup owns a 32-unit x 64-sample tile (one
+// weight fragment feeds two MFMAs) over a slice of K; its four waves split the slice and stream
+// their A (packed weight) and B (input shadow) fragments straight from global memory into
+// registers (every byte feeds MFMAs directly, LDS staging buys nothing) and their partial tiles
+// meet in LDS.  With one slice (small grids of long K excepted) the workgroup writes every record
+// of the block from there; ResNet-50's head has 32 tiles, so K is cut into 8 slices (256
+// workgroups, the per-CU load rate of 32 CUs was the bound: 9.0 us with 64 workgroups, 10.3 with
+// 32, profiles/r04j_layers_rocprof.txt, r04l) whose raw sums go to scratch, and a second, elementwise
+// launch sums them and runs the epilogue.  v_mfma_i32_32x32x32_i8.
 #include <algorithm>
 
 #include "tk_conv.h"
@@ -20,88 +21,18 @@ namespace tk {
 
 namespace {
 
-constexpr int kDenseSteps = 8;   // K = 32 steps whose fragments are loaded before their MFMAs
-constexpr int kDenseWaves = 8;   // K split eight ways inside the workgroup: every wave's loads in one batch
+constexpr int kDenseSteps = 8;     // K = 32 steps whose fragments are loaded before their MFMAs
+constexpr int kDenseMaxSlices = 8; // K slices of a split run (its scratch: slices x [B, U] int32)
 
-// A workgroup owns 32 units x CTD * 32 samples; wave w reduces K steps [w * per, (w + 1) * per)
-// for all of its CTD column tiles (one weight fragment feeds CTD MFMAs).
-template <int CTD>
-__global__ __launch_bounds__(64 * kDenseWaves) void dense_tile_kernel(GemmArgs g, int32_t ksteps) {
-  __shared__ int32_t part[4][32][CTD * 32 + 1];  // [wave pair][unit row][sample col], +1 against conflicts
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r0 = blockIdx.x * 32, c0 = blockIdx.y * (CTD * 32);
-  const int rl = lane & 31, h = lane >> 5;
-  const int per = (ksteps + kDenseWaves - 1) / kDenseWaves;
-  const int s0 = wave * per, s1 = min(ksteps, s0 + per);
-  const int8_t* arow = g.A + (int64_t)(r0 + rl) * g.lda + 16 * h;  // packed rows exist up to rows_pad
-  const int8_t* bcol[CTD];
-  bool col_ok[CTD];
-#pragma unroll
-  for (int j = 0; j < CTD; ++j) {
-    const int col = c0 + j * 32 + rl;
-    col_ok[j] = col < g.N;
-    bcol[j] = g.B + (int64_t)(col_ok[j] ? col : 0) * 16 + (int64_t)h * g.in_pix * 16;
-  }
-  const int64_t bstep = 2 * g.in_pix * 16;  // two 16-channel groups per K step
-  v16i acc[CTD];
-#pragma unroll
-  for (int j = 0; j < CTD; ++j) acc[j] = v16i{0};
-  for (int s = s0; s < s1; s += kDenseSteps) {
-    v4i a[kDenseSteps], b[kDenseSteps][CTD];
-#pragma unroll
-    for (int k = 0; k < kDenseSteps; ++k) {
-      if (s + k < s1) {
-        a[k] = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(arow + (int64_t)(s + k) * 32));
-#pragma unroll
-        for (int j = 0; j < CTD; ++j)
-          b[k][j] = col_ok[j] ? ldg(reinterpret_cast<const v4i*>(bcol[j] + (int64_t)(s + k) * bstep)) : v4i{0, 0, 0, 0};
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kDenseSteps; ++k)
-      if (s + k < s1) {
-#pragma unroll
-        for (int j = 0; j < CTD; ++j) acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[k], b[k][j], acc[j], 0, 0, 0);
-      }
-  }
-  // the eight partial tiles meet in LDS: waves 4..7 store, waves 0..3 add theirs and store the pair
-  // sums, then every thread sums the four pairs of its outputs.  C/D layout: register q holds row
-  // (q & 3) + 8 * (q >> 2) + 4 * h, column rl of the wave's tile j.
-  const int pw = wave & 3;
-  if (wave >= 4) {
-#pragma unroll
-    for (int j = 0; j < CTD; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) part[pw][(q & 3) + 8 * (q >> 2) + 4 * h][j * 32 + rl] = acc[j][q];
-  }
-  __syncthreads();
-  if (wave < 4) {
-#pragma unroll
-    for (int j = 0; j < CTD; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        int32_t& slot = part[pw][(q & 3) + 8 * (q >> 2) + 4 * h][j * 32 + rl];
-        slot = (int32_t)((uint32_t)slot + (uint32_t)acc[j][q]);
-      }
-  }
-  __syncthreads();
-  // epilogue: thread t owns sample c0 + t / 8 and units r0 + 4 (t % 8) .. + 3 (consecutive in the
-  // [B, U] records: 16-byte int32 stores)
-  const int t = threadIdx.x;
-  const int j = t >> 3, i0 = (t & 7) * 4;
-  const int b = c0 + j;
-  if (j >= CTD * 32 || b >= g.N) return;
-  int32_t v[4];
+// zero-point fold, bias_add, requantize, clip and the next layer's shadow of sample b, units
+// u0 .. u0 + 3 (v: the contraction sums)
+__device__ __forceinline__ void dense_epilogue(const GemmArgs& g, int b, int u0, int32_t* v) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const int i = i0 + e;
-    uint32_t x = (uint32_t)part[0][i][j] + (uint32_t)part[1][i][j] + (uint32_t)part[2][i][j] + (uint32_t)part[3][i][j];
     // zero-point folding with zA = 0 (the weight side): out = acc - zB * RA[unit]
-    const int u = min(r0 + i, g.M - 1);
-    x -= (uint32_t)g.zB * (uint32_t)g.RA[u];
-    v[e] = (int32_t)x;
+    const int u = min(u0 + e, g.M - 1);
+    v[e] = (int32_t)((uint32_t)v[e] - (uint32_t)g.zB * (uint32_t)g.RA[u]);
   }
-  const int u0 = r0 + i0;
   const int64_t off = (int64_t)b * g.M + u0;
   const bool full = u0 + 3 < g.M && (off & 3) == 0;
   auto put32 = [&](int32_t* dst, const int32_t* w) {
@@ -142,6 +73,99 @@ __global__ __launch_bounds__(64 * kDenseWaves) void dense_tile_kernel(GemmArgs g
   }
 }
 
+// grid (unit tiles, sample tiles, K slices); slice z = K steps [z * kper, (z + 1) * kper); wave w
+// of the workgroup takes a quarter of the slice.  SPLIT: raw sums to part[z][B][U]; else the
+// block epilogue.
+template <int CTD, bool SPLIT>
+__global__ __launch_bounds__(256) void dense_tile_kernel(GemmArgs g, int32_t ksteps, int32_t kper, int32_t* part) {
+  __shared__ int32_t red[4][32][CTD * 32 + 1];  // [wave][unit row][sample col], +1 against conflicts
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * 32, c0 = blockIdx.y * (CTD * 32);
+  const int rl = lane & 31, h = lane >> 5;
+  const int z0 = blockIdx.z * kper, z1 = min(ksteps, z0 + kper);
+  const int per = (z1 - z0 + 3) / 4;
+  const int s0 = z0 + wave * per, s1 = min(z1, s0 + per);
+  const int8_t* arow = g.A + (int64_t)(r0 + rl) * g.lda + 16 * h;  // packed rows exist up to rows_pad
+  const int8_t* bcol[CTD];
+  bool col_ok[CTD];
+#pragma unroll
+  for (int j = 0; j < CTD; ++j) {
+    const int col = c0 + j * 32 + rl;
+    col_ok[j] = col < g.N;
+    bcol[j] = g.B + (int64_t)(col_ok[j] ? col : 0) * 16 + (int64_t)h * g.in_pix * 16;
+  }
+  const int64_t bstep = 2 * g.in_pix * 16;  // two 16-channel groups per K step
+  v16i acc[CTD];
+#pragma unroll
+  for (int j = 0; j < CTD; ++j) acc[j] = v16i{0};
+  for (int s = s0; s < s1; s += kDenseSteps) {
+    v4i a[kDenseSteps], b[kDenseSteps][CTD];
+#pragma unroll
+    for (int k = 0; k < kDenseSteps; ++k) {
+      if (s + k < s1) {
+        a[k] = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(arow + (int64_t)(s + k) * 32));
+#pragma unroll
+        for (int j = 0; j < CTD; ++j)
+          b[k][j] = col_ok[j] ? ldg(reinterpret_cast<const v4i*>(bcol[j] + (int64_t)(s + k) * bstep)) : v4i{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kDenseSteps; ++k)
+      if (s + k < s1) {
+#pragma unroll
+        for (int j = 0; j < CTD; ++j) acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[k], b[k][j], acc[j], 0, 0, 0);
+      }
+  }
+  // C/D layout: register q holds row (q & 3) + 8 * (q >> 2) + 4 * h, column rl of the tile j
+#pragma unroll
+  for (int j = 0; j < CTD; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) red[wave][(q & 3) + 8 * (q >> 2) + 4 * h][j * 32 + rl] = acc[j][q];
+  __syncthreads();
+  // thread t (of 256) owns samples c0 + t / 8 (+ 32 for CTD = 2) and units r0 + 4 (t % 8) .. + 3
+  // (consecutive in the [B, U] records: 16-byte int32 stores)
+  const int t = threadIdx.x;
+  const int i0 = (t & 7) * 4, u0 = r0 + i0;
+#pragma unroll
+  for (int jj = 0; jj < CTD; ++jj) {
+    const int jc = (t >> 3) + 32 * jj, b = c0 + jc;
+    if (b >= g.N) continue;
+    int32_t v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      v[e] = (int32_t)((uint32_t)red[0][i0 + e][jc] + (uint32_t)red[1][i0 + e][jc] + (uint32_t)red[2][i0 + e][jc] +
+                       (uint32_t)red[3][i0 + e][jc]);
+    if constexpr (SPLIT) {
+      int32_t* dst = part + ((int64_t)blockIdx.z * g.N + b) * g.M + u0;
+      if (u0 + 3 < g.M && ((((int64_t)blockIdx.z * g.N + b) * g.M + u0) & 3) == 0) {
+        *reinterpret_cast<v4i*>(dst) = v4i{v[0], v[1], v[2], v[3]};
+      } else {
+        for (int e = 0; e < 4; ++e)
+          if (u0 + e < g.M) dst[e] = v[e];
+      }
+    } else {
+      dense_epilogue(g, b, u0, v);
+    }
+  }
+}
+
+// the split run's second launch: thread per (sample, 4 units), the slices' sums + the epilogue
+__global__ __launch_bounds__(256) void dense_slices_epilogue_kernel(GemmArgs g, int32_t slices, const int32_t* part) {
+  const int64_t groups = (int64_t)g.N * ((g.M + 3) / 4);
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= groups) return;
+  const int per_row = (g.M + 3) / 4;
+  const int b = (int)(i / per_row), u0 = (int)(i - (int64_t)b * per_row) * 4;
+  int32_t v[4] = {0, 0, 0, 0};
+  for (int z = 0; z < slices; ++z) {
+    const int32_t* src = part + ((int64_t)z * g.N + b) * g.M + u0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (u0 + e < g.M) v[e] = (int32_t)((uint32_t)v[e] + (uint32_t)src[e]);
+  }
+  dense_epilogue(g, b, u0, v);
+}
+
 }  // namespace
 
 bool conv_dense_applies(const ConvGeom& g, const GemmArgs& ga) {
@@ -150,18 +174,38 @@ bool conv_dense_applies(const ConvGeom& g, const GemmArgs& ga) {
          !ga.RB && !ga.has_add && g.cin_pad % 32 == 0 && g.N <= 1024;
 }
 
-int conv_dense_run(const ConvGeom& g, const GemmArgs& ga, hipStream_t s) {
+int64_t conv_dense_scratch_bytes(const ConvGeom& g) {
+  // a split run's K-slice sums (dense geometry only; conv_dense_applies checks the rest)
+  return g.H == 1 && g.W == 1 && g.KH == 1 && g.KW == 1 && g.cin_pad % 32 == 0 && g.N <= 1024
+             ? (int64_t)kDenseMaxSlices * g.N * g.O * 4 : 0;
+}
+
+int conv_dense_run(const ConvGeom& g, const GemmArgs& ga, void* scratch, hipStream_t s) {
   TK_CHECK_ARG(conv_dense_applies(g, ga), "dense tile kernel: not a [B, K] x [U, K]^T block with zero weight zero point");
   TK_CHECK_ARG(ga.RA || ga.zB == 0, "dense tile kernel: weight sums needed for the input zero point");
   TK_CHECK_ARG(ga.k_pad <= ga.lda && (int64_t)(g.O + 31) / 32 * 32 <= g.rows_pad, "dense tile kernel: packed weight rows");
-  // two 32-sample column tiles per workgroup (one weight fragment per two MFMAs) unless the batch
-  // fits one
-  if (g.N > 32) {
-    const dim3 grid((unsigned)((g.O + 31) / 32), (unsigned)((g.N + 63) / 64));
-    hipLaunchKernelGGL(dense_tile_kernel<2>, grid, dim3(64 * kDenseWaves), 0, s, ga, (int32_t)(g.cin_pad / 32));
+  const int ksteps = g.cin_pad / 32;
+  const int ctd = g.N > 32 ? 2 : 1;
+  const unsigned ut = (unsigned)((g.O + 31) / 32), st = (unsigned)((g.N + 32 * ctd - 1) / (32 * ctd));
+  // K slices: enough workgroups for the chip, >= 8 K steps (2 per wave) per slice
+  int slices = scratch ? (int)std::min<int64_t>({(int64_t)kDenseMaxSlices, std::max<int64_t>(1, 256 / ((int64_t)ut * st)),
+                                                 std::max(1, ksteps / 8)})
+                       : 1;
+  const int kper = (ksteps + slices - 1) / slices;
+  slices = (ksteps + kper - 1) / kper;
+  int32_t* part = static_cast<int32_t*>(scratch);
+  const dim3 grid(ut, st, (unsigned)slices);
+  if (slices > 1) {
+    if (ctd == 2) hipLaunchKernelGGL((dense_tile_kernel<2, true>), grid, dim3(256), 0, s, ga, ksteps, kper, part);
+    else hipLaunchKernelGGL((dense_tile_kernel<1, true>), grid, dim3(256), 0, s, ga, ksteps, kper, part);
+    TK_LAUNCH_CHECK();
+    const int64_t groups = (int64_t)g.N * ((g.O + 3) / 4);
+    hipLaunchKernelGGL(dense_slices_epilogue_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, ga, slices,
+                       (const int32_t*)part);
+  } else if (ctd == 2) {
+    hipLaunchKernelGGL((dense_tile_kernel<2, false>), grid, dim3(256), 0, s, ga, ksteps, kper, part);
   } else {
-    const dim3 grid((unsigned)((g.O + 31) / 32), 1u);
-    hipLaunchKernelGGL(dense_tile_kernel<1>, grid, dim3(64 * kDenseWaves), 0, s, ga, (int32_t)(g.cin_pad / 32));
+    hipLaunchKernelGGL((dense_tile_kernel<1, false>), grid, dim3(256), 0, s, ga, ksteps, kper, part);
   }
   TK_LAUNCH_CHECK();
   return TK_OK;

@@ -1699,7 +1699,10 @@ int64_t conv_scratch_bytes(const tk_tensor* data, const tk_tensor* weight, const
   const SplitPlan sp = conv_split_plan(g, mt1, ipt, wide ? 2 * kBK : kBK);
   int64_t split = sp.splits > 1 ? al256(sp.tiles * sp.splits * (int64_t)(2 * 16 * kGemmThreads) * 4) : 0;
   // a conv block's split-K image-tile plans (3x3) use the same space for their partial records
-  if (block && !conv_needs_patch(weight, a)) split = std::max(split, al256(conv_img_split_scratch_bytes(g)));
+  if (block && !conv_needs_patch(weight, a)) {
+    split = std::max(split, al256(conv_img_split_scratch_bytes(g)));
+    split = std::max(split, al256(conv_dense_scratch_bytes(g)));  // the dense head's K-slice sums
+  }
   return bytes + split;
 }
 
@@ -1856,7 +1859,7 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
       set_error("tk_qnn_conv2d_block: algo 5 (dense tiles) does not apply to this block; see tk_conv2d_block_algos");
       return TK_ERR_INVALID_ARG;
     }
-    return conv_dense_run(g, ga, s);
+    return conv_dense_run(g, ga, sc, s);
   }
   if (blk) {
     // whole-image tiles with the patch staged per channel stage (tk_conv_img.hip) where they apply

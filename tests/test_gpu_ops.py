@@ -429,6 +429,10 @@ ALGO_CASES = [
     # and a stride-2 3x3 on an odd input width (no column-parity patch), uint8 with a residual join
     (4, 160, 7, 64, 3, 1, "int8", -3, None, (0, 127)),
     (2, 64, 13, 64, 3, 2, "uint8", 131, (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
+    # dense heads as 1x1 blocks over [B, K, 1, 1] (the dense tile kernel, algo 5): ResNet-50's
+    # 2048 -> 1000 over 8 K slices, and a ragged 40-sample uint8 batch
+    (64, 2048, 1, 1000, 1, 1, "int8", -3, None, (0, 127)),
+    (40, 512, 1, 96, 1, 1, "uint8", 131, None, None),
 ]
 
 
