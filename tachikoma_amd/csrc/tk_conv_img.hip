@@ -756,6 +756,7 @@ bool img_split_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, 
                          int ksplit, ImgPlan* out) {
   ImgPlan pa{}, pb{}, best_b{};
   if (!img_candidate(g, ga, kt, st, R, ipt, CC, two, 1, &pa, 1, ksplit)) return false;
+  if (pa.ct > 4) return false;  // (the split kernels are instantiated for 2 and 4 column tiles per wave)
   const int tiles = pa.a.wgs, wgs = tiles * ksplit;
   if (tiles > 256 || wgs > 2048) return false;  // the plain plans already fill the chip
   pa.a.wgs = wgs;
