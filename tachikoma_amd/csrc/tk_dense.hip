@@ -150,11 +150,12 @@ __global__ __launch_bounds__(256) void dense_tile_kernel(GemmArgs g, int32_t kst
 }
 
 // the split run's second launch: thread per (sample, 4 units), the slices' sums + the epilogue
+// (units up to the shadow's padded channel count, whose shadow bytes are written as 0)
 __global__ __launch_bounds__(256) void dense_slices_epilogue_kernel(GemmArgs g, int32_t slices, const int32_t* part) {
-  const int64_t groups = (int64_t)g.N * ((g.M + 3) / 4);
+  const int per_row = (max(g.M, g.shadow_out ? (int)g.shadow_cpad : 0) + 3) / 4;
+  const int64_t groups = (int64_t)g.N * per_row;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= groups) return;
-  const int per_row = (g.M + 3) / 4;
   const int b = (int)(i / per_row), u0 = (int)(i - (int64_t)b * per_row) * 4;
   int32_t v[4] = {0, 0, 0, 0};
   for (int z = 0; z < slices; ++z) {
@@ -199,7 +200,7 @@ int conv_dense_run(const ConvGeom& g, const GemmArgs& ga, void* scratch, hipStre
     if (ctd == 2) hipLaunchKernelGGL((dense_tile_kernel<2, true>), grid, dim3(256), 0, s, ga, ksteps, kper, part);
     else hipLaunchKernelGGL((dense_tile_kernel<1, true>), grid, dim3(256), 0, s, ga, ksteps, kper, part);
     TK_LAUNCH_CHECK();
-    const int64_t groups = (int64_t)g.N * ((g.O + 3) / 4);
+    const int64_t groups = (int64_t)g.N * ((std::max(g.O, ga.shadow_out ? (int)ga.shadow_cpad : 0) + 3) / 4);
     hipLaunchKernelGGL(dense_slices_epilogue_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, ga, slices,
                        (const int32_t*)part);
   } else if (ctd == 2) {
