@@ -23,9 +23,13 @@
 // (src/relay/qnn/op/requantize.cc:195-273), qnn.add (src/relay/qnn/op/add.cc:40-96) and clip
 // (python/tvm/topi/math.py:615-640) as the other conv-block kernels; parity: tests/test_gpu_ops.py.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -787,9 +791,43 @@ bool img_split_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, 
 
 namespace {
 
+std::vector<ImgPlan> img_plans_build(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga,
+                                     bool have_chunked);
+
 // Every image-tile plan that applies to the conv block, in enumeration order (R, stage width,
-// images per tile, one or two workgroups per CU); empty when the kernel does not apply.
-std::vector<ImgPlan> img_plans(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked) {
+// images per tile, one or two workgroups per CU, then the split-K plans); empty when the kernel
+// does not apply.  Memoised per block shape: a 7x7 block enumerates ~1,000 candidates (split
+// plans each search an epilogue tiling), and the launch path plans on every call, so without the
+// cache each launch spent ~15-20 us of host time before its kernel -- idle GPU time inside the
+// find step's event-timed launches, which made every image plan of those blocks look 2x slower.
+using ImgPlans = std::shared_ptr<const std::vector<ImgPlan>>;
+
+ImgPlans img_plans(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked) {
+#ifdef TK_ABLATION_BUILD
+  // (plans follow TK_IMG_* variables set between calls)
+  return std::make_shared<const std::vector<ImgPlan>>(img_plans_build(g, a, ga, have_chunked));
+#endif
+  const std::array<int64_t, 27> key = {g.N, g.C, g.H, g.W, g.O, g.KH, g.KW, g.OH, g.OW, g.cin_pad, g.k_pad,
+                                       g.rows_pad, a->strides[0], a->strides[1], a->padding[0], a->padding[1],
+                                       a->padding[2], a->padding[3], a->dilation[0], a->dilation[1],
+                                       ga.bias_out != nullptr, ga.RB != nullptr, ga.zA_vec != nullptr, ga.zA,
+                                       ga.has_add, ga.in_pix, have_chunked};
+  static std::mutex mu;
+  static std::map<std::array<int64_t, 27>, ImgPlans> cache;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  ImgPlans plans = std::make_shared<const std::vector<ImgPlan>>(img_plans_build(g, a, ga, have_chunked));
+  std::lock_guard<std::mutex> lock(mu);
+  if (cache.size() > 4096) cache.clear();
+  cache.emplace(key, plans);
+  return plans;
+}
+
+std::vector<ImgPlan> img_plans_build(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga,
+                                     bool have_chunked) {
   std::vector<ImgPlan> out;
   if (!env_int("TK_IMG", 1) || !ga.bias_out) return out;  // conv blocks only
   if (ga.RB || ga.zA_vec || ga.zA != 0) return out;       // the weights' zero point must be 0
@@ -846,7 +884,8 @@ std::vector<ImgPlan> img_plans(const ConvGeom& g, const tk_conv2d_attrs* a, cons
 
 int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked,
                    int32_t* algos, int max_algos) {
-  const std::vector<ImgPlan> plans = img_plans(g, a, ga, have_chunked);
+  const ImgPlans pp = img_plans(g, a, ga, have_chunked);
+  const std::vector<ImgPlan>& plans = *pp;
   std::vector<int> order(plans.size());
   for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return plans[x].cost < plans[y].cost; });
@@ -869,7 +908,8 @@ int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& 
 
 int conv_img_describe(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked, int algo,
                       char* buf, int len) {
-  const std::vector<ImgPlan> plans = img_plans(g, a, ga, have_chunked);
+  const ImgPlans pp = img_plans(g, a, ga, have_chunked);
+  const std::vector<ImgPlan>& plans = *pp;
   const int i = algo - kAlgoImg0;
   if (i < 0 || i >= (int)plans.size()) return TK_ERR_INVALID_ARG;
   const ImgPlan& p = plans[i];
@@ -908,7 +948,8 @@ static int set_lds(ImgKernel kern, size_t lds, int* rc) {
 int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked, void* scratch,
                  int algo, hipStream_t s, int* rc) {
   if (algo == kAlgoIm2col || algo == kAlgoPf2 || algo == kAlgoPf3) return 0;
-  const std::vector<ImgPlan> plans = img_plans(g, a, ga, chunked != nullptr);
+  const ImgPlans pp = img_plans(g, a, ga, chunked != nullptr);
+  const std::vector<ImgPlan>& plans = *pp;
   if (plans.empty() && algo == 0) return 0;
   if (plans.empty() || (algo >= kAlgoImg0 && algo - kAlgoImg0 >= (int)plans.size()) ||
       (algo != 0 && algo != kAlgoImg && algo < kAlgoImg0)) {
