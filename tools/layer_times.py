@@ -17,7 +17,8 @@ def main(path, model="resnet50", batch=64):
     plan = lower(m.mod, m.params)
     groups = exec_groups(plan)
     blocks = [g for g in groups if g.kind in ("conv_block", "dense_block")]
-    fams = ("gemm_i8_kernel", "direct_conv_kernel", "conv_img_kernel", "conv_pf_kernel", "dense_tile_kernel")
+    fams = ("gemm_i8_kernel", "direct_conv_kernel", "conv_img_kernel", "conv_pf_kernel", "dense_tile_kernel",
+            "dense_slices_epilogue_kernel")
     g_rows = [r for r in rows if any(f in r["Kernel_Name"] for f in fams)]
     # idle time before each launch: end of the previous kernel (any) to this start
     prev_end = {}
@@ -51,7 +52,8 @@ def main(path, model="resnet50", batch=64):
             # split-K partial passes (im2col tiles' partials, image tiles' partial records): their
             # time goes to the block's second launch (the reduce / epilogue pass)
             if L > n and ("true, false, 1," in r["Kernel_Name"] or re.search(r"conv_img_kernel<\d+, \d+, \d+, \d+, 1>",
-                                                                             r["Kernel_Name"])):
+                                                                             r["Kernel_Name"])
+                          or re.search(r"dense_tile_kernel<\d+, true>", r["Kernel_Name"])):
                 pending += d
                 continue
             dur[i].append(d + pending)

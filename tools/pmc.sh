@@ -15,7 +15,7 @@ i=0
 for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
              "SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $group --kernel-include-regex "gemm_i8_kernel|conv_img_kernel|conv_pf_kernel|dense_tile_kernel" --output-format csv \
+  timeout -k 10 300 rocprofv3 --pmc $group --kernel-include-regex "gemm_i8_kernel|conv_img_kernel|conv_pf_kernel|dense_tile_kernel|dense_slices_epilogue_kernel" --output-format csv \
       -d "$OUT/pass$i" -o run -- python3 bench.py --steps 2 --warmup 1 --skip-cpu --no-trace "$@" \
       > "$OUT/pass$i.log" 2>&1 || { echo "pass $i ($group) failed"; tail -5 "$OUT/pass$i.log"; exit 1; }
 done

@@ -20,7 +20,8 @@ from collections import defaultdict
 def main(d, runs=18):
     path = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    fams = ("gemm_i8_kernel", "conv_img_kernel", "direct_conv_kernel", "conv_pf_kernel", "dense_tile_kernel")
+    fams = ("gemm_i8_kernel", "conv_img_kernel", "direct_conv_kernel", "conv_pf_kernel", "dense_tile_kernel",
+            "dense_slices_epilogue_kernel")
     gemm = [r for r in rows if any(f in r["Kernel_Name"] for f in fams)]
     # launches per step = the period of the kernel-name sequence (the module's find step launches
     # candidate kernels first: drop everything before the first whole period from the end)
