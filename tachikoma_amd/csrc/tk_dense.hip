@@ -44,8 +44,13 @@ __device__ __forceinline__ void dense_epilogue(const GemmArgs& g, int b, int u0,
     }
   };
   auto put8 = [&](uint8_t* dst, const int32_t* w) {
-    for (int e = 0; e < 4; ++e)
-      if (u0 + e < g.M) dst[off + e] = (uint8_t)w[e];
+    if (full) {  // (4-aligned in a [B, U] record: one dword)
+      *reinterpret_cast<uint32_t*>(dst + off) = ((uint32_t)w[0] & 0xFFu) | (((uint32_t)w[1] & 0xFFu) << 8) |
+                                                (((uint32_t)w[2] & 0xFFu) << 16) | ((uint32_t)w[3] << 24);
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (u0 + e < g.M) dst[off + e] = (uint8_t)w[e];
+    }
   };
   put32(g.C, v);
   if (!g.bias_out) return;  // a plain contraction (no block)
@@ -64,12 +69,14 @@ __device__ __forceinline__ void dense_epilogue(const GemmArgs& g, int b, int u0,
     put8(g.clip_out, v);
   }
   if (g.shadow_out) {
-    // the next MFMA layer's shadow [units / 16][B][16] (padded units of the last group as 0)
-    for (int e = 0; e < 4; ++e) {
-      const int u = u0 + e;
-      if (u < g.M) g.shadow_out[((int64_t)(u >> 4) * g.N + b) * 16 + (u & 15)] = (uint8_t)((uint32_t)v[e] ^ g.shadow_xor);
-      else if (u < g.shadow_cpad) g.shadow_out[((int64_t)(u >> 4) * g.N + b) * 16 + (u & 15)] = 0;
-    }
+    // the next MFMA layer's shadow [units / 16][B][16] (padded units of the last group as 0): the
+    // 4 units (u0 % 4 == 0) are 4 bytes of one 16-byte chunk, one dword store
+    uint32_t word = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (u0 + e < g.M) word |= (((uint32_t)v[e] ^ g.shadow_xor) & 0xFFu) << (8 * e);
+    if (u0 < g.shadow_cpad)
+      *reinterpret_cast<uint32_t*>(g.shadow_out + ((int64_t)(u0 >> 4) * g.N + b) * 16 + (u0 & 15)) = word;
   }
 }
 
@@ -150,21 +157,36 @@ __global__ __launch_bounds__(256) void dense_tile_kernel(GemmArgs g, int32_t kst
 }
 
 // the split run's second launch: thread per (sample, 4 units), the slices' sums + the epilogue
-// (units up to the shadow's padded channel count, whose shadow bytes are written as 0)
-__global__ __launch_bounds__(256) void dense_slices_epilogue_kernel(GemmArgs g, int32_t slices, const int32_t* part) {
+// (units up to the shadow's padded channel count, whose shadow bytes are written as 0; 64-thread
+// blocks so that the ~16k threads of a classifier head spread over the CUs, every slice's sums
+// loaded in one batch of 16-byte loads)
+__global__ __launch_bounds__(64) void dense_slices_epilogue_kernel(GemmArgs g, int32_t slices, const int32_t* part) {
   const int per_row = (max(g.M, g.shadow_out ? (int)g.shadow_cpad : 0) + 3) / 4;
   const int64_t groups = (int64_t)g.N * per_row;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= groups) return;
   const int b = (int)(i / per_row), u0 = (int)(i - (int64_t)b * per_row) * 4;
-  int32_t v[4] = {0, 0, 0, 0};
-  for (int z = 0; z < slices; ++z) {
-    const int32_t* src = part + ((int64_t)z * g.N + b) * g.M + u0;
+  uint32_t v[4] = {0, 0, 0, 0};
+  if (g.M % 4 == 0 && u0 < g.M) {
+    v4i s[kDenseMaxSlices];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (u0 + e < g.M) v[e] = (int32_t)((uint32_t)v[e] + (uint32_t)src[e]);
+    for (int z = 0; z < kDenseMaxSlices; ++z)
+      if (z < slices) s[z] = ldg(reinterpret_cast<const v4i*>(part + ((int64_t)z * g.N + b) * g.M + u0));
+#pragma unroll
+    for (int z = 0; z < kDenseMaxSlices; ++z)
+      if (z < slices)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (uint32_t)s[z][e];
+  } else {
+    for (int z = 0; z < slices; ++z) {
+      const int32_t* src = part + ((int64_t)z * g.N + b) * g.M + u0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (u0 + e < g.M) v[e] += (uint32_t)src[e];
+    }
   }
-  dense_epilogue(g, b, u0, v);
+  int32_t w[4] = {(int32_t)v[0], (int32_t)v[1], (int32_t)v[2], (int32_t)v[3]};
+  dense_epilogue(g, b, u0, w);
 }
 
 }  // namespace
@@ -201,7 +223,7 @@ int conv_dense_run(const ConvGeom& g, const GemmArgs& ga, void* scratch, hipStre
     else hipLaunchKernelGGL((dense_tile_kernel<1, true>), grid, dim3(256), 0, s, ga, ksteps, kper, part);
     TK_LAUNCH_CHECK();
     const int64_t groups = (int64_t)g.N * ((std::max(g.O, ga.shadow_out ? (int)ga.shadow_cpad : 0) + 3) / 4);
-    hipLaunchKernelGGL(dense_slices_epilogue_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, ga, slices,
+    hipLaunchKernelGGL(dense_slices_epilogue_kernel, dim3((unsigned)((groups + 63) / 64)), dim3(64), 0, s, ga, slices,
                        (const int32_t*)part);
   } else if (ctd == 2) {
     hipLaunchKernelGGL((dense_tile_kernel<2, false>), grid, dim3(256), 0, s, ga, ksteps, kper, part);
