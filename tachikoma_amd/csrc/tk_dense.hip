@@ -83,14 +83,14 @@ __device__ __forceinline__ void dense_epilogue(const GemmArgs& g, int b, int u0,
 // grid (unit tiles, sample tiles, K slices); slice z = K steps [z * kper, (z + 1) * kper); wave w
 // of the workgroup takes a quarter of the slice.  SPLIT: raw sums to part[z][B][U]; else the
 // block epilogue.
-template <int CTD, bool SPLIT>
-__global__ __launch_bounds__(256) void dense_tile_kernel(GemmArgs g, int32_t ksteps, int32_t kper, int32_t* part) {
-  __shared__ int32_t red[4][32][CTD * 32 + 1];  // [wave][unit row][sample col], +1 against conflicts
+template <int CTD, bool SPLIT, int W = 4>
+__global__ __launch_bounds__(64 * W) void dense_tile_kernel(GemmArgs g, int32_t ksteps, int32_t kper, int32_t* part) {
+  __shared__ int32_t red[W][32][CTD * 32 + 1];  // [wave][unit row][sample col], +1 against conflicts
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r0 = blockIdx.x * 32, c0 = blockIdx.y * (CTD * 32);
   const int rl = lane & 31, h = lane >> 5;
   const int z0 = blockIdx.z * kper, z1 = min(ksteps, z0 + kper);
-  const int per = (z1 - z0 + 3) / 4;
+  const int per = (z1 - z0 + W - 1) / W;
   const int s0 = z0 + wave * per, s1 = min(z1, s0 + per);
   const int8_t* arow = g.A + (int64_t)(r0 + rl) * g.lda + 16 * h;  // packed rows exist up to rows_pad
   const int8_t* bcol[CTD];
@@ -129,9 +129,10 @@ __global__ __launch_bounds__(256) void dense_tile_kernel(GemmArgs g, int32_t kst
 #pragma unroll
     for (int q = 0; q < 16; ++q) red[wave][(q & 3) + 8 * (q >> 2) + 4 * h][j * 32 + rl] = acc[j][q];
   __syncthreads();
-  // thread t (of 256) owns samples c0 + t / 8 (+ 32 for CTD = 2) and units r0 + 4 (t % 8) .. + 3
+  // thread t (< 256) owns samples c0 + t / 8 (+ 32 for CTD = 2) and units r0 + 4 (t % 8) .. + 3
   // (consecutive in the [B, U] records: 16-byte int32 stores)
   const int t = threadIdx.x;
+  if (t >= 256) return;
   const int i0 = (t & 7) * 4, u0 = r0 + i0;
 #pragma unroll
   for (int jj = 0; jj < CTD; ++jj) {
@@ -139,9 +140,12 @@ __global__ __launch_bounds__(256) void dense_tile_kernel(GemmArgs g, int32_t kst
     if (b >= g.N) continue;
     int32_t v[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      v[e] = (int32_t)((uint32_t)red[0][i0 + e][jc] + (uint32_t)red[1][i0 + e][jc] + (uint32_t)red[2][i0 + e][jc] +
-                       (uint32_t)red[3][i0 + e][jc]);
+    for (int e = 0; e < 4; ++e) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) x += (uint32_t)red[w][i0 + e][jc];
+      v[e] = (int32_t)x;
+    }
     if constexpr (SPLIT) {
       int32_t* dst = part + ((int64_t)blockIdx.z * g.N + b) * g.M + u0;
       if (u0 + 3 < g.M && ((((int64_t)blockIdx.z * g.N + b) * g.M + u0) & 3) == 0) {
@@ -208,6 +212,17 @@ int conv_dense_run(const ConvGeom& g, const GemmArgs& ga, void* scratch, hipStre
   TK_CHECK_ARG(ga.RA || ga.zB == 0, "dense tile kernel: weight sums needed for the input zero point");
   TK_CHECK_ARG(ga.k_pad <= ga.lda && (int64_t)(g.O + 31) / 32 * 32 <= g.rows_pad, "dense tile kernel: packed weight rows");
   const int ksteps = g.cin_pad / 32;
+  // one launch where 32-sample tiles give the chip >= 48 workgroups: eight waves split K (every
+  // wave's loads in one batch for K <= 2048)
+  {
+    const unsigned ut1 = (unsigned)((g.O + 31) / 32), st1 = (unsigned)((g.N + 31) / 32);
+    if ((int64_t)ut1 * st1 >= 48 || !scratch) {
+      hipLaunchKernelGGL((dense_tile_kernel<1, false, 8>), dim3(ut1, st1, 1u), dim3(512), 0, s, ga, ksteps, ksteps,
+                         (int32_t*)nullptr);
+      TK_LAUNCH_CHECK();
+      return TK_OK;
+    }
+  }
   const int ctd = g.N > 32 ? 2 : 1;
   const unsigned ut = (unsigned)((g.O + 31) / 32), st = (unsigned)((g.N + 32 * ctd - 1) / (32 * ctd));
   // K slices: enough workgroups for the chip, >= 8 K steps (2 per wave) per slice
