@@ -58,9 +58,12 @@ def parse(argv=None):
                    help="memory: trace image complete in pinned host RAM; file: also write every step's image "
                         "to trace.rank<r>.tkt, overlapped with the next step (two pinned images, writer thread)")
     p.add_argument("--out-dir", default="/tmp")
-    p.add_argument("--file-overlap", choices=["on", "off"], default="on",
-                   help="file sink: write image i while step i+1 runs (on) or finish each write before the next "
-                        "step starts (off: no D2H / writer concurrency, the contention check)")
+    p.add_argument("--file-overlap", choices=["on", "off", "auto"], default="auto",
+                   help="file sink: write image i while step i+1 runs (on), finish each write before the next "
+                        "step starts (off: no D2H / writer concurrency), or auto: time 3 steps of each before the "
+                        "warm-up and keep the faster (the writer and the next step's D2H slow each other by "
+                        "box-dependent amounts: overlapped won on one round-4 box, 126.8 vs 107.7 op-traces/s, and "
+                        "lost on another, 89.3 vs 106.2)")
     p.add_argument("--no-trace", action="store_true", help="compute-only steps (profiling aid; not the metric)")
     p.add_argument("--tune-report", default=None, help="write the find step's per-node kernel timings (JSON) here")
     p.add_argument("--tune-table", default="auto",
@@ -419,6 +422,8 @@ def main(argv=None) -> int:
     d2h_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
 
+    overlap_mode = ["off" if args.file_overlap == "off" else "on"]
+
     def step(i, timed=False):
         if args.no_trace:
             m.run(trace=False)
@@ -438,7 +443,7 @@ def main(argv=None) -> int:
             d2h_ev[i][1].record(cap.capture_stream)
         if writer is not None:
             pending[k] = writer.submit(write_image, cap)
-            if args.file_overlap == "off":
+            if overlap_mode[0] == "off":
                 pending[k].result()
 
     def drain():
@@ -457,6 +462,20 @@ def main(argv=None) -> int:
     if args.run_mode == "auto" and not args.no_trace:
         mode_pick = m.pick_run_mode(steps=2)
         torch.cuda.synchronize(device)
+    overlap_pick = None
+    if writer is not None and args.file_overlap == "auto":
+        # the sink's find step (untimed): 3 steps overlapped vs 3 serialised, the faster is kept
+        overlap_pick = {}
+        for mode in ("on", "off"):
+            overlap_mode[0] = mode
+            step(0)
+            drain()
+            tp = time.perf_counter()
+            for i in range(3):
+                step(i)
+            drain()
+            overlap_pick[mode] = round((time.perf_counter() - tp) / 3 * 1e3, 1)
+        overlap_mode[0] = min(overlap_pick, key=overlap_pick.get)
     for i in range(args.warmup):
         step(i)
     drain()
@@ -578,7 +597,8 @@ def main(argv=None) -> int:
         # the file on disk must carry exactly the records the device digested
         from tachikoma_amd.trace_format import trace_file_digest
         fd = trace_file_digest(path)
-        file_check = {"path": path, "filesystem": mount_of(path), "overlap": args.file_overlap,
+        file_check = {"path": path, "filesystem": mount_of(path), "overlap": overlap_mode[0],
+                      "overlap_pick_ms_per_step": overlap_pick,
                       "writer": {k: os.environ[k] for k in ("TK_WRITE_THREADS", "TK_WRITE_PIECE_MB", "TK_WRITE_BUFFERED")
                                  if os.environ.get(k)} or "default (O_DIRECT, 256 MiB pieces, 2 threads)",
                       "file_digest": shard.hex64(fd), "device_digest": shard.hex64(digests[rank]),
@@ -726,7 +746,7 @@ def main(argv=None) -> int:
             "parity": par,
             "file_sink": None if args.sink != "file" else
             {k: ranks[0]["file_sink"].get(k) for k in ("achieved_GBps", "probe_GBps", "frac", "equal", "overlap",
-                                                      "filesystem", "writer")},
+                                                      "overlap_pick_ms_per_step", "filesystem", "writer")},
             "ranks": ranks,
             "extra": {
                 "compute_only_ms_per_step": round(compute_ms, 3),

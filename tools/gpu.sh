@@ -55,6 +55,8 @@ for r in "$@"; do
     filesink)
       (df -hT /tmp . ; cat /proc/mounts) > "$O/mounts.txt" 2>&1
       run 600 bench_file.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file --out-dir /tmp
+      run 600 bench_file_overlap.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file \
+        --out-dir /tmp --file-overlap on
       run 600 bench_file_serial.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file \
         --out-dir /tmp --file-overlap off ;;
     filesweep)
