@@ -14,6 +14,7 @@
 #   layers     rocprofv3 kernel trace of compute-only steps (per-layer durations)
 #   filesink   bench --sink file, overlapped and serial     filesweep  file sink writer shapes
 #   realized   realized relay.quantize ResNet-50 trace rate (tools/realized_times.py)
+#   gloo2      2-rank rehearsal on one GPU (gloo collectives; both ranks' records cross one PCIe link)
 #   hostmem    host DRAM write / read bandwidth of the GPU's NUMA node, alone and beside a traced bench
 #   tests:<k>  pytest -m gpu -k <k>               file:<path>  pytest -m gpu of one test file
 set -o pipefail
@@ -68,6 +69,7 @@ for r in "$@"; do
           --sink file --out-dir /tmp
       done ;;
     realized) run 600 realized.log python3 -u tools/realized_times.py ;;
+    gloo2) run 600 bench_2rank_gloo.json python3 -u bench.py --gpus 2 --dist-backend gloo --steps 10 --warmup 3 ;;
     hostmem)
       # host DRAM bandwidth of the GPU's NUMA node, alone and while a traced bench writes its image
       node=$(python3 -c 'import sys; sys.path.insert(0, "."); from tachikoma_amd import shard; print(shard.pci_numa_node(shard.gpu_pci_address(0)))')
