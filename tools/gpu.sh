@@ -69,6 +69,8 @@ for r in "$@"; do
           --sink file --out-dir /tmp
       done ;;
     realized) run 600 realized.log python3 -u tools/realized_times.py ;;
+    splitlayers) run 400 splitlayers.log rocprofv3 --kernel-trace --output-format csv -d "$O/splitlayers" -o run -- \
+        python3 -u bench.py --steps 3 --warmup 1 --skip-cpu --no-trace --tune-table profiles/r04_split_probe_table.json ;;
     gloo2) run 600 bench_2rank_gloo.json python3 -u bench.py --gpus 2 --dist-backend gloo --steps 10 --warmup 3 ;;
     hostmem)
       # host DRAM bandwidth of the GPU's NUMA node, alone and while a traced bench writes its image
