@@ -96,7 +96,13 @@ def summarise(d, launches=None, runs=None, model="resnet50", batch=64):
         disp.append({"i": i, "kernel": name, "grid": m["grid"], "lds_bytes": m["lds"],
                      "lds_conflict_per_inst": round(steps[i].get("SQ_LDS_BANK_CONFLICT", 0.0) / lds_i, 3) if lds_i else None,
                      "SQ_INSTS_LDS": lds_i, "SQ_LDS_BANK_CONFLICT": steps[i].get("SQ_LDS_BANK_CONFLICT"),
-                     "hbm_bytes": steps[i].get("FETCH_SIZE", 0.0) * KIB * 2 + steps[i].get("WRITE_SIZE", 0.0) * KIB})
+                     "hbm_bytes": steps[i].get("FETCH_SIZE", 0.0) * KIB * 2 + steps[i].get("WRITE_SIZE", 0.0) * KIB,
+                     # share of the waves' cycles spent waiting on counters / on issue / issuing
+                     **{k: round(steps[i].get(c, 0.0) / steps[i]["SQ_WAVE_CYCLES"], 3)
+                        for k, c in (("wait_any_per_wave_cycle", "SQ_WAIT_ANY"),
+                                     ("wait_inst_per_wave_cycle", "SQ_WAIT_INST_ANY"),
+                                     ("active_inst_per_wave_cycle", "SQ_ACTIVE_INST_ANY"))
+                        if steps[i].get("SQ_WAVE_CYCLES")}})
     per_kernel = {}
     for name, f in sorted(fam.items(), key=lambda kv: -kv[1].get("SQ_LDS_BANK_CONFLICT", 0.0)):
         li = f.get("SQ_INSTS_LDS", 0.0)
