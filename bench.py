@@ -85,6 +85,10 @@ def parse(argv=None):
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse N>1 on one GPU")
     p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
+    p.add_argument("--force-pg", action="store_true",
+                   help="start the process group and run the N>1 collectives (elapsed all-reduce, record-digest "
+                        "all-gather, rank-info all-gather, status broadcast) even at one rank: exercises the RCCL "
+                        "branch on a single GPU")
     return p.parse_args(argv)
 
 
@@ -294,6 +298,14 @@ def find_tune_table(model: str, batch: int):
 
 # ---------------------------------------------------------------- one rank
 
+def dump_maps_at_exit() -> None:
+    """TK_DUMP_MAPS=path: write /proc/self/maps there (the mapping the process exits with), so that
+    raw PCs of a crash during exit (glog / rocprofv3 backtraces) can be symbolised offline."""
+    path = os.environ.get("TK_DUMP_MAPS")
+    if path:
+        with open("/proc/self/maps") as src, open(path, "w") as dst:
+            dst.write(src.read())
+
 def check_gpu_count(args) -> None:
     """`--gpus N` over RCCL needs N visible GPUs (one rank per GPU): fail at once, before any rank
     starts or ``init_process_group("nccl")`` waits on a rank that cannot exist.  Counting devices
@@ -338,7 +350,13 @@ def main(argv=None) -> int:
     import torch
     import torch.distributed as dist
 
-    if world > 1:
+    pg = world > 1 or args.force_pg  # the collectives below run whenever a process group exists
+    if pg and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if pg:
         if args.dist_backend == "nccl":
             torch.cuda.set_device(local_rank)
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
@@ -454,7 +472,7 @@ def main(argv=None) -> int:
         torch.cuda.synchronize(device)  # every stream, the capture streams included
 
     def barrier():
-        if world > 1:
+        if pg:
             dist.barrier()
 
     # submission find step (untimed): host-issued vs one replayed HIP graph per traced step
@@ -504,7 +522,7 @@ def main(argv=None) -> int:
         [rec_bytes / (a.elapsed_time(z) * 1e-3) / 1e9 for a, z in d2h_ev]
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
+    if pg:
         tc = t.to(coll_dev)
         dist.all_reduce(tc, op=dist.ReduceOp.MAX)
         t = tc
@@ -623,7 +641,7 @@ def main(argv=None) -> int:
     parity = Parity(read_trace(caps[0].bytes()).records) if not args.no_trace else None
     cpu = None
     quota = cpu_quota()
-    host_group = dist.new_group(backend="gloo") if world > 1 else None
+    host_group = dist.new_group(backend="gloo") if pg else None
     if parity is not None:
         from oracle import graph_ref
         # (at N = 1 the CPU baseline's samples are the parity set; --skip-cpu keeps two)
@@ -636,7 +654,7 @@ def main(argv=None) -> int:
                 rec = graph_ref.calibrate(one.mod, one.params, {"data": x[i:i + 1]}, backend="c", threads=share)
                 parity.check(i, offset + i, rec)
                 del rec
-        if world > 1:
+        if pg:
             dist.barrier(group=host_group)
         if rank == 0 and not args.skip_cpu:
             cpus = home_cpus if world == 1 else os.sched_getaffinity(0)
@@ -645,7 +663,7 @@ def main(argv=None) -> int:
             _log(f"cpu baseline (oracle port, {threads} threads) + parity ...")
             cpu = cpu_baseline(model_fn, offset, count, args.cpu_budget_s, threads, parity)
             cpu["n_gpus_running"] = world
-        if world > 1:
+        if pg:
             dist.barrier(group=host_group)
     per_step = {"min": round(min(step_gbps), 2), "max": round(max(step_gbps), 2),
                 "mean": round(sum(step_gbps) / len(step_gbps), 2)} if step_gbps else None
@@ -674,7 +692,7 @@ def main(argv=None) -> int:
                           note="trace image bytes per traced step (written while the next step runs) vs the same "
                                "image written alone by the same writer, best of 2 probes before the timed region "
                                "and 2 after")
-    if world > 1:
+    if pg:
         ranks = [None] * world
         dist.all_gather_object(ranks, rank_info)
     else:
@@ -713,7 +731,7 @@ def main(argv=None) -> int:
                                    f"full per-op trace to pinned host memory",
                        "model": args.model, "global_batch": B * world, "samples_per_gpu": B, "seq_len": None,
                        "parallelism": f"batch-shard x{world}", "sink": args.sink,
-                       "dist_backend": args.dist_backend if world > 1 else None},
+                       "dist_backend": args.dist_backend if pg else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved_bw / 1e9, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved_bw / 1e9 / HBM_PEAK_GBPS, 4),
                          "traffic": None if pmc is None else int(pmc["per_launch"]),
@@ -774,6 +792,10 @@ def main(argv=None) -> int:
                 "records_per_sample": len(m.plan.records),
                 "op_records_per_s": round(value * len(m.plan.records), 1),
                 "record_digests": [shard.hex64(d) for d in digests],
+                "collectives": {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                                "device": str(coll_dev),
+                                "ran": ["barrier", "all_reduce(max elapsed)", "all_gather(record digest)",
+                                        "all_gather_object(rank info)", "broadcast(status)"]} if pg else None,
                 "library": _lib.build_info(),
                 "host_cpus": {"affinity": len(home_cpus), "cgroup_quota": quota, "os_cpu_count": os.cpu_count()},
             },
@@ -781,11 +803,20 @@ def main(argv=None) -> int:
         print(json.dumps(line), flush=True)
         if rc:
             _log(f"PARITY FAILURE: {par['mismatches']} mismatching records, first {par['first_mismatch']}")
-    if world > 1:
+    if pg:
         flag = torch.tensor([rc], dtype=torch.int32, device=coll_dev)
         dist.broadcast(flag, 0)
         rc = int(flag.item())
         dist.destroy_process_group()
+    # teardown while the HIP runtime is alive: device idle, native module destroyed, pinned images
+    # released -- nothing is left for finalisers or library static destructors at exit
+    caps.clear()
+    parity = None
+    m.close()
+    import gc
+    gc.collect()
+    torch._C._host_emptyCache()  # the pinned trace images go back to the driver now, not at exit
+    dump_maps_at_exit()
     return rc
 
 

@@ -141,8 +141,9 @@ def eval_call(call, args, backend: str = "numpy", threads: int = 1):
     if op in ("qnn.add", "qnn.subtract", "qnn.mul"):
         c = [_const(call.args[i]) for i in range(2, 8)]
         fn = {"qnn.add": ref.qnn_add, "qnn.subtract": ref.qnn_subtract, "qnn.mul": ref.qnn_mul}[op]
-        kw = {"rounding": _resolve_rounding(a)} if op == "qnn.mul" else {}
-        return fn(args[0], args[1], *c, lhs_axis=a.get("lhs_axis", -1), rhs_axis=a.get("rhs_axis", -1), **kw)
+        # every inner Requantize takes the requantize_config's rounding (qnn/utils.h:106-122)
+        return fn(args[0], args[1], *c, lhs_axis=a.get("lhs_axis", -1), rhs_axis=a.get("rhs_axis", -1),
+                  rounding=_resolve_rounding(a))
     if op == "qnn.concatenate":
         scales = [_const(f) for f in call.args[1].fields]
         zps = [_const(f) for f in call.args[2].fields]

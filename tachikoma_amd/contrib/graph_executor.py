@@ -125,6 +125,21 @@ class GraphModule:
         if self.plan.inputs:
             self._meta["n_samples"] = int(self.plan.inputs[0].shape[0]) if self.plan.inputs[0].shape else 1
 
+    def close(self) -> None:
+        """Wait for the device, then release the native module and the pinned trace image.  Call it
+        (or use the module as a context manager) before the process exits; an atexit hook closes
+        any module left open (device_module.close_all)."""
+        self.module.close()
+        if self._capture is not None:
+            self._capture.capture_stream.synchronize()
+            self._capture = None
+
+    def __enter__(self) -> "GraphModule":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
     # -- reference surface -------------------------------------------------
     def set_input(self, key=None, value=None, **params):
         """graph_executor.py:166-197: ``key`` (name or input index) = ``value`` plus keyword

@@ -243,14 +243,28 @@ class _Builder:
         elif p.op == "qnn.requantize":
             out = self.requantize_lower(ins[0], a, p.consts, a.get("channel_axis", 1), p.out.dtype)
         elif p.op == "qnn.add":
+            if not (tuple(self.t(ins[0]).shape) == tuple(self.t(ins[1]).shape) == tuple(p.out.shape)):
+                # QnnBroadcastRel operands: the canonical evaluators (oracle and device) add
+                # same-shape tensors only
+                raise UnsupportedError(f"canonical graph: broadcasting qnn.add {p.name}")
             sides = []
             for side, x in (("lhs", ins[0]), ("rhs", ins[1])):
                 if a[f"{side}_upcast"]:
                     sides.append(self.cast(x, "int32"))
                 else:
+                    # RequantizeOrUpcast (op_common.h:186-207): the side's Requantize with the
+                    # op's rounding (requantize_config at construction) and, per axis, the side's
+                    # multipliers / shifts / zero points along {side}_axis
                     ra = {"mode": a[f"{side}_mode"], "multiplier": a[f"{side}_multiplier"], "shift": a[f"{side}_shift"],
-                          "input_zero_point": a[f"{side}_zero_point"], "output_zero_point": a["output_zero_point"]}
-                    sides.append(self.requantize_lower(x, ra, {}, -1, "int32"))
+                          "input_zero_point": a[f"{side}_zero_point"], "output_zero_point": a["output_zero_point"],
+                          "rounding": a.get("rounding", "UPWARD")}
+                    consts = {}
+                    if f"{side}_multipliers" in p.consts:
+                        consts["multipliers"] = p.consts[f"{side}_multipliers"]
+                        consts["shifts"] = p.consts[f"{side}_shifts"]
+                    if f"{side}_zero_points" in p.consts:
+                        consts["input_zero_points"] = p.consts[f"{side}_zero_points"]
+                    sides.append(self.requantize_lower(x, ra, consts, a.get(f"{side}_axis", 1), "int32"))
             o = self.emit("add", sides, {}, p.out.shape, "int32")
             o = self.subtract_scalar(o, a["output_zero_point"])
             lo, hi = _RANGE[p.out.dtype]

@@ -17,7 +17,10 @@ separate trace record) from one kernel.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
+import sys
+import weakref
 from typing import Callable, Dict, List, Optional
 
 import numpy as np
@@ -35,6 +38,24 @@ def torch_dtype(name: str):
     torch = _torch()
     return {"int8": torch.int8, "uint8": torch.uint8, "int16": torch.int16, "int32": torch.int32,
             "int64": torch.int64, "float32": torch.float32}[name]
+
+
+# Every DeviceModule whose native module is alive.  The atexit hook closes them before the
+# interpreter finalises (atexit runs first, LIFO after torch's own hooks were registered at import),
+# so no tk_module_destroy -- HIP graph / event / stream / hipFree calls -- ever runs from a finaliser
+# or after the HIP runtime's static destructors (the round-4 exit SIGSEGV under rocprofv3 was raised
+# inside __cxa_finalize).
+_LIVE: "weakref.WeakSet[DeviceModule]" = weakref.WeakSet()
+
+
+@atexit.register
+def close_all() -> None:
+    """Close every live DeviceModule (also callable directly, e.g. before os._exit)."""
+    for m in list(_LIVE):
+        try:
+            m.close()
+        except Exception as e:  # report, keep closing the others
+            sys.stderr.write(f"[tachikoma] closing a module at exit failed: {e}\n")
 
 
 def tune_table_digest(entries) -> str:
@@ -425,6 +446,7 @@ class DeviceModule:
         handle = ctypes.c_void_p()
         _lib.check(self.lib.tk_module_create(arr, len(nodes), ctypes.byref(handle)), "tk_module_create")
         self.handle = handle
+        _LIVE.add(self)
         self.n_nodes = len(nodes)
 
     def _fill_binary(self, qb, op: PlanOp) -> None:
@@ -606,14 +628,38 @@ class DeviceModule:
         if nbytes > 0:
             n.ext[3] = self._scratch(nbytes).data_ptr()
 
-    def __del__(self):
+    @property
+    def closed(self) -> bool:
         h = getattr(self, "handle", None)
-        if h is not None and h.value:
-            try:
-                self.lib.tk_module_destroy(h)
-            except Exception:
-                pass
+        return h is None or not h.value
+
+    def close(self) -> None:
+        """Release the native module (tk_module_destroy: its HIP graphs, events, streams and packed
+        capture mirrors) after the device has finished every stream that may still use them, and
+        drop the HBM buffers.  Idempotent.  Runs while the HIP runtime is alive: explicitly, from
+        the atexit hook below (before interpreter finalisation and before any library's static
+        destructors), or from ``__del__`` outside finalisation -- never from a finaliser at process
+        teardown, where the runtime (or a profiler's interception tables) may already be gone."""
+        h = getattr(self, "handle", None)
+        if h is None or not h.value:
+            return
+        torch = _torch()
+        try:
+            torch.cuda.synchronize(self.device)
+        finally:
             self.handle = None
+            _LIVE.discard(self)
+            _lib.check(self.lib.tk_module_destroy(h), "tk_module_destroy")
+            self.buffers = {}
+            self._keep = []
+
+    def __del__(self):
+        if sys.is_finalizing():
+            return  # leaked on purpose: the process is ending, no HIP calls from finalisers
+        try:
+            self.close()
+        except Exception:
+            pass
 
     # ------------------------------------------------------------ execution
     def _check_value(self, name: str, value):

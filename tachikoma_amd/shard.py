@@ -52,8 +52,9 @@ def gather_digests(digest, device=None) -> List[int]:
         t = digest.reshape(1).to(torch.int64)
     else:
         t = torch.tensor([_to_i64(int(digest))], dtype=torch.int64, device=device)
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return [int(t.item()) & 0xFFFFFFFFFFFFFFFF]
+    # (at world size 1 the all-gather still runs: bench.py --force-pg exercises the RCCL path)
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [int(v.item()) & 0xFFFFFFFFFFFFFFFF for v in out]
@@ -122,11 +123,14 @@ def gpu_pci_address(device_index: int) -> Optional[str]:
         return None
 
 
-def pci_numa_node(pci: Optional[str]) -> Optional[int]:
+SYSFS = os.environ.get("TK_SYSFS_ROOT", "/sys")  # a fake tree in tests (tests/test_placement.py)
+
+
+def pci_numa_node(pci: Optional[str], sysfs: Optional[str] = None) -> Optional[int]:
     if not pci:
         return None
     try:
-        with open(f"/sys/bus/pci/devices/{pci}/numa_node") as f:
+        with open(f"{sysfs or SYSFS}/bus/pci/devices/{pci}/numa_node") as f:
             node = int(f.read().strip())
     except (OSError, ValueError):
         return None
@@ -146,28 +150,44 @@ def _parse_cpulist(text: str) -> List[int]:
     return cpus
 
 
-def node_cpus(node: int) -> List[int]:
+def node_cpus(node: int, sysfs: Optional[str] = None) -> List[int]:
     try:
-        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+        with open(f"{sysfs or SYSFS}/devices/system/node/node{node}/cpulist") as f:
             return _parse_cpulist(f.read())
     except OSError:
         return []
 
 
-def bind_to_gpu_node(device_index: int) -> dict:
+def placement(pci: Optional[str], affinity=None, sysfs: Optional[str] = None) -> dict:
+    """Where a rank driving the GPU at ``pci`` runs: the GPU's NUMA node and that node's CPUs
+    within ``affinity`` (default: this process's).  Pure: nothing is bound.  {"pci", "numa_node",
+    "cpus" (sorted list), "bound"}: bound is False (cpus = affinity) when the node or its CPU list
+    cannot be read or does not meet the affinity."""
+    aff = sorted(os.sched_getaffinity(0) if affinity is None else affinity)
+    node = pci_numa_node(pci, sysfs)
+    cpus = sorted(set(node_cpus(node, sysfs)) & set(aff)) if node is not None else []
+    return {"pci": pci, "numa_node": node, "cpus": cpus or aff, "bound": bool(cpus)}
+
+
+def rank_plan(world: int, pcis: List[Optional[str]], affinity=None, sysfs: Optional[str] = None) -> List[dict]:
+    """The N-rank launch plan of one node (bench.py --gpus N, one process per GPU): rank r drives
+    GPU r (LOCAL_RANK = r), binds to its GPU's NUMA node's CPUs and first-touches its pinned trace
+    image from there, so every image sits in its own socket's DRAM.  Fails when there are fewer
+    GPUs than ranks (one GPU per rank)."""
+    if world > len(pcis):
+        raise ValueError(f"{world} ranks need {world} GPUs, {len(pcis)} visible")
+    return [dict(rank=r, gpu=r, image_node=p["numa_node"], **p)
+            for r, p in ((r, placement(pcis[r], affinity, sysfs)) for r in range(world))]
+
+
+def bind_to_gpu_node(device_index: int, pci: Optional[str] = None, sysfs: Optional[str] = None) -> dict:
     """Restrict this process to the CPUs of the GPU's NUMA node (intersected with the current
-    affinity).  Returns {"pci", "numa_node", "cpus", "bound"}; nothing changes when the node
-    or its CPU list cannot be read."""
-    pci = gpu_pci_address(device_index)
-    node = pci_numa_node(pci)
-    info = {"pci": pci, "numa_node": node, "cpus": len(os.sched_getaffinity(0)), "bound": False}
-    if node is None:
-        return info
-    cpus = set(node_cpus(node)) & set(os.sched_getaffinity(0))
-    if cpus:
-        os.sched_setaffinity(0, cpus)
-        info.update(cpus=len(cpus), bound=True)
-    return info
+    affinity).  Returns {"pci", "numa_node", "cpus" (count), "bound"}; nothing changes when the
+    node or its CPU list cannot be read."""
+    info = placement(pci if pci is not None else gpu_pci_address(device_index), sysfs=sysfs)
+    if info["bound"]:
+        os.sched_setaffinity(0, info["cpus"])
+    return dict(info, cpus=len(info["cpus"]))
 
 
 def numa_pages(ptr: int, nbytes: int) -> Optional[dict]:

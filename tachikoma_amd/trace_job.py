@@ -253,7 +253,14 @@ class GraphModuleTracer:
         return fut
 
     def close(self) -> None:
+        """Wait for the writer, then release every module (device first, then the native module:
+        GraphModule.close) while the HIP runtime is alive."""
         self.writer.shutdown(wait=True)
+        for m, caps, _ in self.modules.values():
+            m.close()
+            caps.clear()
+        self.modules.clear()
+        self.digest_slots.clear()
 
 
 def main(argv=None) -> int:

@@ -143,3 +143,36 @@ def test_tonearest_requantize_lowering():
     assert any(r.op == "qnn.requantize" for r in plan.ops if r.name in {o.record for o in checked})
     names = [n.func_name for n in fused_nodes(canon)]
     assert any("greater_equal_where" in n for n in names), names
+
+
+@pytest.mark.parametrize("rounding", ["UPWARD", "TONEAREST"])
+def test_per_axis_qnn_add_lowering(rounding):
+    """qnn.add with a per-axis side (scales and zero points along lhs_axis) and the rounding of the
+    requantize_config it was built under: each side lowers to its own Requantize (RequantizeOrUpcast,
+    src/relay/qnn/op/op_common.h:186-207) along that side's axis, and the canonical values equal the
+    QNN oracle's record; a broadcasting add is refused, not lowered wrongly."""
+    x = relay.var("x", (2, 3, 4, 5), "int8")
+    y = relay.var("y", (2, 3, 4, 5), "int8")
+    with qnn.op.requantize_config(rounding=rounding):
+        e = qnn.op.add(x, y, relay.const(np.array([0.11, 0.23, 0.37], np.float32)),
+                       relay.const(np.array([1, -3, 4], np.int32)), 0.25, 1, 0.5, 2, lhs_axis=1)
+    mod = relay.IRModule.from_expr(e)
+    plan = lower(mod, {})
+    (op,) = plan.ops
+    assert op.attrs["rounding"] == rounding and "lhs_multipliers" in op.consts and not op.attrs["per_tensor"]
+    canon = canonicalize(plan)
+    kinds = [o.op for o in canon.ops]
+    if rounding == "UPWARD":
+        assert "fixed_point_multiply_per_axis" in kinds
+    else:
+        assert "fixed_point_multiply_per_axis" not in kinds and "where" in kinds
+    rng = np.random.default_rng(3)
+    xs = {"x": rng.integers(-128, 128, (2, 3, 4, 5), dtype=np.int8),
+          "y": rng.integers(-128, 128, (2, 3, 4, 5), dtype=np.int8)}
+    vals = canonical_ref.evaluate(canon, dict(xs))
+    rec = graph_ref.calibrate(mod, {}, xs)
+    rop = [o for o in canon.ops if o.record is not None]
+    assert rop and all(np.array_equal(vals[o.name], rec[o.record]) for o in rop)
+    b = qnn.op.add(x, relay.var("z", (3, 1, 1), "int8"), 0.5, 0, 0.25, 1, 0.5, 0)
+    with pytest.raises(relay.UnsupportedError if hasattr(relay, "UnsupportedError") else Exception):
+        canonicalize(lower(relay.IRModule.from_expr(b), {}))

@@ -53,6 +53,41 @@ def test_lenet5_trace(device, tmp_path):
     _compare(tr.records, exp)
 
 
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_lenet5_batch1_trace(device, tmp_path, use_graph):
+    """BASELINE config 2 as stated: LeNet-5 int8 MNIST at batch 1 (the batch-1 tilings of every
+    kernel), host-issued and as one replayed HIP graph, every record bit-exact vs the oracle, over
+    several inputs through the same module (set_input between traced runs)."""
+    model = zoo.lenet5(batch=1)
+    lib = relay.build(model.mod, target="mi355x", params=model.params)
+    m = graph_executor.GraphModule(lib["default"]())
+    m.module.use_graph = use_graph
+    for i in range(3):
+        x = model.sample_inputs(i, 1)
+        m.set_input("data", x)
+        path = str(tmp_path / f"lenet5_b1_{i}.tkt")
+        m.dump_trace(path)
+        tr = read_trace(path)
+        exp = graph_ref.calibrate(model.mod, model.params, {"data": x})
+        assert set(tr.records) == set(exp)
+        _compare(tr.records, exp)
+
+
+def test_resnet18_tonearest_trace(device, tmp_path):
+    """ResNet-18 built under requantize_config(rounding="TONEAREST"): every requantize and both
+    RequantizeOrUpcasts of each qnn.add (fused residual joins) round to nearest
+    (qnn/utils.h:106-122, utils.cc:59-216); bit-exact vs the oracle."""
+    from tachikoma_amd.relay import qnn
+    with qnn.op.requantize_config(rounding="TONEAREST"):
+        model = zoo.resnet18(batch=2)
+    x = model.random_input()
+    m, tr = _run_trace(model, x, tmp_path)
+    adds = [o for o in m.plan.ops if o.op == "qnn.add"]
+    assert adds and all(o.attrs["rounding"] == "TONEAREST" for o in adds)
+    exp = graph_ref.calibrate(model.mod, model.params, {"data": x}, backend="c")
+    _compare(tr.records, exp)
+
+
 @pytest.mark.parametrize("name,batch,fuse", [("resnet18", 2, True), ("resnet18", 2, False), ("mobilenet_v2", 1, True),
                                              ("mobilenet_v2", 1, False), ("resnet50", 2, True)])
 def test_cnn_trace_bit_exact(device, tmp_path, name, batch, fuse):
