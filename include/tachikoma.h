@@ -424,6 +424,56 @@ typedef struct {
 } tk_transpose_attrs;
 int tk_transpose(const tk_tensor* data, tk_tensor* out, const tk_transpose_attrs* attrs, void* stream);
 
+/* qnn.leaky_relu (src/relay/qnn/op/leaky_relu.cc:85-140, QnnLeakyReluCanonicalize), int8 / uint8:
+ *   q   = RequantizeOrUpcast(int32(x)) to the output params (`rq`, per-tensor; `upcast` = plain cast)
+ *   out = int32(x) < input_zero_point ? FPM(q, alpha) + FPM(output_zero_point, 1 - alpha) : q
+ * clipped and cast to the input dtype (ConvertDtype).  FPM = fixed_point_multiply =
+ * tir.q_multiply_shift (intrin_rule.cc:197-250, the power-of-two branch included) with
+ * GetFixedPointMultiplierShift(alpha) / (1 - alpha) from tk_fixed_point_multiplier_shift. */
+typedef struct {
+  tk_requantize_attrs rq;
+  int32_t upcast;
+  int32_t input_zero_point;
+  int32_t output_zero_point;
+  int32_t alpha_multiplier, alpha_shift;
+  int32_t zp_multiplier, zp_shift;
+} tk_leaky_relu_attrs;
+int tk_qnn_leaky_relu(const tk_tensor* data, tk_tensor* out, const tk_leaky_relu_attrs* attrs, void* stream);
+
+/* The qnn unary ops (qnn.sqrt / rsqrt / exp / erf / sigmoid / hardswish / tanh / log / abs,
+ * src/relay/qnn/op/unary_elementwise_op.cc:31-56) legalize to a table lookup
+ * (python/tvm/relay/qnn/op/legalizations.py:54-86, canonicalizations.py:32-160):
+ * out = table[reinterpret<uint8>(x)], the 256-entry table built when the graph is built.
+ * int8 / uint8 data, same-dtype output; `table` is a device array of 256 bytes. */
+int tk_qnn_lookup(const tk_tensor* data, tk_tensor* out, const void* table, void* stream);
+
+/* qnn.batch_matmul (src/relay/qnn/op/batch_matmul.cc:162-228): x [B, M, K] int8/uint8, y [B', N, K]
+ * (transpose_b; B == B' or one of them 1) -> int32 [max(B, B'), M, N] = sum_k (x - zx)(y - zy)
+ * modulo 2^32 (the four-term canonical form).  Runs the qnn.dense kernel per batch entry with
+ * the zero points of `attrs` (input = x, kernel = y); workspace from
+ * tk_qnn_batch_matmul_workspace_bytes. */
+int64_t tk_qnn_batch_matmul_workspace_bytes(const tk_tensor* x, const tk_tensor* y);
+int tk_qnn_batch_matmul(const tk_tensor* x, const tk_tensor* y, tk_tensor* out, const tk_dense_attrs* attrs,
+                        void* workspace, void* stream);
+
+/* qnn.conv2d_transpose (legalizations.py:97-130: int16 operand shifts, then nn.conv2d_transpose,
+ * python/tvm/topi/nn/conv2d_transpose.py:79-140): NCHW int8/uint8 data, IOHW weight
+ * (C, O / groups, KH, KW) -> int32 NCHW (N, O, (H-1)*sh + KH - pt - pb + oph, ...):
+ *   out[n, o, y, x] = sum over c of o's group, r, s with y + pt - r = sh * iy, x + pl - s = sw * ix
+ *                     of int16(d - zd) * int16(w[c, o % (O/groups), r, s] - zw)      (int32, wraps)
+ * kernel_zero_points: optional device array of O/groups entries (bias_add on the weight's axis 1). */
+typedef struct {
+  int32_t strides[2];
+  int32_t padding[4];           /* top, left, bottom, right */
+  int32_t output_padding[2];
+  int32_t groups;
+  int32_t input_zero_point;
+  int32_t kernel_zero_point;
+  const int32_t* kernel_zero_points;
+} tk_conv2d_transpose_attrs;
+int tk_qnn_conv2d_transpose(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
+                            const tk_conv2d_transpose_attrs* attrs, void* stream);
+
 /* ---------------------------------------------------------------- executor
  * Native run loop replacing GraphExecutor::Run (graph_executor.cc:61-66) and
  * the debug executor's per-node copy-out (graph_executor_debug.cc:249-284).
@@ -456,6 +506,10 @@ enum {
   TK_NODE_QNN_BINARY = 23, /* in: lhs, rhs; attrs.qnn_binary */
   TK_NODE_CONCAT = 24,     /* in: 1..TK_MAX_NODE_INPUTS tensors; attrs.concat */
   TK_NODE_TRANSPOSE = 25,  /* in: data; attrs.transpose (layout changes around NHWC convs) */
+  TK_NODE_LEAKY_RELU = 26, /* in: data; attrs.leaky_relu */
+  TK_NODE_LOOKUP = 27,     /* in: data; ext[0]: the 256-byte device table (qnn unary ops) */
+  TK_NODE_BATCH_MATMUL = 28, /* in: x, y; attrs.dense (zero points); ext[0]: workspace */
+  TK_NODE_CONV2D_TRANSPOSE = 29, /* in: data (NCHW), weight (IOHW); attrs.conv2d_transpose */
 };
 
 #define TK_MAX_NODE_INPUTS 8
@@ -483,6 +537,8 @@ typedef struct {
     tk_qnn_binary_attrs qnn_binary;
     tk_concat_attrs concat;
     tk_transpose_attrs transpose;
+    tk_leaky_relu_attrs leaky_relu;
+    tk_conv2d_transpose_attrs conv2d_transpose;
     struct { int64_t a_min, a_max; } clip;
     struct { int32_t axis; } bias_add;
   } attrs;
@@ -513,20 +569,33 @@ int tk_module_run(tk_module* mod, void* stream, void* capture_stream, void* cons
  * are kept; tk_module_tune drops them; profiling mode runs tk_module_run. */
 int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst);
 /* How tk_module_run_graph copies records to host memory:
- *   0 (default) packed: the graph runs the nodes plus, after the node that completes each chunk of
- *     the trace image (tk_module_set_trace_chunks, 8 by default; chunks end where every record below
- *     them is written), a kernel that gathers the chunk's records into a device mirror of the image
- *     range the records span (header bytes included, loaded once from the host image) and an external
- *     event-record node; the chunk then leaves as one host-issued hipMemcpyAsync on capture_stream
- *     gated on that event.  Two mirrors alternate, so a run's kernels overlap the previous run's
- *     copies.  Whole-chunk copies run at 57.0 GB/s against 56.0 for per-record copies and 54.0-54.6
- *     for graph memcpy nodes (profiles/r04c_copyprobe.jsonl).  Record buffers must be 16-byte aligned
- *     and readable in whole 16-byte chunks; host destinations must not overlap.
+ *   0 (default) packed: the node loop is cut into one graph per chunk of the trace image
+ *     (tk_module_set_trace_chunks, 8 by default; a chunk ends at the node after which every record
+ *     below it is written) plus a tail graph; each chunk graph ends with a kernel that gathers the
+ *     chunk's records into a device mirror of the image range the records span (header bytes
+ *     included, loaded once from the host image).  After launching a chunk graph the call records a
+ *     host-side event on `stream` and issues the chunk's hipMemcpyAsync on capture_stream gated on
+ *     it (torch's bundled HIP 7.0 refuses external event-record nodes in stream capture), so a run
+ *     costs chunks + 1 graph launches.  Two mirrors alternate, so a run's kernels overlap the
+ *     previous run's copies.  Device memory: each packed plan holds two mirrors the size of the whole
+ *     span (ResNet-50 at 64 samples: 2 x 7.45 GB), and up to two plans (two host images: the file
+ *     sink) are cached, i.e. up to 4 x span.  Whole-chunk copies run at 57.0 GB/s against 56.0 for
+ *     per-record copies and 54.0-54.6 for graph memcpy nodes (profiles/r04c_copyprobe.jsonl).  Record
+ *     buffers must be 16-byte aligned and readable in whole 16-byte chunks; host destinations must
+ *     not overlap.
  *   2..4 one memcpy node per record in that many parallel chains (1 chain: pass 5);
  *   1 one copy kernel per node (kernel nodes writing pinned memory with 16-byte stores). */
 int tk_module_set_graph_copies(tk_module* mod, int copy_kernels);
 /* Chunks of the packed capture (1..256). */
 int tk_module_set_trace_chunks(tk_module* mod, int chunks);
+/* Copy trace of packed traced runs (the in-process counterpart of a memory-copy trace, e.g.
+ * rocprofv3 --memory-copy-trace): with tracing on, each packed run records a timing event on the
+ * compute stream before its first launch and two on the capture stream around every chunk copy.
+ * tk_module_copy_trace then (after waiting for the last run's copies) writes, per chunk c,
+ * out[3c .. 3c+2] = {bytes, copy start ms, copy end ms} relative to that first event, and returns
+ * the chunk count (out may hold fewer: max_chunks). */
+int tk_module_set_copy_trace(tk_module* mod, int enable);
+int tk_module_copy_trace(tk_module* mod, double* out, int max_chunks);
 /* Makes `stream` wait for the copies of the last traced run: call before writing any
  * tensor the module reads (GraphModule.set_input / load_params,
  * graph_executor.cc:158-166 SetInput) on a stream of your own. */

@@ -149,6 +149,25 @@ def eval_call(call, args, backend: str = "numpy", threads: int = 1):
         zps = [_const(f) for f in call.args[2].fields]
         return ref.qnn_concatenate(args[0], scales, zps, _const(call.args[3]), _const(call.args[4]), axis=a["axis"],
                                    rounding=_resolve_rounding(a))
+    if op == "qnn.leaky_relu":
+        return ref.qnn_leaky_relu(args[0], a["alpha"], *[_const(call.args[i]) for i in range(1, 5)],
+                                  rounding=_resolve_rounding(a))
+    if op in ref.unary_functions():
+        return ref.qnn_unary(op, args[0], *[_const(call.args[i]) for i in range(1, 5)])
+    if op == "qnn.batch_matmul":
+        return ref.qnn_batch_matmul(args[0], args[1], _const(call.args[2]), _const(call.args[3]))
+    if op == "qnn.conv2d_transpose":
+        x, w = args[0], args[1]
+        dl, kl = a.get("data_layout", "NCHW"), a.get("kernel_layout", "IOHW")
+        if dl == "NHWC":
+            x = np.ascontiguousarray(x.transpose(0, 3, 1, 2))
+        if kl != "IOHW":
+            w = np.ascontiguousarray(w.transpose([kl.index(ch) for ch in "IOHW"]))
+        za = np.asarray(_const(call.args[2])).reshape(-1)[0]
+        zw = np.asarray(_const(call.args[3]))
+        out = ref.qnn_conv2d_transpose(x, w, za, zw if zw.size > 1 else zw.reshape(-1)[0], strides=a["strides"],
+                                       padding=a["padding"], output_padding=a["output_padding"], groups=a["groups"])
+        return np.ascontiguousarray(out.transpose(0, 2, 3, 1)) if dl == "NHWC" else out
     if op == "qnn.quantize":
         return ref.quantize(args[0], _const(call.args[1]), _const(call.args[2]), axis=a["axis"],
                             out_dtype=a["out_dtype"])

@@ -199,6 +199,31 @@ class tk_transpose_attrs(ctypes.Structure):
     _fields_ = [("ndim", ctypes.c_int32), ("perm", ctypes.c_int32 * 6)]
 
 
+class tk_leaky_relu_attrs(ctypes.Structure):
+    _fields_ = [
+        ("rq", tk_requantize_attrs),
+        ("upcast", ctypes.c_int32),
+        ("input_zero_point", ctypes.c_int32),
+        ("output_zero_point", ctypes.c_int32),
+        ("alpha_multiplier", ctypes.c_int32),
+        ("alpha_shift", ctypes.c_int32),
+        ("zp_multiplier", ctypes.c_int32),
+        ("zp_shift", ctypes.c_int32),
+    ]
+
+
+class tk_conv2d_transpose_attrs(ctypes.Structure):
+    _fields_ = [
+        ("strides", ctypes.c_int32 * 2),
+        ("padding", ctypes.c_int32 * 4),
+        ("output_padding", ctypes.c_int32 * 2),
+        ("groups", ctypes.c_int32),
+        ("input_zero_point", ctypes.c_int32),
+        ("kernel_zero_point", ctypes.c_int32),
+        ("kernel_zero_points", ctypes.c_void_p),
+    ]
+
+
 class _clip(ctypes.Structure):
     _fields_ = [("a_min", ctypes.c_int64), ("a_max", ctypes.c_int64)]
 
@@ -223,6 +248,8 @@ class tk_node_attrs(ctypes.Union):
         ("qnn_binary", tk_qnn_binary_attrs),
         ("concat", tk_concat_attrs),
         ("transpose", tk_transpose_attrs),
+        ("leaky_relu", tk_leaky_relu_attrs),
+        ("conv2d_transpose", tk_conv2d_transpose_attrs),
         ("clip", _clip),
         ("bias_add", _bias_add),
     ]
@@ -261,6 +288,7 @@ NODE_KINDS = {
     "conv_block": 13, "dense_block": 14, "add_block": 15, "postops": 16,
     "ewise": 17, "conv2d_f32": 18, "dense_f32": 19, "nn.pad": 20,
     "qnn.quantize": 21, "qnn.dequantize": 22, "qnn_binary": 23, "qnn.concatenate": 24, "transpose": 25,
+    "qnn.leaky_relu": 26, "lookup": 27, "qnn.batch_matmul": 28, "qnn.conv2d_transpose": 29,
 }
 MAX_NODE_INPUTS = 8
 MAX_NODE_OUTPUTS = 6
@@ -314,6 +342,11 @@ SIGNATURES = {
     "tk_qnn_concatenate": (ctypes.c_int, [ctypes.POINTER(_PT), ctypes.c_int, _PT, ctypes.POINTER(tk_concat_attrs),
                                           _VP]),
     "tk_transpose": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_transpose_attrs), _VP]),
+    "tk_qnn_leaky_relu": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_leaky_relu_attrs), _VP]),
+    "tk_qnn_lookup": (ctypes.c_int, [_PT, _PT, _VP, _VP]),
+    "tk_qnn_batch_matmul_workspace_bytes": (_I64, [_PT, _PT]),
+    "tk_qnn_batch_matmul": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_dense_attrs), _VP, _VP]),
+    "tk_qnn_conv2d_transpose": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_conv2d_transpose_attrs), _VP]),
     "tk_find_scale_by_kl": (ctypes.c_int, [ctypes.POINTER(_I32), ctypes.POINTER(_F32), ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(_F32)]),
     "tk_module_create": (ctypes.c_int, [ctypes.POINTER(tk_node), ctypes.c_int, ctypes.POINTER(_VP)]),
@@ -328,6 +361,8 @@ SIGNATURES = {
     "tk_module_run_graph": (ctypes.c_int, [_VP, _VP, _VP, ctypes.POINTER(_VP)]),
     "tk_module_set_graph_copies": (ctypes.c_int, [_VP, ctypes.c_int]),
     "tk_module_set_trace_chunks": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "tk_module_set_copy_trace": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "tk_module_copy_trace": (ctypes.c_int, [_VP, ctypes.POINTER(_F64), ctypes.c_int]),
     "tk_module_tune": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
                                       ctypes.POINTER(_F32)]),
     "tk_module_set_node_algo": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int]),

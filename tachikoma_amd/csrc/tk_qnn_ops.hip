@@ -440,6 +440,167 @@ int transpose_impl(const tk_tensor* x, tk_tensor* y, const tk_transpose_attrs* a
   return TK_ERR_DTYPE;
 }
 
+// ---------------------------------------------------------------- qnn.leaky_relu
+// QnnLeakyReluCanonicalize (src/relay/qnn/op/leaky_relu.cc:85-140):
+//   data = int32(x);  q = RequantizeOrUpcast(data) at the output params
+//   out  = ConvertDtype(Where(Less(data, zp_in), FPM(q, alpha) + FPM(zp_out, 1 - alpha), q))
+// FPM = fixed_point_multiply -> tir.q_multiply_shift (intrin_rule.cc:197-250): the int32
+// power-of-two branch when the multiplier is 1 << 30, else the int64 QMultiplyShift form.
+__device__ __forceinline__ int32_t fpm_tir(int32_t x, int32_t m, int32_t s) {
+  return m == (1 << 30) ? qms_pow2(x, s) : qms_upward(x, m, s);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kQBlock) void leaky_relu_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n,
+                                                              RqParams rq, int32_t upcast, int32_t zp_in,
+                                                              int32_t zp_out, int32_t am, int32_t as, int32_t zm,
+                                                              int32_t zs) {
+  const int32_t scaled_z = fpm_tir(zp_out, zm, zs);  // FPM(zp_out, 1 - alpha): a constant
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    const int32_t d = (int32_t)x[i];
+    const int32_t q = upcast ? d : rq_apply(d, 0, rq);
+    const int32_t add = (int32_t)((uint32_t)fpm_tir(q, am, as) + (uint32_t)scaled_z);
+    int32_t o = d < zp_in ? add : q;
+    o = o < (int32_t)Lim<T>::lo ? (int32_t)Lim<T>::lo : o > (int32_t)Lim<T>::hi ? (int32_t)Lim<T>::hi : o;
+    y[i] = (T)o;
+  }
+}
+
+static bool pow2_shift_ok(int32_t m, int32_t s) { return !(m == (1 << 30) && s == 1); }
+
+int qnn_leaky_relu_impl(const tk_tensor* x, tk_tensor* y, const tk_leaky_relu_attrs* a, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y) && numel(x) == numel(y) && dt_of(x) == dt_of(y), "bad tensors");
+  TK_CHECK_ARG(is_int8ish(x), "qnn.leaky_relu: int8 or uint8 data expected");
+  TK_CHECK_ARG(a->upcast || !per_axis_mode(a->rq.mode), "qnn.leaky_relu: per-tensor requantize only");
+  // (q_multiply_shift's power-of-two branch with shift 1 needs a rounding factor 1 << -1, which
+  // the reference's compiler rejects: alpha == 0 or 1 does not build there either)
+  TK_CHECK_ARG(pow2_shift_ok(a->alpha_multiplier, a->alpha_shift) && pow2_shift_ok(a->zp_multiplier, a->zp_shift),
+               "qnn.leaky_relu: alpha 0 or 1 (fixed_point_multiply by 1.0) is not buildable in the reference");
+  const RqParams rq = rq_params(a->rq);
+  const int64_t n = numel(x);
+  auto go = [&](auto tag) -> int {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((leaky_relu_kernel<T>), dim3(qgrid(n)), dim3(kQBlock), 0, s, (const T*)ptr(x), (T*)ptr(y), n,
+                       rq, a->upcast, a->input_zero_point, a->output_zero_point, a->alpha_multiplier, a->alpha_shift,
+                       a->zp_multiplier, a->zp_shift);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  };
+  return is_int(x, 8) ? go((int8_t)0) : go((uint8_t)0);
+}
+
+// ---------------------------------------------------------------- qnn unary ops (table lookup)
+// take(table, reinterpret<uint8>(x), mode="fast") (python/tvm/relay/qnn/op/canonicalizations.py:
+// 157-160): 16 bytes per thread and step, the table in LDS.
+__global__ __launch_bounds__(kQBlock) void lookup_kernel(const uint8_t* __restrict__ x, uint8_t* __restrict__ y,
+                                                          int64_t n, const uint8_t* __restrict__ table) {
+  __shared__ uint8_t t[256];
+  t[threadIdx.x] = table[threadIdx.x];  // kQBlock == 256
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  const int64_t n16 = n / 16;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n16; i += stride) {
+    uint4 v = reinterpret_cast<const uint4*>(x)[i];
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = (uint32_t)t[w[k] & 0xFF] | ((uint32_t)t[(w[k] >> 8) & 0xFF] << 8) |
+             ((uint32_t)t[(w[k] >> 16) & 0xFF] << 16) | ((uint32_t)t[w[k] >> 24] << 24);
+    reinterpret_cast<uint4*>(y)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  for (int64_t i = n16 * 16 + blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) y[i] = t[x[i]];
+}
+
+int qnn_lookup_impl(const tk_tensor* x, tk_tensor* y, const void* table, hipStream_t s) {
+  static_assert(kQBlock == 256, "one table entry per thread");
+  TK_CHECK_ARG(x && y && table, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y) && numel(x) == numel(y) && is_int8ish(x) && is_int8ish(y), "bad tensors");
+  TK_CHECK_ARG(((uintptr_t)ptr(x) | (uintptr_t)ptr(y)) % 16 == 0, "qnn lookup: 16-byte aligned buffers expected");
+  const int64_t n = numel(x);
+  hipLaunchKernelGGL(lookup_kernel, dim3(qgrid((n + 15) / 16)), dim3(kQBlock), 0, s, (const uint8_t*)ptr(x),
+                     (uint8_t*)ptr(y), n, (const uint8_t*)table);
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
+// ---------------------------------------------------------------- qnn.conv2d_transpose
+// int16 operand shifts (legalizations.py:97-130) and nn.conv2d_transpose (topi conv2d_transpose_nchw,
+// python/tvm/topi/nn/conv2d_transpose.py:79-140: dilate by the stride, pad by k - 1 - pad (+ the
+// output padding), the kernel flipped): an output pixel (y, x) gathers input pixels iy with
+// y + pt - r = sh * iy for each kernel row r (likewise columns), products in int32, wrapping sums.
+// A direct gather kernel (one output element per thread): transpose convolutions are not on the
+// ResNet-50 trace path; the operands stay in L2 for these shapes.
+template <typename Ti, typename Tw>
+__global__ __launch_bounds__(kQBlock) void conv2d_transpose_kernel(
+    const Ti* __restrict__ x, const Tw* __restrict__ w, int32_t* __restrict__ y, int64_t n_out, int C, int H, int W,
+    int O, int OH, int OW, int KH, int KW, int sh, int sw, int pt, int pl, int groups, int32_t zx, int32_t zw,
+    const int32_t* __restrict__ zws) {
+  const int og = O / groups, cg = C / groups;
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n_out; i += stride) {
+    const int ox = (int)(i % OW);
+    const int oy = (int)((i / OW) % OH);
+    const int o = (int)((i / ((int64_t)OW * OH)) % O);
+    const int64_t nb = i / ((int64_t)OW * OH * O);
+    const int g = o / og, oo = o - g * og;
+    const int16_t kz = (int16_t)(zws ? zws[oo] : zw);
+    uint32_t acc = 0;
+    for (int c = g * cg; c < (g + 1) * cg; ++c) {
+      const Ti* xc = x + ((nb * C + c) * H) * (int64_t)W;
+      const Tw* wc = w + (((int64_t)c * og + oo) * KH) * KW;
+      for (int r = 0; r < KH; ++r) {
+        const int ty = oy + pt - r;
+        if (ty < 0 || ty % sh) continue;
+        const int iy = ty / sh;
+        if (iy >= H) continue;
+        for (int q = 0; q < KW; ++q) {
+          const int tx = ox + pl - q;
+          if (tx < 0 || tx % sw) continue;
+          const int ix = tx / sw;
+          if (ix >= W) continue;
+          const int16_t d = (int16_t)((int16_t)xc[(int64_t)iy * W + ix] - (int16_t)zx);
+          const int16_t k = (int16_t)((int16_t)wc[r * KW + q] - kz);
+          acc += (uint32_t)((int32_t)d * (int32_t)k);
+        }
+      }
+    }
+    y[i] = (int32_t)acc;
+  }
+}
+
+int qnn_conv2d_transpose_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, const tk_conv2d_transpose_attrs* a,
+                              hipStream_t s) {
+  TK_CHECK_ARG(x && w && y && a, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(w) && compact(y) && x->ndim == 4 && w->ndim == 4 && y->ndim == 4, "4-D tensors");
+  TK_CHECK_ARG(is_int8ish(x) && is_int8ish(w) && is_int(y, 32), "int8/uint8 operands, int32 output");
+  const int N = (int)x->shape[0], C = (int)x->shape[1], H = (int)x->shape[2], W = (int)x->shape[3];
+  const int og = (int)w->shape[1], KH = (int)w->shape[2], KW = (int)w->shape[3];
+  const int groups = a->groups;
+  TK_CHECK_ARG(groups >= 1 && C % groups == 0 && w->shape[0] == C, "weight (C, O/groups, KH, KW) for the data's C");
+  const int O = og * groups;
+  const int sh = a->strides[0], sw = a->strides[1];
+  TK_CHECK_ARG(sh >= 1 && sw >= 1 && a->output_padding[0] >= 0 && a->output_padding[0] < sh &&
+               a->output_padding[1] >= 0 && a->output_padding[1] < sw, "strides / output padding");
+  const int OH = (H - 1) * sh + KH - a->padding[0] - a->padding[2] + a->output_padding[0];
+  const int OW = (W - 1) * sw + KW - a->padding[1] - a->padding[3] + a->output_padding[1];
+  TK_CHECK_ARG(y->shape[0] == N && y->shape[1] == O && y->shape[2] == OH && y->shape[3] == OW,
+               "output shape (N, O, (H-1)*s + K - pads + output_padding, ...) expected");
+  const int64_t n = numel(y);
+  auto go = [&](auto tx, auto tw) -> int {
+    using Ti = decltype(tx);
+    using Tw = decltype(tw);
+    hipLaunchKernelGGL((conv2d_transpose_kernel<Ti, Tw>), dim3(qgrid(n)), dim3(kQBlock), 0, s, (const Ti*)ptr(x),
+                       (const Tw*)ptr(w), (int32_t*)ptr(y), n, C, H, W, O, OH, OW, KH, KW, sh, sw, a->padding[0],
+                       a->padding[1], groups, a->input_zero_point, a->kernel_zero_point, a->kernel_zero_points);
+    TK_LAUNCH_CHECK();
+    return TK_OK;
+  };
+  if (is_int(x, 8)) return is_int(w, 8) ? go((int8_t)0, (int8_t)0) : go((int8_t)0, (uint8_t)0);
+  return is_int(w, 8) ? go((uint8_t)0, (int8_t)0) : go((uint8_t)0, (uint8_t)0);
+}
+
 }  // namespace tk
 
 extern "C" {
@@ -460,6 +621,16 @@ int tk_qnn_concatenate(const tk_tensor* const* inputs, int n, tk_tensor* out, co
 }
 int tk_transpose(const tk_tensor* data, tk_tensor* out, const tk_transpose_attrs* attrs, void* stream) {
   return tk::transpose_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_leaky_relu(const tk_tensor* data, tk_tensor* out, const tk_leaky_relu_attrs* attrs, void* stream) {
+  return tk::qnn_leaky_relu_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_lookup(const tk_tensor* data, tk_tensor* out, const void* table, void* stream) {
+  return tk::qnn_lookup_impl(data, out, table, tk::as_stream(stream));
+}
+int tk_qnn_conv2d_transpose(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
+                            const tk_conv2d_transpose_attrs* attrs, void* stream) {
+  return tk::qnn_conv2d_transpose_impl(data, weight, out, attrs, tk::as_stream(stream));
 }
 
 }  // extern "C"

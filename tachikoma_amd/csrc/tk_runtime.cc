@@ -66,6 +66,52 @@ int qnn_concatenate_impl(const tk_tensor* const* xs, int n_in, tk_tensor* y, con
 int transpose_impl(const tk_tensor* x, tk_tensor* y, const tk_transpose_attrs* a, hipStream_t s);
 int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
                             int32_t* algos, int max_algos);
+int qnn_leaky_relu_impl(const tk_tensor* x, tk_tensor* y, const tk_leaky_relu_attrs* a, hipStream_t s);
+int qnn_lookup_impl(const tk_tensor* x, tk_tensor* y, const void* table, hipStream_t s);
+int qnn_conv2d_transpose_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, const tk_conv2d_transpose_attrs* a,
+                              hipStream_t s);
+
+// qnn.batch_matmul (src/relay/qnn/op/batch_matmul.cc:162-228): the qnn.dense kernel per batch entry,
+// on [M, K] / [N, K] / [M, N] views of x[b], y[b] (b or 0 where that operand's batch is 1), out[b];
+// one workspace serves every entry (the launches are stream-ordered).
+static bool bmm_check(const tk_tensor* x, const tk_tensor* y) {
+  return x && y && compact(x) && compact(y) && x->ndim == 3 && y->ndim == 3 && x->shape[2] == y->shape[2] &&
+         (x->shape[0] == y->shape[0] || x->shape[0] == 1 || y->shape[0] == 1);
+}
+struct View2 {
+  int64_t shape[2];
+  tk_tensor t;
+  View2(const tk_tensor* src, int64_t b) {
+    t = *src;
+    shape[0] = src->shape[1];
+    shape[1] = src->shape[2];
+    t.ndim = 2;
+    t.shape = shape;
+    t.strides = nullptr;
+    t.byte_offset = src->byte_offset + (uint64_t)(b * shape[0] * shape[1] * elem_bytes(src));
+  }
+};
+int64_t batch_matmul_workspace_bytes(const tk_tensor* x, const tk_tensor* y) {
+  if (!bmm_check(x, y)) {
+    set_error("qnn.batch_matmul: x [B, M, K], y [B', N, K] with B == B' or one of them 1");
+    return TK_ERR_INVALID_ARG;
+  }
+  View2 xv(x, 0), yv(y, 0);
+  return dense_workspace_bytes(&xv.t, &yv.t);
+}
+int batch_matmul_impl(const tk_tensor* x, const tk_tensor* y, tk_tensor* out, const tk_dense_attrs* a, void* ws,
+                      hipStream_t s) {
+  TK_CHECK_ARG(bmm_check(x, y) && out && a, "qnn.batch_matmul: x [B, M, K], y [B', N, K] (B == B' or one is 1)");
+  const int64_t B = std::max(x->shape[0], y->shape[0]);
+  TK_CHECK_ARG(compact(out) && out->ndim == 3 && out->shape[0] == B && out->shape[1] == x->shape[1] &&
+               out->shape[2] == y->shape[1] && is_int(out, 32), "qnn.batch_matmul: int32 [B, M, N] output");
+  for (int64_t b = 0; b < B; ++b) {
+    View2 xv(x, x->shape[0] == 1 ? 0 : b), yv(y, y->shape[0] == 1 ? 0 : b), ov(out, b);
+    const int rc = dense_impl(&xv.t, &yv.t, &ov.t, a, ws, s);
+    if (rc) return rc;
+  }
+  return TK_OK;
+}
 int conv2d_block_algo_info_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs, int algo,
                                 char* buf, int len);
 
@@ -166,6 +212,14 @@ static int run_node(Node& n, hipStream_t s) {
     }
     case TK_NODE_TRANSPOSE:
       return transpose_impl(i0, o, &d.attrs.transpose, s);
+    case TK_NODE_LEAKY_RELU:
+      return qnn_leaky_relu_impl(i0, o, &d.attrs.leaky_relu, s);
+    case TK_NODE_LOOKUP:
+      return qnn_lookup_impl(i0, o, d.ext[0], s);
+    case TK_NODE_BATCH_MATMUL:
+      return batch_matmul_impl(i0, i1, o, &d.attrs.dense, d.ext[0], s);
+    case TK_NODE_CONV2D_TRANSPOSE:
+      return qnn_conv2d_transpose_impl(i0, i1, o, &d.attrs.conv2d_transpose, s);
   }
   set_error("tk_module: unknown node kind " + std::to_string(d.kind));
   return TK_ERR_INVALID_ARG;
@@ -252,6 +306,12 @@ struct tk_module {
   bool graph_packed = true;
   int pack_chunks = 8;
   std::vector<std::unique_ptr<PackPlan>> packs;
+  // copy trace of packed runs (tk_module_set_copy_trace): a timing event on the compute stream
+  // before the run's first launch, and two per chunk on the capture stream around its copy
+  bool copy_trace = false;
+  hipEvent_t ct_t0 = nullptr;
+  std::vector<hipEvent_t> ct_ev;
+  std::vector<int64_t> ct_bytes;
   void drop_graph() {
     for (Graph& x : graphs) {
       if (x.ge) (void)hipGraphExecDestroy(x.ge);
@@ -268,6 +328,8 @@ struct tk_module {
     if (capture_done) (void)hipEventDestroy(capture_done);
     if (graph_join) (void)hipEventDestroy(graph_join);
     if (graph_pre) (void)hipEventDestroy(graph_pre);
+    if (ct_t0) (void)hipEventDestroy(ct_t0);
+    for (auto e : ct_ev) (void)hipEventDestroy(e);
     if (cap_s) (void)hipStreamDestroy(cap_s);
     if (cap_cs) (void)hipStreamDestroy(cap_cs);
     for (hipStream_t x : cap_cx)
@@ -388,6 +450,13 @@ int tk_conv2d_f32(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out
 }
 int tk_dense_f32(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out, void* stream) {
   return tk::dense_f32_impl(data, weight, out, tk::as_stream(stream));
+}
+int64_t tk_qnn_batch_matmul_workspace_bytes(const tk_tensor* x, const tk_tensor* y) {
+  return tk::batch_matmul_workspace_bytes(x, y);
+}
+int tk_qnn_batch_matmul(const tk_tensor* x, const tk_tensor* y, tk_tensor* out, const tk_dense_attrs* attrs,
+                        void* workspace, void* stream) {
+  return tk::batch_matmul_impl(x, y, out, attrs, workspace, tk::as_stream(stream));
 }
 int tk_digest_bytes(const void* data, int64_t nbytes, uint64_t* out_device, void* stream) {
   return tk::digest_impl(data, nbytes, out_device, tk::as_stream(stream));
@@ -745,14 +814,30 @@ static int run_packed(tk_module* mod, hipStream_t s, hipStream_t cs, void* const
   // the pack into mirror m waits for that mirror's last copies (two runs ago); the records the
   // kernels overwrite are only read by the packs of the previous launch on the same stream
   if (plan->mirror_used[m]) TK_HIP(hipStreamWaitEvent(s, plan->mirror_done[m], 0));
+  const bool trace = mod->copy_trace;
+  if (trace) {
+    if (!mod->ct_t0) TK_HIP(hipEventCreate(&mod->ct_t0));
+    while (mod->ct_ev.size() < 2 * plan->chunks.size()) {
+      hipEvent_t e;
+      TK_HIP(hipEventCreate(&e));
+      mod->ct_ev.push_back(e);
+    }
+    mod->ct_bytes.assign(plan->chunks.size(), 0);
+    TK_HIP(hipEventRecord(mod->ct_t0, s));
+  }
   for (size_t c = 0; c < plan->ge[m].size(); ++c) {
     TK_HIP(hipGraphLaunch(plan->ge[m][c], s));
     if (c >= plan->chunks.size()) break;  // the tail graph
     const PackPlan::Chunk& ch = plan->chunks[c];
     TK_HIP(hipEventRecord(plan->ev[m][c], s));
     TK_HIP(hipStreamWaitEvent(cs, plan->ev[m][c], 0));
+    if (trace) TK_HIP(hipEventRecord(mod->ct_ev[2 * c], cs));
     TK_HIP(hipMemcpyAsync(plan->host_lo + ch.off, (char*)plan->mirror[m] + ch.off, (size_t)ch.len,
                           hipMemcpyDeviceToHost, cs));
+    if (trace) {
+      TK_HIP(hipEventRecord(mod->ct_ev[2 * c + 1], cs));
+      mod->ct_bytes[c] = ch.len;
+    }
   }
   TK_HIP(hipEventRecord(plan->mirror_done[m], cs));
   plan->mirror_used[m] = true;
@@ -760,6 +845,34 @@ static int run_packed(tk_module* mod, hipStream_t s, hipStream_t cs, void* const
   mod->capture_recorded = true;
   mod->capture_plain = false;
   return TK_OK;
+}
+
+int tk_module_set_copy_trace(tk_module* mod, int enable) {
+  if (!mod) {
+    tk::set_error("tk_module_set_copy_trace: null module");
+    return TK_ERR_INVALID_ARG;
+  }
+  mod->copy_trace = enable != 0;
+  mod->ct_bytes.clear();
+  return TK_OK;
+}
+
+int tk_module_copy_trace(tk_module* mod, double* out, int max_chunks) {
+  if (!mod || (max_chunks > 0 && !out)) {
+    tk::set_error("tk_module_copy_trace: invalid argument");
+    return TK_ERR_INVALID_ARG;
+  }
+  const int n = (int)mod->ct_bytes.size();
+  for (int c = 0; c < n && c < max_chunks; ++c) {
+    float a = 0.f, b = 0.f;
+    TK_HIP(hipEventSynchronize(mod->ct_ev[2 * c + 1]));
+    TK_HIP(hipEventElapsedTime(&a, mod->ct_t0, mod->ct_ev[2 * c]));
+    TK_HIP(hipEventElapsedTime(&b, mod->ct_t0, mod->ct_ev[2 * c + 1]));
+    out[3 * c] = (double)mod->ct_bytes[c];
+    out[3 * c + 1] = a;
+    out[3 * c + 2] = b;
+  }
+  return n;
 }
 
 int tk_module_run_graph(tk_module* mod, void* stream, void* capture_stream, void* const* host_dst) {

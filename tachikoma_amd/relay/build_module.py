@@ -24,6 +24,7 @@ import numpy as np
 from .. import _lib
 from .expr import Call, Constant, Expr, Function, IRModule, Tuple, Var, post_order
 from .op import INT_DTYPES
+from .qnn import op as _qnn
 
 TARGETS = ("mi355x", "rocm", "hip", "gfx950")
 
@@ -135,6 +136,15 @@ def requantize_plan(input_scale: np.ndarray, output_scale, rounding: str):
     _lib.check(lib.tk_requantize_prepare(arr, n, ctypes.c_float(float(np.float32(output_scale))), rnd, ms, ss,
                                          ctypes.byref(mode)), "tk_requantize_prepare")
     return int(mode.value), np.array(ms[:cap], dtype=np.int32), np.array(ss[:cap], dtype=np.int32)
+
+
+def fixed_point_multiplier_shift(v: float) -> Tuple[int, int]:
+    """GetFixedPointMultiplierShift (src/relay/qnn/utils.cc:33-57) of a double, through the
+    library's host port (tk_fixed_point_multiplier_shift)."""
+    m, s = ctypes.c_int32(), ctypes.c_int32()
+    _lib.check(_lib.load().tk_fixed_point_multiplier_shift(ctypes.c_double(float(v)), ctypes.byref(m), ctypes.byref(s)),
+               "tk_fixed_point_multiplier_shift")
+    return int(m.value), int(s.value)
 
 
 def _clip_bound(v: float, dtype: str) -> int:
@@ -397,6 +407,55 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
         else:
             a["zero_point"] = 0
             consts["zero_points"] = zv.reshape(-1)
+    elif op == "qnn.leaky_relu":
+        # QnnLeakyReluCanonicalize (leaky_relu.cc:85-140): RequantizeOrUpcast to the output params,
+        # then the alpha / (1 - alpha) fixed-point multiplies
+        ins = _tensor_args(call, 1, names)
+        s_in, z_in, s_out, z_out = (_scalar(call.args[i], "qnn.leaky_relu param") for i in range(1, 5))
+        rounding = _qnn_rounding(a)
+        up = _is_equal_scalar(s_in, s_out) and _is_equal_scalar(z_in, z_out)
+        mode, ms, ss = requantize_plan(np.float32(s_in), np.float32(s_out), rounding)
+        a.update(rounding=rounding, upcast=int(up), mode=mode, multiplier=int(ms[0]), shift=int(ss[0]),
+                 input_zero_point=int(z_in), output_zero_point=int(z_out), input_scale=float(np.float32(s_in)),
+                 output_scale=float(np.float32(s_out)))
+        am, as_ = fixed_point_multiplier_shift(a["alpha"])
+        zm, zs = fixed_point_multiplier_shift(1.0 - a["alpha"])
+        if (am, as_) == (1 << 30, 1) or (zm, zs) == (1 << 30, 1):
+            # q_multiply_shift's power-of-two branch needs 1 << -1 there (intrin_rule.cc:231): the
+            # reference's compiler rejects the shift amount, so the graph does not build
+            raise UnsupportedError(f"qnn.leaky_relu: alpha={a['alpha']} (a fixed_point_multiply by 1.0) does not "
+                                   "build in the reference")
+        a.update(alpha_multiplier=am, alpha_shift=as_, zp_multiplier=zm, zp_shift=zs)
+    elif op in _qnn.UNARY_OPS:
+        # legalized to a 256-entry table lookup (legalizations.py:54-86); the device module builds
+        # the table (relay/qnn/legalize.py)
+        ins = _tensor_args(call, 1, names)
+        s_in, z_in, s_out, z_out = (_scalar(call.args[i], f"{op} param") for i in range(1, 5))
+        a.update(in_scale=float(np.float32(s_in)), in_zero_point=int(z_in), out_scale=float(np.float32(s_out)),
+                 out_zero_point=int(z_out))
+    elif op == "qnn.batch_matmul":
+        ins = _tensor_args(call, 2, names)
+        a.update(input_zero_point=int(_scalar(call.args[2], "qnn.batch_matmul x_zero_point")),
+                 kernel_zero_point=int(_scalar(call.args[3], "qnn.batch_matmul y_zero_point")),
+                 x_scale=float(np.float32(_scalar(call.args[4], "scale"))),
+                 y_scale=float(np.float32(_scalar(call.args[5], "scale"))))
+    elif op == "qnn.conv2d_transpose":
+        ins = _tensor_args(call, 2, names)
+        za = np.asarray(_scalar(call.args[2], "qnn.conv2d_transpose input_zero_point"))
+        zw = np.asarray(_scalar(call.args[3], "qnn.conv2d_transpose kernel_zero_point"))
+        a["input_zero_point"] = int(za.reshape(-1)[0])  # scalar or one element (QnnConv2DTransposeRel)
+        if zw.ndim == 0 or zw.size == 1:
+            a["kernel_zero_point"] = int(zw.reshape(-1)[0])
+        else:
+            # bias_add(int16(w), -int16(zp)) on the weight's axis 1 (legalizations.py:124-127): the
+            # per-group output channel of an IOHW weight
+            if a["kernel_layout"] != "IOHW" or zw.size != call.args[1].shape[1]:
+                raise UnsupportedError("qnn.conv2d_transpose: a vector kernel zero point needs an IOHW kernel, one "
+                                       "entry per output channel of a group")
+            a["kernel_zero_point"] = 0
+            consts["kernel_zero_points"] = zw.reshape(-1).astype(np.int32)
+        a["input_scale"] = np.asarray(_scalar(call.args[4], "scale")).tolist()
+        a["kernel_scale"] = np.asarray(_scalar(call.args[5], "scale")).tolist()
     elif op == "transpose":
         ins = _tensor_args(call, 1, names)
         if len(call.shape) > 6:

@@ -27,6 +27,8 @@ import numpy as np
 
 from .. import _lib
 from .build_module import ExecGroup, Plan, PlanOp, exec_groups
+from .qnn import legalize as _legalize
+from .qnn import op as _qnn
 
 
 def _torch():
@@ -87,6 +89,7 @@ class DeviceModule:
         self._derived: Dict[str, List[Callable[[int], None]]] = {}
         self.groups = exec_groups(plan, fuse=fuse)
         self.tuning: List[dict] = []
+        self.tables: Dict[str, object] = {}  # qnn unary ops: op name -> its device lookup table
         # runs as one replayed HIP graph (tk_module_run_graph) instead of host-issued nodes and
         # copies; GraphModule.pick_run_mode chooses by timing both on this host
         self.use_graph = False
@@ -120,6 +123,9 @@ class DeviceModule:
         torch = _torch()
         self.layout: Dict[str, Dict[str, object]] = {}
         for op in self.plan.ops:
+            if op.op == "qnn.conv2d_transpose":
+                self._alloc_transpose_layout(op)
+                continue
             if op.op != "qnn.conv2d":
                 continue
             dl, kl = op.attrs.get("data_layout", "NCHW"), op.attrs.get("kernel_layout", "OIHW")
@@ -146,6 +152,30 @@ class DeviceModule:
                 self.buffers[L["w"]] = torch.empty(tuple(wt.shape[k] for k in perm), dtype=torch_dtype(wt.dtype),
                                                    device=self.device)
                 self._register_transpose(op.inputs[1], L["w"], perm)
+            self.layout[op.name] = L
+
+    def _alloc_transpose_layout(self, op: PlanOp) -> None:
+        """qnn.conv2d_transpose runs on NCHW data and an IOHW weight: NHWC data goes through
+        "<op>:nchw_in" / "<op>:nchw_out" and any other kernel layout through "<op>:iohw_w"."""
+        torch = _torch()
+        dl, kl = op.attrs["data_layout"], op.attrs["kernel_layout"]
+        L: Dict[str, object] = {"x": op.inputs[0], "w": op.inputs[1], "y": op.name}
+        if dl == "NHWC":
+            xt = self.plan.tensor(op.inputs[0])
+            n_, h_, w_, c_ = xt.shape
+            L["x"] = f"{op.name}:nchw_in"
+            self.buffers[L["x"]] = torch.empty((n_, c_, h_, w_), dtype=torch_dtype(xt.dtype), device=self.device)
+            n_, oh, ow, o_ = op.out.shape
+            L["y"] = f"{op.name}:nchw_out"
+            self.buffers[L["y"]] = torch.empty((n_, o_, oh, ow), dtype=torch.int32, device=self.device)
+        if kl != "IOHW":
+            wt = self.plan.tensor(op.inputs[1])
+            perm = tuple(kl.index(ch) for ch in "IOHW")
+            L["w"] = f"{op.name}:iohw_w"
+            self.buffers[L["w"]] = torch.empty(tuple(wt.shape[k] for k in perm), dtype=torch_dtype(wt.dtype),
+                                               device=self.device)
+            self._register_transpose(op.inputs[1], L["w"], perm)
+        if dl != "NCHW" or kl != "IOHW":
             self.layout[op.name] = L
 
     def _transpose_attrs(self, perm):
@@ -331,6 +361,9 @@ class DeviceModule:
                 if kind == "qnn.conv2d" and op.name in self.layout:
                     self._emit_layout_conv(n, op, mfma[op.name], shadow_bufs, ensure_shadow, stream, emit)
                     continue
+                if kind == "qnn.conv2d_transpose":
+                    self._emit_conv2d_transpose(n, op, emit)
+                    continue
                 if kind == "qnn.conv2d":
                     n.kind = _lib.NODE_KINDS["qnn.conv2d"]
                     self._conv_attrs(n.attrs.conv2d, op)
@@ -374,6 +407,30 @@ class DeviceModule:
                 elif kind == "transpose":
                     n.kind = _lib.NODE_KINDS["transpose"]
                     n.attrs.transpose = self._transpose_attrs(a["axes"])
+                elif kind == "qnn.leaky_relu":
+                    n.kind = _lib.NODE_KINDS[kind]
+                    la = n.attrs.leaky_relu
+                    r = la.rq
+                    r.mode, r.axis, r.multiplier, r.shift = a["mode"], -1, a["multiplier"], a["shift"]
+                    r.input_zero_point, r.output_zero_point = a["input_zero_point"], a["output_zero_point"]
+                    la.upcast = a["upcast"]
+                    la.input_zero_point, la.output_zero_point = a["input_zero_point"], a["output_zero_point"]
+                    la.alpha_multiplier, la.alpha_shift = a["alpha_multiplier"], a["alpha_shift"]
+                    la.zp_multiplier, la.zp_shift = a["zp_multiplier"], a["zp_shift"]
+                elif kind in _qnn.UNARY_OPS:
+                    n.kind = _lib.NODE_KINDS["lookup"]
+                    table = _legalize.build_table(self.lib, kind, op.out.dtype, a["in_scale"], a["in_zero_point"],
+                                                  a["out_scale"], a["out_zero_point"], self.device, stream)
+                    self._keep.append(table)
+                    self.tables[op.name] = table
+                    n.ext[0] = table.data_ptr()
+                elif kind == "qnn.batch_matmul":
+                    n.kind = _lib.NODE_KINDS[kind]
+                    self._dense_attrs(n.attrs.dense, op)
+                    ws = self.lib.tk_qnn_batch_matmul_workspace_bytes(ins[0].ptr, ins[1].ptr)
+                    if ws < 0:
+                        _lib.check(int(ws), f"{op.name} qnn.batch_matmul workspace")
+                    n.ext[0] = self._scratch(ws).data_ptr()
                 elif kind == "nn.bias_add":
                     n.kind = _lib.NODE_KINDS["nn.bias_add"]
                     n.attrs.bias_add.axis = a["axis"]
@@ -497,6 +554,39 @@ class DeviceModule:
         n.inputs[0], n.inputs[1] = ins[0].ptr, ins[1].ptr
         n.outputs[0] = self._ref(L["y"]).ptr
         emit(n, "qnn.conv2d", [] if L["y"] != op.name else [op.name])
+        if L["y"] != op.name:
+            transpose_node(L["y"], op.name, self._TO_NHWC, [op.name])
+
+    def _emit_conv2d_transpose(self, n, op: PlanOp, emit) -> None:
+        """qnn.conv2d_transpose: [transpose NHWC data -> NCHW], the NCHW / IOHW kernel, [transpose ->
+        the NHWC record]; a non-IOHW weight was transposed into "<op>:iohw_w" (re-derived on rewrite)."""
+        L = self.layout.get(op.name, {"x": op.inputs[0], "w": op.inputs[1], "y": op.name})
+        a = op.attrs
+
+        def transpose_node(src: str, dst: str, perm, records):
+            t = _lib.tk_node()
+            t.kind = _lib.NODE_KINDS["transpose"]
+            t.attrs.transpose = self._transpose_attrs(perm)
+            t.n_inputs, t.n_outputs = 1, 1
+            t.inputs[0], t.outputs[0] = self._ref(src).ptr, self._ref(dst).ptr
+            emit(t, "transpose", records)
+
+        if L["x"] != op.inputs[0]:
+            transpose_node(op.inputs[0], L["x"], self._TO_NCHW, [])
+        n.kind = _lib.NODE_KINDS["qnn.conv2d_transpose"]
+        ta = n.attrs.conv2d_transpose
+        ta.strides[:] = list(a["strides"])
+        ta.padding[:] = list(a["padding"])
+        ta.output_padding[:] = list(a["output_padding"])
+        ta.groups = a["groups"]
+        ta.input_zero_point = a["input_zero_point"]
+        ta.kernel_zero_point = a["kernel_zero_point"]
+        if "kernel_zero_points" in op.consts:
+            ta.kernel_zero_points = self._dev_i32(op.consts["kernel_zero_points"]).data_ptr()
+        n.n_inputs, n.n_outputs = 2, 1
+        n.inputs[0], n.inputs[1] = self._ref(L["x"]).ptr, self._ref(L["w"]).ptr
+        n.outputs[0] = self._ref(L["y"]).ptr
+        emit(n, "qnn.conv2d_transpose", [] if L["y"] != op.name else [op.name])
         if L["y"] != op.name:
             transpose_node(L["y"], op.name, self._TO_NHWC, [op.name])
 
@@ -779,8 +869,9 @@ class DeviceModule:
     def tuning_table(self) -> dict:
         """The find step's choice per conv-block node, keyed by the node's records (stable across
         processes for one plan), with the library it was measured with."""
-        return {"format": "tachikoma-tune-table", "version": 1, "library": _lib.build_info(),
-                "entries": [{"records": t["records"], "algo": t["algo"], "us": t["us"]} for t in self.tuning]}
+        return {"format": "tachikoma-tune-table", "version": 2, "library": _lib.build_info(),
+                "entries": [{"records": t["records"], "algo": t["algo"], "us": t["us"],
+                             "kernel": t.get("kernel") or self.algo_info(t["node"], t["algo"])} for t in self.tuning]}
 
     def apply_tuning(self, table) -> List[dict]:
         """Replays a tune table (``tuning_table()``, or a JSON file of one) with tk_module_set_node_algo;
@@ -793,6 +884,7 @@ class DeviceModule:
         if table.get("format") != "tachikoma-tune-table":
             raise _lib.TachikomaError("not a tachikoma tune table")
         by_records = {tuple(e["records"]): e for e in table["entries"]}
+        same_lib = table.get("library") == _lib.build_info()
         applied = []
         for i, (kind, recs) in enumerate(zip(self.node_kinds, self.node_records)):
             if self._node_kind(i) != _lib.NODE_KINDS["conv_block"]:  # dense blocks run as 1x1 conv blocks
@@ -800,12 +892,34 @@ class DeviceModule:
             e = by_records.get(tuple(recs))
             if e is None:
                 raise _lib.TachikomaError(f"tune table has no entry for the conv block writing {recs}")
-            _lib.check(self.lib.tk_module_set_node_algo(self.handle, i, int(e["algo"])), "tk_module_set_node_algo")
-            applied.append({"node": i, "records": list(recs), "algo": int(e["algo"]), "us": e.get("us"),
-                            "kernel": self.algo_info(i, int(e["algo"])), "candidates": []})
+            # algo numbers are plan indices that move when the planner changes: a table from another
+            # library is replayed by kernel description (version 2 tables), never by number
+            algo = int(e["algo"])
+            if e.get("kernel"):
+                if not (same_lib and self.algo_info(i, algo) == e["kernel"]):
+                    match = [a for a in self.node_algos(i) if self.algo_info(i, a) == e["kernel"]]
+                    if not match:
+                        raise _lib.TachikomaError(f"tune table: no kernel '{e['kernel']}' for the conv block "
+                                                  f"writing {recs} in this library")
+                    algo = match[0]
+            elif not same_lib:
+                raise _lib.TachikomaError(f"tune table from library {table.get('library')} (this is "
+                                          f"{_lib.build_info()}) has no kernel descriptions: algo numbers would "
+                                          f"select other kernels")
+            _lib.check(self.lib.tk_module_set_node_algo(self.handle, i, algo), "tk_module_set_node_algo")
+            applied.append({"node": i, "records": list(recs), "algo": algo, "us": e.get("us"),
+                            "kernel": self.algo_info(i, algo), "candidates": []})
         self.tuning = applied
         self.tune_table_digest = tune_table_digest(applied)
         return applied
+
+    def node_algos(self, node: int) -> List[int]:
+        """tk_conv2d_block_algos: every kernel (algo) conv-block node `node` can run on."""
+        n = self._nodes[node]
+        buf = (ctypes.c_int32 * 512)()
+        cnt = self.lib.tk_conv2d_block_algos(n.inputs[0], n.inputs[1], ctypes.byref(n.attrs.block), buf, 512)
+        _lib.check(min(cnt, 0), "tk_conv2d_block_algos")
+        return list(buf[:min(cnt, 512)])
 
     def algo_info(self, node: int, algo: int) -> str:
         """tk_conv2d_block_algo_info: what kernel `algo` is on conv-block node `node`."""

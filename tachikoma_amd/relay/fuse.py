@@ -52,6 +52,10 @@ _PATTERNS = {
     # cast; cast / subtract / multiply; requantizes + subtract / multiply; requantizes + concatenate)
     "qnn.quantize": kBroadcast, "qnn.dequantize": kBroadcast, "qnn.subtract": kBroadcast, "qnn.mul": kBroadcast,
     "qnn.concatenate": kInjective, "transpose": kInjective,
+    # round 5: leaky_relu canonicalizes to requantize / fixed_point_multiply / add / where (broadcast),
+    # the unary ops to take (injective), batch_matmul / conv2d_transpose to their nn ops
+    "qnn.leaky_relu": kBroadcast, "qnn.batch_matmul": kOutEWiseFusable, "qnn.conv2d_transpose": kOutEWiseFusable,
+    **{f"qnn.{u}": kInjective for u in ("sqrt", "rsqrt", "exp", "erf", "sigmoid", "hardswish", "tanh", "log", "abs")},
     "annotation.stop_fusion": kOpaque, "annotation.cast_hint": kOpaque,
     "tachikoma.qnn.conv2d": kOpaque, "tachikoma.qnn.dense": kOpaque,  # external (BYOC) functions
 }

@@ -167,7 +167,13 @@ def _call(op: str, args: List[Expr], attrs: Dict[str, Any]) -> Expr:
             return _qnn.dense(*args, **a)
         if op == "qnn.requantize":
             return _qnn.requantize(*args, **a)
-        if op in ("qnn.add", "qnn.subtract", "qnn.mul", "qnn.concatenate", "qnn.quantize", "qnn.dequantize"):
+        if op in ("qnn.add", "qnn.subtract", "qnn.mul", "qnn.concatenate", "qnn.quantize", "qnn.dequantize",
+                  "qnn.leaky_relu", "qnn.batch_matmul", "qnn.conv2d_transpose") or op in _qnn.UNARY_OPS:
+            if op == "qnn.batch_matmul":
+                a.pop("transpose_a", None)
+                a.pop("transpose_b", None)
+            if op == "qnn.leaky_relu":  # alpha is an attribute, the constructor's second argument
+                return _qnn.leaky_relu(args[0], a.pop("alpha"), *args[1:], **a)
             return getattr(_qnn, op.split(".")[1])(*args, **a)
         if op == "transpose":
             return _op.transpose(*args, **a)
@@ -328,6 +334,9 @@ class _Parser:
         if t[0] == "string":
             return json.loads(t[1])
         if t[0] == "number":
+            m = _NUM_SUFFIX.match(t[1])
+            if m.group("s") is None and any(c in m.group("v") for c in ".eE"):
+                return float(m.group("v"))  # a double attribute (e.g. qnn.leaky_relu's alpha), not float32
             v = _number(t[1])
             return v.item()
         if t[1] in ("True", "False"):
@@ -362,14 +371,19 @@ class _Parser:
                 raise ParseError(f"{name} is a tuple (nn.batch_norm): use a field, e.g. {name}.0")
             return v
         if t[1] == "(":
-            # a tuple literal: qnn.concatenate's tensors, scales and zero points
+            # a tuple literal -- qnn.concatenate's tensors, scales and zero points: `()`, `(a,)` or
+            # two or more fields -- or a parenthesised expression `(a)` (grouping, not a 1-tuple)
             self.next()
             fields = []
+            comma = False
             while self.peek()[1] != ")":
                 fields.append(self.parse_expr())
                 if self.peek()[1] == ",":
                     self.next()
+                    comma = True
             self.next()
+            if len(fields) == 1 and not comma:
+                return fields[0]
             return Tuple(fields)
         if t[0] == "number":
             self.next()

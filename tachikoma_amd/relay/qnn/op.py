@@ -256,3 +256,152 @@ def dequantize(data: Expr, input_scale, input_zero_point, axis: int = -1) -> Cal
     _axis_param(s, data.shape, axis, "qnn.dequantize")
     _axis_param(z, data.shape, axis, "qnn.dequantize")
     return Call("qnn.dequantize", [data, s, z], {"axis": int(axis)}, TensorType(data.shape, "float32"))
+
+
+def _scalar_param(p: Expr, what: str) -> None:
+    shp = p.checked_type.shape
+    if shp != () and int(np.prod(shp)) != 1:
+        raise TypeError(f"{what}: scale / zero point must be a scalar (or one element), got shape {shp}")
+
+
+def leaky_relu(x: Expr, alpha: float, input_scale, input_zero_point, output_scale, output_zero_point) -> Call:
+    """``qnn.leaky_relu`` (src/relay/qnn/op/leaky_relu.cc:33-77): int8 / uint8 data, scalar params,
+    the output in the input's dtype."""
+    if x.dtype not in ("int8", "uint8"):
+        raise TypeError(f"qnn.leaky_relu: int8 or uint8 data expected, got {x.dtype}")
+    args = [x, _c(input_scale, "float32"), _c(input_zero_point, "int32"), _c(output_scale, "float32"),
+            _c(output_zero_point, "int32")]
+    for p in args[1:]:
+        if p.checked_type.shape != ():
+            raise TypeError("qnn.leaky_relu: scales and zero points must be scalars")
+    cfg = current_requantize_config()
+    attrs = {"alpha": float(alpha), "cfg_rounding": cfg["rounding"], "cfg_compute_dtype": cfg["compute_dtype"]}
+    return Call("qnn.leaky_relu", args, attrs, TensorType(x.shape, x.dtype))
+
+
+# the unary ops of src/relay/qnn/op/unary_elementwise_op.cc:31-56 (QNN_CREATE_UNARY_ELEMENTWISE_OP);
+# each is legalized to a 256-entry table lookup (python/tvm/relay/qnn/op/legalizations.py:54-86)
+UNARY_OPS = ("qnn.sqrt", "qnn.rsqrt", "qnn.exp", "qnn.erf", "qnn.sigmoid", "qnn.hardswish", "qnn.tanh", "qnn.log",
+             "qnn.abs")
+
+
+def _unary(name: str, x: Expr, scale, zero_point, output_scale, output_zero_point) -> Call:
+    """QnnUnaryElementwiseRel: int8 / uint8 data, scalar params, same dtype out."""
+    if x.dtype not in ("int8", "uint8"):
+        raise TypeError(f"{name}: int8 or uint8 data expected, got {x.dtype}")
+    args = [x, _c(scale, "float32"), _c(zero_point, "int32"), _c(output_scale, "float32"),
+            _c(output_zero_point, "int32")]
+    for p in args[1:]:
+        if p.checked_type.shape != ():
+            raise TypeError(f"{name}: scales and zero points must be scalars")
+    return Call(name, args, {}, TensorType(x.shape, x.dtype))
+
+
+def sqrt(x, scale, zero_point, output_scale, output_zero_point) -> Call:
+    return _unary("qnn.sqrt", x, scale, zero_point, output_scale, output_zero_point)
+
+
+def rsqrt(x, scale, zero_point, output_scale, output_zero_point) -> Call:
+    return _unary("qnn.rsqrt", x, scale, zero_point, output_scale, output_zero_point)
+
+
+def exp(x, scale, zero_point, output_scale, output_zero_point) -> Call:
+    return _unary("qnn.exp", x, scale, zero_point, output_scale, output_zero_point)
+
+
+def erf(x, scale, zero_point, output_scale, output_zero_point) -> Call:
+    return _unary("qnn.erf", x, scale, zero_point, output_scale, output_zero_point)
+
+
+def sigmoid(x, scale, zero_point, output_scale, output_zero_point) -> Call:
+    return _unary("qnn.sigmoid", x, scale, zero_point, output_scale, output_zero_point)
+
+
+def hardswish(x, scale, zero_point, output_scale, output_zero_point) -> Call:
+    return _unary("qnn.hardswish", x, scale, zero_point, output_scale, output_zero_point)
+
+
+def tanh(x, scale, zero_point, output_scale, output_zero_point) -> Call:
+    return _unary("qnn.tanh", x, scale, zero_point, output_scale, output_zero_point)
+
+
+def log(x, scale, zero_point, output_scale, output_zero_point) -> Call:
+    return _unary("qnn.log", x, scale, zero_point, output_scale, output_zero_point)
+
+
+def abs(x, scale, zero_point, output_scale, output_zero_point) -> Call:  # noqa: A001 (the reference's name)
+    return _unary("qnn.abs", x, scale, zero_point, output_scale, output_zero_point)
+
+
+def batch_matmul(x: Expr, y: Expr, x_zero_point, y_zero_point, x_scale, y_scale, out_dtype="int32") -> Call:
+    """``qnn.batch_matmul`` (src/relay/qnn/op/batch_matmul.cc:40-97): [B, M, K] x [B', N, K] (transpose_b,
+    B == B' or one of them 1) -> int32 [max(B, B'), M, N]; scalar zero points and scales."""
+    if str(np.dtype(out_dtype)) != "int32":
+        raise TypeError("qnn.batch_matmul: out_dtype must be int32 (QnnBatchMatmulRel)")
+    for e in (x, y):
+        if e.dtype not in ("int8", "uint8"):
+            raise TypeError(f"qnn.batch_matmul: int8 or uint8 operands expected, got {e.dtype}")
+        if len(e.shape) != 3:
+            raise TypeError(f"qnn.batch_matmul: rank-3 operands expected, got {e.shape}")
+    (bx, m, k), (by, n, k2) = x.shape, y.shape
+    if k != k2 or not (bx == by or bx == 1 or by == 1):
+        raise TypeError(f"qnn.batch_matmul: {x.shape} x {y.shape}^T")
+    args = [x, y, _c(x_zero_point, "int32"), _c(y_zero_point, "int32"), _c(x_scale, "float32"),
+            _c(y_scale, "float32")]
+    for p in args[2:]:
+        if p.checked_type.shape != ():
+            raise TypeError("qnn.batch_matmul: zero points and scales must be scalars")
+    return Call("qnn.batch_matmul", args, {"transpose_a": False, "transpose_b": True, "out_dtype": "int32"},
+                TensorType((max(bx, by), m, n), "int32"))
+
+
+TRANSPOSE_KERNEL_LAYOUTS = ("IOHW", "OIHW", "HWOI", "HWIO", "OHWI")
+
+
+def conv2d_transpose(data: Expr, weight: Expr, input_zero_point, kernel_zero_point, input_scale, kernel_scale,
+                     strides=(1, 1), padding=(0, 0), dilation=(1, 1), groups: int = 1, channels=None,
+                     kernel_size=None, data_layout="NCHW", kernel_layout="IOHW", out_layout="",
+                     output_padding=(0, 0), out_dtype="int32") -> Call:
+    """``qnn.conv2d_transpose`` (src/relay/qnn/op/convolution_transpose.cc:42-150; Conv2DTransposeRel):
+    NCHW / NHWC data; the kernel's 'I' axis is the data's channels, 'O' the output channels per group;
+    output in the data layout, (H - 1) * stride + KH - pad_top - pad_bottom + output_padding rows."""
+    if data_layout not in ("NCHW", "NHWC") or kernel_layout not in TRANSPOSE_KERNEL_LAYOUTS:
+        raise NotImplementedError(f"qnn.conv2d_transpose: data layout {data_layout} / kernel layout {kernel_layout}")
+    if out_layout not in ("", data_layout):
+        raise NotImplementedError("qnn.conv2d_transpose: out_layout must be the data layout")
+    if str(np.dtype(out_dtype)) != "int32":
+        raise NotImplementedError("qnn.conv2d_transpose: out_dtype int32 (int16 is not implemented)")
+    for e in (data, weight):
+        if e.dtype not in ("int8", "uint8"):
+            raise TypeError(f"qnn.conv2d_transpose: int8 or uint8 operands expected, got {e.dtype}")
+    if tuple(_tuple2(dilation)) != (1, 1):
+        raise NotImplementedError("qnn.conv2d_transpose: dilation must be 1 (topi conv2d_transpose_nchw)")
+    if data_layout == "NCHW":
+        n, c, h, w = data.shape
+    else:
+        n, h, w, c = data.shape
+    ks = dict(zip(kernel_layout, weight.shape))
+    ci, og, kh, kw = ks["I"], ks["O"], ks["H"], ks["W"]
+    if ci != c or c % groups:
+        raise TypeError(f"qnn.conv2d_transpose: kernel {weight.shape} ({kernel_layout}) for {c} channels, "
+                        f"groups={groups}")
+    if kernel_size is not None and tuple(_tuple2(kernel_size)) != (kh, kw):
+        raise TypeError("qnn.conv2d_transpose: kernel_size does not match the kernel shape")
+    sh, sw = _tuple2(strides)
+    pt, pl, pb, pr = get_pad_tuple2d(padding)
+    oph, opw = _tuple2(output_padding)
+    if oph >= sh or opw >= sw:
+        raise TypeError("qnn.conv2d_transpose: output_padding must be smaller than the stride")
+    oh = (h - 1) * sh + kh - pt - pb + oph
+    ow = (w - 1) * sw + kw - pl - pr + opw
+    o = og * groups
+    args = [data, weight, _c(input_zero_point, "int32"), _c(kernel_zero_point, "int32"), _c(input_scale, "float32"),
+            _c(kernel_scale, "float32")]
+    _scalar_param(args[2], "qnn.conv2d_transpose input_zero_point")
+    _scalar_param(args[4], "qnn.conv2d_transpose input_scale")
+    attrs = {"strides": (sh, sw), "padding": (pt, pl, pb, pr), "dilation": (1, 1), "groups": int(groups),
+             "channels": int(channels) if channels is not None else o, "kernel_size": (kh, kw),
+             "data_layout": data_layout, "kernel_layout": kernel_layout, "output_padding": (oph, opw),
+             "out_dtype": "int32"}
+    shape = (n, o, oh, ow) if data_layout == "NCHW" else (n, oh, ow, o)
+    return Call("qnn.conv2d_transpose", args, attrs, TensorType(shape, "int32"))

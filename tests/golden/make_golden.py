@@ -24,6 +24,9 @@ DEQUANT = "tests/python/relay/test_op_qnn_dequantize.py"
 CONCAT = "tests/python/relay/test_op_qnn_concatenate.py"
 MUL = "tests/python/relay/test_op_qnn_mul.py"
 SUB = "tests/python/relay/test_op_qnn_subtract.py"
+LEAKY = "tests/python/relay/test_op_qnn_leaky_relu.py"
+UNARY = "tests/python/relay/test_op_qnn_unary_elementwise.py"
+BMM = "tests/python/relay/test_op_qnn_batch_matmul.py"
 
 
 def arr(a, dtype):
@@ -367,13 +370,99 @@ def subtract_cases():
     return c
 
 
+def leaky_relu_cases():
+    """test_op_qnn_leaky_relu.py:36-73: the test's own golden formula (dequantize, alpha, np.around,
+    clip to uint8) on its literal data."""
+    x = np.array((255, 133, 0, 9)).reshape((1, 4))
+    s_in, z_in, s_out, z_out, alpha = 0.125, 60, 0.6, 17, 0.9
+    deq = s_in * (x - z_in)
+    prod = np.clip(np.around(deq * alpha / s_out + z_out), 0, 255)
+    rq = np.clip(np.round(deq / s_out + z_out), 0, 255)
+    gold = np.where(x < z_in, prod, rq)
+    return [{"op": "qnn.leaky_relu", "source": f"{LEAKY}:24-73", "name": "qnn_leaky_relu",
+             "inputs": {"data": arr(x, "uint8")},
+             "attrs": {"alpha": alpha, "input_scale": s_in, "input_zero_point": z_in, "output_scale": s_out,
+                       "output_zero_point": z_out},
+             "expected": arr(gold, "uint8")}]
+
+
+def unary_cases():
+    """test_op_qnn_unary_elementwise.py: golden = np.around(f(scale * (x - zp)) / s_out + zp_out), clipped,
+    the float function evaluated in float64 on the test's literal inputs (every bit pattern, or
+    the rsqrt saturation vector).  `class Sqrt` lacks the Test prefix (not collected there)."""
+    import scipy.special
+
+    def hardswish(x):
+        x2 = np.clip(x + 3.0, 0.0, 6.0)
+        return x * x2 / 6.0
+
+    fns = {"qnn.rsqrt": lambda x: 1 / np.sqrt(x), "qnn.exp": np.exp, "qnn.tanh": np.tanh,
+           "qnn.erf": scipy.special.erf, "qnn.sigmoid": lambda x: 1 / (1 + np.exp(-x)), "qnn.hardswish": hardswish}
+    lines = {"qnn.rsqrt": "129-165", "qnn.exp": "181-186", "qnn.tanh": "189-194", "qnn.erf": "197-202",
+             "qnn.sigmoid": "205-210", "qnn.hardswish": "213-218"}
+
+    def gold(op, x, s, z, os_, oz, dt):
+        with np.errstate(all="ignore"):
+            o = fns[op](s * (np.asarray(x, dtype=np.float64) - z))
+        o = np.around(o / os_ + oz)
+        info = np.iinfo(dt)
+        return np.clip(o, info.min, info.max).astype(dt)
+
+    def case(op, name, x, dt, s, z, os_, oz):
+        return {"op": "qnn.unary", "source": f"{UNARY}:{lines[op]}", "name": f"{op.split('.')[1]}_{name}",
+                "inputs": {"data": arr(x, dt)},
+                "attrs": {"unary_op": op, "scale": s, "zero_point": z, "output_scale": os_, "output_zero_point": oz},
+                "expected": arr(gold(op, x, s, z, os_, oz, dt), dt)}
+
+    c = []
+    sat = np.array((255, 133, 0, 9)).reshape((1, 4))
+    c.append(case("qnn.rsqrt", "saturation_same", sat, "uint8", 0.125, 0, 0.125, 0))
+    c.append(case("qnn.rsqrt", "saturation_out_scale", sat, "uint8", 0.125, 0, 0.25, 0))
+    for op in fns:
+        c.append(case(op, "all_uint8", np.arange(0, 256, dtype="uint8"), "uint8", 0.125, 0, 0.125, 0))
+        x8 = np.arange(1, 128, dtype="int8") if op == "qnn.rsqrt" else np.arange(0, 256, dtype="uint8").view("int8")
+        c.append(case(op, "all_int8", x8, "int8", 0.125, 0, 0.125, 0))
+    return c
+
+
+def batch_matmul_cases():
+    """test_op_qnn_batch_matmul.py:78-174: literal operands and outputs for batch sizes 1, 4, 7 and
+    the four zero-point combinations, plus the requantized int8 output."""
+    xv = [1, 3, 5, 7, 9, 11, 13, 15, -19, -21, 1, 3, 5, 7, 9, 11, 13, -17, 17, -21]
+    yv = [1, 3, 5, 7, 9, 11, 13, 15, 17, 19, 1, 3, 5, 7, 9]
+    outs = {(True, True): [165, 415, 165, -197, -207, -197, 165, 415, 165, -105, -75, -105],
+            (False, False): [81960, 88360, 81960, 78400, 84540, 78400, 81960, 88360, 81960, 78984, 85164, 78984],
+            (True, False): [3240, 3490, 3240, -320, -330, -320, 3240, 3490, 3240, 264, 294, 264],
+            (False, True): [3240, 9640, 3240, 2878, 9018, 2878, 3240, 9640, 3240, 2970, 9150, 2970]}
+    c = []
+    for b in (1, 4, 7):
+        x = np.array(xv)[np.newaxis, np.newaxis, :].repeat(b, axis=1).astype("int8").reshape(b, 4, 5)
+        y = np.array(yv)[np.newaxis, np.newaxis, :].repeat(b, axis=1).astype("int8").reshape(b, 3, 5)
+        for (xz0, yz0), o in outs.items():
+            exp = np.array(o)[np.newaxis, np.newaxis, :].repeat(b, axis=1).reshape(b, 4, 3)
+            c.append({"op": "qnn.batch_matmul", "source": f"{BMM}:73-174", "name": f"b{b}_xzp{int(not xz0)}_yzp{int(not yz0)}",
+                      "inputs": {"x": arr(x, "int8"), "y": arr(y, "int8")},
+                      "attrs": {"x_zero_point": 0 if xz0 else -123, "y_zero_point": 0 if yz0 else -123,
+                                "x_scale": 0.5, "y_scale": 0.5},
+                      "expected": arr(exp, "int32")})
+        exp = np.array([20, 51, 20, -26, -27, -26, 20, 51, 20, -14, -10, -14])[np.newaxis, np.newaxis, :].repeat(
+            b, axis=1).reshape(b, 4, 3)
+        c.append({"op": "qnn.batch_matmul", "source": f"{BMM}:131-158,259-265", "name": f"b{b}_requantized",
+                  "inputs": {"x": arr(x, "int8"), "y": arr(y, "int8")},
+                  "attrs": {"x_zero_point": 0, "y_zero_point": 0, "x_scale": 0.5, "y_scale": 0.5},
+                  "requantize": {"input_scale": 0.25, "output_scale": 2.0, "output_zero_point": -1, "out_dtype": "int8"},
+                  "expected": arr(exp, "int8")})
+    return c
+
+
 def main():
     doc = {
         "about": "Literal known-answer vectors transcribed from the reference's unit tests "
                  "(CortexFoundation/tachikoma @ /root/reference). Generated by make_golden.py.",
         "pinned_config": {"target": "llvm (no -mcpu)", "compute_dtype": "int64", "rounding_default": "UPWARD"},
         "cases": requantize_cases() + dense_cases() + conv_cases() + add_cases() + quantize_cases() +
-                 dequantize_cases() + concatenate_cases() + mul_cases() + subtract_cases(),
+                 dequantize_cases() + concatenate_cases() + mul_cases() + subtract_cases() + leaky_relu_cases() +
+                 unary_cases() + batch_matmul_cases(),
     }
     path = os.path.join(HERE, "qnn_kats.json")
     with open(path, "w") as f:

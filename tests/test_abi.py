@@ -49,6 +49,8 @@ int main(void) {
   P(tk_qparams_attrs) P(tk_qnn_binary_attrs) P(tk_concat_attrs) P(tk_transpose_attrs)
   O(tk_qparams_attrs, zero_points) O(tk_qnn_binary_attrs, out) O(tk_qnn_binary_attrs, output_zero_point)
   O(tk_concat_attrs, rq)
+  P(tk_leaky_relu_attrs) P(tk_conv2d_transpose_attrs) O(tk_leaky_relu_attrs, alpha_multiplier)
+  O(tk_leaky_relu_attrs, zp_shift) O(tk_conv2d_transpose_attrs, kernel_zero_points)
   return 0;
 }
 """
@@ -86,6 +88,11 @@ def test_ctypes_layout_matches_c(tmp_path):
         "tk_qnn_binary_attrs.out": _lib.tk_qnn_binary_attrs.out.offset,
         "tk_qnn_binary_attrs.output_zero_point": _lib.tk_qnn_binary_attrs.output_zero_point.offset,
         "tk_concat_attrs.rq": _lib.tk_concat_attrs.rq.offset,
+        "tk_leaky_relu_attrs": ctypes.sizeof(_lib.tk_leaky_relu_attrs),
+        "tk_conv2d_transpose_attrs": ctypes.sizeof(_lib.tk_conv2d_transpose_attrs),
+        "tk_leaky_relu_attrs.alpha_multiplier": _lib.tk_leaky_relu_attrs.alpha_multiplier.offset,
+        "tk_leaky_relu_attrs.zp_shift": _lib.tk_leaky_relu_attrs.zp_shift.offset,
+        "tk_conv2d_transpose_attrs.kernel_zero_points": _lib.tk_conv2d_transpose_attrs.kernel_zero_points.offset,
     }
     for k, v in py.items():
         assert int(got[k]) == v, (k, got[k], v)

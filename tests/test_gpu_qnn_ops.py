@@ -304,3 +304,155 @@ def test_frontend_qnn_graph_text(device, tmp_path):
     m.trace_capture().synchronize()
     tr2 = read_trace(m.trace_capture().bytes(), copy=True)
     _check(tr2.records, exp)
+
+
+# ---------------------------------------------------------------- round 5: leaky_relu, the unary
+# table lookups, batch_matmul, conv2d_transpose
+
+@pytest.mark.parametrize("case", load_cases("qnn.leaky_relu"), ids=lambda c: c["name"])
+def test_leaky_relu_kat(device, tmp_path, case):
+    a = case["attrs"]
+    x = load_array(case["inputs"]["data"])
+    v = relay.var("x", x.shape, str(x.dtype))
+    e = qnn.op.leaky_relu(v, a["alpha"], np.float32(a["input_scale"]), np.int32(a["input_zero_point"]),
+                          np.float32(a["output_scale"]), np.int32(a["output_zero_point"]))
+    rec, exp = _trace(e, {"x": x}, tmp_path)
+    _check(rec, exp)
+    np.testing.assert_array_equal(rec["%0"], load_array(case["expected"]))
+
+
+@pytest.mark.parametrize("dtype", ["int8", "uint8"])
+@pytest.mark.parametrize("alpha,s_in,z_in,s_out,z_out,rounding", [
+    (0.1, 0.05, 3, 0.05, 3, "UPWARD"),        # same params: RequantizeOrUpcast casts
+    (0.25, 0.05, -7, 0.11, 9, "UPWARD"),
+    (0.5, 0.125, 60, 0.6, 17, "TONEAREST"),   # alpha 0.5: the power-of-two fixed_point_multiply
+    (0.333, 0.02, 0, 0.0625, -4, "TONEAREST"),
+    (0.9, 0.125, 60, 0.25, 0, "UPWARD"),      # 1 - alpha = 0.1
+])
+def test_leaky_relu_random(device, tmp_path, dtype, alpha, s_in, z_in, s_out, z_out, rounding):
+    rng = np.random.default_rng(int(alpha * 1000) + 7)
+    lo, hi = (0, 256) if dtype == "uint8" else (-128, 128)
+    x = rng.integers(lo, hi, (3, 5, 67)).astype(dtype)
+    v = relay.var("x", x.shape, dtype)
+    with qnn.op.requantize_config(rounding=rounding):
+        e = qnn.op.leaky_relu(v, alpha, np.float32(s_in), np.int32(z_in), np.float32(s_out), np.int32(z_out))
+    rec, exp = _trace(e, {"x": x}, tmp_path)
+    _check(rec, exp)
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.unary"), ids=lambda c: c["name"])
+def test_unary_kat(device, tmp_path, case):
+    a = case["attrs"]
+    x = load_array(case["inputs"]["data"])
+    v = relay.var("x", x.shape, str(x.dtype))
+    e = getattr(qnn.op, a["unary_op"].split(".")[1])(v, np.float32(a["scale"]), np.int32(a["zero_point"]),
+                                                     np.float32(a["output_scale"]), np.int32(a["output_zero_point"]))
+    rec, exp = _trace(e, {"x": x}, tmp_path)
+    _check(rec, exp)
+    np.testing.assert_array_equal(rec["%0"], load_array(case["expected"]))
+
+
+@pytest.mark.parametrize("op", list(qnn.op.UNARY_OPS))
+@pytest.mark.parametrize("dtype", ["int8", "uint8"])
+def test_unary_every_pattern_and_ragged(device, tmp_path, op, dtype):
+    """Every 8-bit pattern (the whole table) in a ragged tensor (the 16-byte path and its tail), with
+    asymmetric params, bit-exact vs the oracle's table (same numpy functions)."""
+    rng = np.random.default_rng(hash(op) % 1000)
+    base = np.arange(256, dtype=np.uint8).view(dtype)
+    x = np.concatenate([base, rng.integers(0, 256, 1000 - 256).astype(np.uint8).view(dtype)]).reshape(8, 125)
+    v = relay.var("x", x.shape, dtype)
+    e = getattr(qnn.op, op.split(".")[1])(v, np.float32(0.037), np.int32(5 if dtype == "uint8" else -3),
+                                          np.float32(0.021), np.int32(100 if dtype == "uint8" else 2))
+    rec, exp = _trace(e, {"x": x}, tmp_path)
+    _check(rec, exp)
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.batch_matmul"), ids=lambda c: c["name"])
+def test_batch_matmul_kat(device, tmp_path, case):
+    a = case["attrs"]
+    x, y = load_array(case["inputs"]["x"]), load_array(case["inputs"]["y"])
+    vx, vy = relay.var("x", x.shape, "int8"), relay.var("y", y.shape, "int8")
+    e = qnn.op.batch_matmul(vx, vy, np.int32(a["x_zero_point"]), np.int32(a["y_zero_point"]), np.float32(a["x_scale"]),
+                            np.float32(a["y_scale"]))
+    if "requantize" in case:
+        r = case["requantize"]
+        e = qnn.op.requantize(e, np.float32(r["input_scale"]), np.int32(0), np.float32(r["output_scale"]),
+                              np.int32(r["output_zero_point"]), out_dtype=r["out_dtype"])
+    rec, exp = _trace(e, {"x": x, "y": y}, tmp_path)
+    _check(rec, exp)
+    np.testing.assert_array_equal(rec[sorted(rec, key=lambda k: int(k[1:]) if k[1:].isdigit() else -1)[-1]],
+                                  load_array(case["expected"]))
+
+
+@pytest.mark.parametrize("bx,by,m,n,k,dtype,zx,zy", [
+    (4, 4, 33, 70, 96, "int8", 3, -5),
+    (1, 6, 128, 64, 64, "uint8", 128, 120),   # x broadcast over y's batch
+    (5, 1, 17, 9, 200, "int8", 0, 7),          # y broadcast
+    (12, 12, 128, 128, 64, "int8", -1, 0),     # attention-shaped
+])
+def test_batch_matmul_random(device, tmp_path, bx, by, m, n, k, dtype, zx, zy):
+    rng = np.random.default_rng(bx * 100 + m)
+    lo, hi = (0, 256) if dtype == "uint8" else (-128, 128)
+    x = rng.integers(lo, hi, (bx, m, k)).astype(dtype)
+    y = rng.integers(lo, hi, (by, n, k)).astype(dtype)
+    vx, vy = relay.var("x", x.shape, dtype), relay.var("y", y.shape, dtype)
+    e = qnn.op.batch_matmul(vx, vy, np.int32(zx), np.int32(zy), np.float32(0.1), np.float32(0.2))
+    rec, exp = _trace(e, {"x": x, "y": y}, tmp_path)
+    _check(rec, exp)
+
+
+@pytest.mark.parametrize("ds,ws,zd,zw,st,pad,opad,groups,dtype,dl,kl", [
+    # test_op_qnn_conv2_transpose.py's cases
+    ((2, 1, 2, 4), (1, 3, 2, 2), 0, 0, (1, 1), (0, 0), (0, 0), 1, "uint8", "NCHW", "IOHW"),
+    ((2, 4, 2, 4), (4, 3, 2, 2), 0, 1, (1, 1), (0, 0), (0, 0), 1, "int8", "NCHW", "IOHW"),
+    ((2, 4, 2, 4), (4, 3, 2, 2), 5, 3, (1, 1), (0, 0), (0, 0), 1, "uint8", "NCHW", "IOHW"),
+    ((1, 4, 2, 2), (4, 3, 2, 2), 8, 5, (1, 1), (1, 1), (0, 0), 1, "uint8", "NCHW", "IOHW"),
+    ((2, 2, 4, 4), (2, 2, 3, 4), 5, 3, (1, 1), (0, 0), (0, 0), 1, "uint8", "NHWC", "HWOI"),
+    ((2, 8, 6, 4), (2, 2, 3, 4), 8, 3, (1, 1), (1, 1, 2, 2), (0, 0), 1, "uint8", "NHWC", "HWOI"),
+    # strides, output padding, groups, a per-channel kernel zero point
+    ((2, 16, 7, 7), (16, 8, 3, 3), 2, -1, (2, 2), (1, 1), (1, 1), 1, "int8", "NCHW", "IOHW"),
+    ((1, 12, 5, 6), (12, 4, 4, 4), -3, 2, (2, 3), (1, 0, 2, 1), (1, 2), 3, "int8", "NCHW", "IOHW"),
+    ((2, 4, 3, 3), (4, 3, 2, 2), 1, [1, -2, 3], (2, 2), (0, 0), (0, 0), 1, "uint8", "NCHW", "IOHW"),
+    ((1, 6, 6, 8), (3, 3, 8, 5), 4, 1, (2, 2), (1, 1), (0, 0), 1, "int8", "NHWC", "HWIO"),
+])
+def test_conv2d_transpose(device, tmp_path, ds, ws, zd, zw, st, pad, opad, groups, dtype, dl, kl):
+    rng = np.random.default_rng(sum(ds) + sum(ws))
+    lo, hi = (0, 256) if dtype == "uint8" else (-128, 128)
+    x = rng.integers(lo, hi, ds).astype(dtype)
+    w = rng.integers(lo, hi, ws).astype(dtype)
+    vx, vw = relay.var("x", ds, dtype), relay.var("w", ws, dtype)
+    e = qnn.op.conv2d_transpose(vx, vw, np.int32(zd), _c(zw, "int32"), np.float32(0.5), np.float32(0.25), strides=st,
+                                padding=pad, groups=groups, data_layout=dl, kernel_layout=kl, output_padding=opad)
+    rec, exp = _trace(e, {"x": x}, tmp_path, params={"w": w})
+    _check(rec, exp)
+
+
+def test_round5_ops_in_one_graph_text(device, tmp_path):
+    """A generator-shaped QNN graph -- conv2d_transpose -> requantize -> leaky_relu -> hardswish ->
+    batch_matmul over the flattened maps -- built from constructors, printed as Relay text, parsed back
+    and traced (plain and as a replayed HIP graph), every record bit-exact vs the oracle."""
+    rng = np.random.default_rng(5)
+    x = rng.integers(-128, 128, (2, 8, 4, 4)).astype(np.int8)
+    w = rng.integers(-128, 128, (8, 4, 3, 3)).astype(np.int8)
+    vx, vw = relay.var("x", x.shape, "int8"), relay.var("w", w.shape, "int8")
+    ct = qnn.op.conv2d_transpose(vx, vw, np.int32(1), np.int32(0), np.float32(0.05), np.float32(0.01), strides=(2, 2),
+                                 padding=(1, 1), output_padding=(1, 1))
+    rq = qnn.op.requantize(ct, np.float32(0.0005), np.int32(0), np.float32(0.1), np.int32(-2), out_dtype="int8")
+    lr = qnn.op.leaky_relu(rq, 0.2, np.float32(0.1), np.int32(-2), np.float32(0.08), np.int32(0))
+    hs = qnn.op.hardswish(lr, np.float32(0.08), np.int32(0), np.float32(0.05), np.int32(-10))
+    r3 = relay.reshape(hs, (2, 4, 64))
+    bm = qnn.op.batch_matmul(r3, r3, np.int32(-10), np.int32(-10), np.float32(0.05), np.float32(0.05))
+    mod = relay.IRModule.from_expr(bm)
+    text = mod.astext()
+    assert "qnn.conv2d_transpose" in text and "qnn.leaky_relu" in text and "qnn.hardswish" in text
+    mod2 = relay.parse(text)
+    exp = graph_ref.calibrate(mod2, {"w": w}, {"x": x})
+    for use_graph in (False, True):
+        lib = relay.build(mod2, target="mi355x", params={"w": w})
+        m = graph_executor.GraphModule(lib["default"]())
+        m.module.use_graph = use_graph
+        m.set_input(x=x)
+        path = str(tmp_path / f"g{int(use_graph)}.tkt")
+        m.dump_trace(path)
+        _check(read_trace(path, copy=True).records, exp)
+        m.close()

@@ -156,3 +156,92 @@ def test_binary_broadcast_and_per_axis():
     sc = np.array([np.float32(np.float64(x) * np.float64(y)) for x, y in zip(ls, rs)], np.float32)
     exp = ref.requantize(prod, sc, np.int32(0), np.float32(0.05), np.int32(0), axis=1, out_dtype="int8")
     np.testing.assert_array_equal(out, exp)
+
+
+# ---- round 5: the rest of the QNN dialect (leaky_relu, unary table lookups, batch_matmul,
+# conv2d_transpose)
+
+@pytest.mark.parametrize("case", load_cases("qnn.leaky_relu"), ids=lambda c: c["name"])
+def test_leaky_relu_kat(case):
+    a = case["attrs"]
+    out = ref.qnn_leaky_relu(load_array(case["inputs"]["data"]), a["alpha"], a["input_scale"], a["input_zero_point"],
+                             a["output_scale"], a["output_zero_point"])
+    np.testing.assert_array_equal(out, load_array(case["expected"]))
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.unary"), ids=lambda c: c["name"])
+def test_unary_kat(case):
+    a = case["attrs"]
+    out = ref.qnn_unary(a["unary_op"], load_array(case["inputs"]["data"]), a["scale"], a["zero_point"],
+                        a["output_scale"], a["output_zero_point"])
+    np.testing.assert_array_equal(out, load_array(case["expected"]))
+
+
+@pytest.mark.parametrize("case", load_cases("qnn.batch_matmul"), ids=lambda c: c["name"])
+def test_batch_matmul_kat(case):
+    a = case["attrs"]
+    out = ref.qnn_batch_matmul(load_array(case["inputs"]["x"]), load_array(case["inputs"]["y"]), a["x_zero_point"],
+                               a["y_zero_point"])
+    if "requantize" in case:
+        r = case["requantize"]
+        out = ref.requantize(out, np.float32(r["input_scale"]), np.int32(0), np.float32(r["output_scale"]),
+                             np.int32(r["output_zero_point"]), out_dtype=r["out_dtype"])
+    np.testing.assert_array_equal(out, load_array(case["expected"]))
+
+
+def test_leaky_relu_alpha_one_is_rejected():
+    # fixed_point_multiply by 1.0 takes q_multiply_shift's power-of-two branch with shift 1: the
+    # reference's compiler rejects the 1 << -1 rounding factor (intrin_rule.cc:223-237)
+    x = np.array([1, 2, 3], np.int8)
+    with pytest.raises(ValueError):
+        ref.qnn_leaky_relu(x, 1.0, 0.5, 0, 0.5, 0)
+    with pytest.raises(ValueError):
+        ref.qnn_leaky_relu(x, 0.0, 0.5, 0, 0.5, 0)
+
+
+def _conv2d_transpose_topi(d, w, zd, zw, strides, padding, output_padding, groups):
+    """The definition as topi writes it (conv2d_transpose.py:79-140): int16 shifts, dilate the data
+    by the stride, pad by k - 1 - pad (+ output padding at the end), correlate with the kernel
+    flipped and transposed to OIHW -- an independent restatement to pin qnn_ref's gather form."""
+    d = d.astype(np.int64) - zd
+    w = w.astype(np.int64) - (np.asarray(zw).reshape(1, -1, 1, 1) if np.ndim(zw) else zw)
+    n, c, h, wd = d.shape
+    _, og, kh, kw = w.shape
+    sh, sw = strides
+    pt, pl, pb, pr = padding
+    dil = np.zeros((n, c, (h - 1) * sh + 1, (wd - 1) * sw + 1), np.int64)
+    dil[:, :, ::sh, ::sw] = d
+    pad = np.pad(dil, ((0, 0), (0, 0), (kh - 1 - pt, kh - 1 - pb + output_padding[0]),
+                       (kw - 1 - pl, kw - 1 - pr + output_padding[1])))
+    oh, ow = pad.shape[2] - kh + 1, pad.shape[3] - kw + 1
+    cg = c // groups
+    out = np.zeros((n, og * groups, oh, ow), np.int64)
+    for o in range(og * groups):
+        g, oo = divmod(o, og)
+        kt = w[g * cg:(g + 1) * cg, oo, ::-1, ::-1]  # (cg, kh, kw), flipped
+        for y in range(oh):
+            for x in range(ow):
+                out[:, o, y, x] = np.einsum("nchw,chw->n", pad[:, g * cg:(g + 1) * cg, y:y + kh, x:x + kw], kt)
+    return ref.wrap_i32(out).astype(np.int32)
+
+
+@pytest.mark.parametrize("cfg", [
+    # test_op_qnn_conv2_transpose.py's shapes: no / kernel / input / both zero points, padding, strides
+    ((2, 1, 2, 4), (1, 3, 2, 2), 0, 0, (1, 1), (0, 0, 0, 0), (0, 0), 1, "uint8"),
+    ((2, 4, 2, 4), (4, 3, 2, 2), 0, 1, (1, 1), (0, 0, 0, 0), (0, 0), 1, "uint8"),
+    ((2, 4, 2, 4), (4, 3, 2, 2), 5, 0, (1, 1), (0, 0, 0, 0), (0, 0), 1, "int8"),
+    ((1, 4, 2, 2), (4, 3, 2, 2), 8, 5, (1, 1), (1, 1, 1, 1), (0, 0), 1, "uint8"),
+    ((2, 4, 5, 3), (4, 2, 3, 3), 3, 2, (2, 2), (1, 0, 1, 2), (1, 1), 1, "int8"),
+    ((1, 6, 4, 4), (6, 2, 3, 3), -2, 1, (2, 1), (0, 1, 1, 0), (1, 0), 3, "int8"),
+    ((1, 4, 3, 3), (4, 3, 2, 2), 1, [1, -2, 3], (2, 2), (0, 0, 0, 0), (0, 0), 1, "uint8"),
+])
+def test_conv2d_transpose_oracle_matches_topi_definition(cfg):
+    ds, ws, zd, zw, st, pad, opad, groups, dt = cfg
+    rng = np.random.default_rng(7)
+    info = np.iinfo(dt)
+    d = rng.integers(info.min, info.max + 1, ds).astype(dt)
+    w = rng.integers(info.min, info.max + 1, ws).astype(dt)
+    got = ref.qnn_conv2d_transpose(d, w, zd, np.asarray(zw), strides=st, padding=pad, output_padding=opad,
+                                   groups=groups)
+    exp = _conv2d_transpose_topi(d, w, zd, zw, st, pad, opad, groups)
+    np.testing.assert_array_equal(got, exp)

@@ -105,3 +105,13 @@ def test_parse_errors():
         relay.parse('def @main(%x: Tensor[(4), int8]) { cast(%y, dtype="int32") }')
     with pytest.raises(relay.ParseError):
         relay.parse('def @main(%x: Tensor[(4), int8]) { qnn.add(%x, %x, meta[relay.Constant][3], 0, 1f, 0, 1f, 0) }')
+
+
+def test_parenthesised_expression_is_grouping_not_tuple():
+    """`(%x)` groups (a tensor), `(%x,)` is a 1-tuple, `()` the empty tuple (Relay's text format)."""
+    from tachikoma_amd.relay.expr import Tuple
+    m = relay.parse('def @main(%x: Tensor[(4), int8]) { cast((%x), dtype="int32") }')
+    assert m["main"].body.op == "cast" and not isinstance(m["main"].body.args[0], Tuple)
+    m = relay.parse('def @main(%x: Tensor[(2, 3), int8]) { qnn.concatenate((%x,), (0.5f,), (0,), 0.5f, 0, axis=0) }')
+    (tup,) = [a for a in m["main"].body.args[:1]]
+    assert isinstance(tup, Tuple) and len(tup.fields) == 1

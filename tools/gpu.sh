@@ -7,6 +7,8 @@
 #   bench      default bench line (20/5 steps)      host      same, --run-mode host
 #   findstep   the find step on this GPU, written as a tune table (commit it as profiles/<tag>_tune_table.json)
 #   copytrace  rocprofv3 memory-copy trace of 3 traced steps, graph then host-issued
+#   copytrace1 the graph-mode copy trace alone (exit mapping dumped: TK_DUMP_MAPS)
+#   copytracetorch control: a torch-only process under the copy-trace flags
 #   copytraceprobe  rocprofv3 memory-copy trace of tools/probe_copies (torch-free; bench under it crashes at exit)
 #   copyprobe  the step's 233 record copies isolated: host-issued, graph chains, packed chunks (tools/probe_copies)
 #   prof       rocprofv3 kernel-trace --stats of the default bench (compute + traced steps)
@@ -45,6 +47,12 @@ for r in "$@"; do
         python3 -u bench.py --steps 3 --warmup 1 --skip-cpu
       run 400 copytrace_host.log rocprofv3 --memory-copy-trace --output-format csv -d "$O/copy_host" -o run -- \
         python3 -u bench.py --steps 3 --warmup 1 --skip-cpu --run-mode host ;;
+    copytrace1)  # graph mode only, with the exit mapping dumped for symbolising a crash at exit
+      run 400 copytrace_graph.log env TK_DUMP_MAPS="$O/maps.txt" rocprofv3 --memory-copy-trace --stats \
+        --output-format csv -d "$O/copy_graph" -o run -- python3 -u bench.py --steps 3 --warmup 1 --skip-cpu ;;
+    copytracetorch)  # control: torch alone (no libtachikoma) under the same profiler flags
+      run 300 copytrace_torch.log rocprofv3 --memory-copy-trace --stats --output-format csv -d "$O/copy_torch" \
+        -o run -- python3 -u tools/probe_torch_copies.py ;;
     copytraceprobe) run 300 copytrace_probe.log rocprofv3 --memory-copy-trace --stats --output-format csv \
         -d "$O/copy_probe" -o run -- ./tools/probe_copies tools/resnet50_b64_record_sizes.txt 1 ;;
     copyprobe) run 300 copyprobe.jsonl ./tools/probe_copies tools/resnet50_b64_record_sizes.txt 3 ;;
