@@ -85,6 +85,9 @@ def parse(argv=None):
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse N>1 on one GPU")
     p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
+    p.add_argument("--copy-trace", default=None,
+                   help="after the timed region, trace 3 more packed steps with per-chunk copy timing "
+                        "(tk_module_copy_trace: the in-process memory-copy trace of the real step) into this JSON file")
     p.add_argument("--force-pg", action="store_true",
                    help="start the process group and run the N>1 collectives (elapsed all-reduce, record-digest "
                         "all-gather, rank-info all-gather, status broadcast) even at one rank: exercises the RCCL "
@@ -482,18 +485,23 @@ def main(argv=None) -> int:
         torch.cuda.synchronize(device)
     overlap_pick = None
     if writer is not None and args.file_overlap == "auto":
-        # the sink's find step (untimed): 3 steps overlapped vs 3 serialised, the faster is kept
-        overlap_pick = {}
-        for mode in ("on", "off"):
-            overlap_mode[0] = mode
-            step(0)
-            drain()
-            tp = time.perf_counter()
-            for i in range(3):
-                step(i)
-            drain()
-            overlap_pick[mode] = round((time.perf_counter() - tp) / 3 * 1e3, 1)
-        overlap_mode[0] = min(overlap_pick, key=overlap_pick.get)
+        # the sink's find step (untimed): overlapped vs serialised, 3 steps each, interleaved over
+        # 3 rounds (on, off, on, off, ...) so that a box's disk drifting between probes (10.5-16.7
+        # GB/s on one round-4 box) hits both modes alike; each mode's median round is compared
+        rounds = {"on": [], "off": []}
+        for _ in range(3):
+            for mode in ("on", "off"):
+                overlap_mode[0] = mode
+                step(0)
+                drain()
+                tp = time.perf_counter()
+                for i in range(3):
+                    step(i)
+                drain()
+                rounds[mode].append((time.perf_counter() - tp) / 3 * 1e3)
+        overlap_pick = {k: round(float(np.median(v)), 1) for k, v in rounds.items()}
+        overlap_pick["rounds_ms"] = {k: [round(x, 1) for x in v] for k, v in rounds.items()}
+        overlap_mode[0] = min(("on", "off"), key=lambda k: overlap_pick[k])
     for i in range(args.warmup):
         step(i)
     drain()
@@ -529,6 +537,34 @@ def main(argv=None) -> int:
     elapsed_max = float(t.item())
     if writer is not None:
         writer.shutdown()
+
+    # ---- copy trace of the real traced step (packed graph mode): per chunk, bytes and the copy's
+    # start / end on the capture stream after the step's first launch; gaps between chunk copies
+    # are time the PCIe link idles inside a step
+    copy_trace = None
+    if args.copy_trace and not args.no_trace and m.module.use_graph and args.graph_copies == 0:
+        m.module.set_copy_trace(True)
+        steps_ct = []
+        for i in range(3):
+            step(i)
+            drain()
+            ch = m.module.copy_trace()
+            busy = sum(c["end_ms"] - c["start_ms"] for c in ch)
+            gaps = [round(b["start_ms"] - a["end_ms"], 4) for a, b in zip(ch, ch[1:])]
+            tot = sum(c["bytes"] for c in ch)
+            steps_ct.append({"chunks": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in c.items()} for c in ch],
+                             "bytes": tot, "copy_busy_ms": round(busy, 3),
+                             "first_copy_start_ms": round(ch[0]["start_ms"], 3) if ch else None,
+                             "last_copy_end_ms": round(ch[-1]["end_ms"], 3) if ch else None,
+                             "gaps_ms": gaps, "GBps_while_copying": round(tot / (busy * 1e-3) / 1e9, 2) if busy else None,
+                             "GBps_first_to_last": round(tot / ((ch[-1]["end_ms"] - ch[0]["start_ms"]) * 1e-3) / 1e9, 2)
+                             if ch else None})
+        m.module.set_copy_trace(False)
+        copy_trace = {"source": "tk_module_copy_trace (HIP timing events around each chunk copy on the capture stream)",
+                      "steps": steps_ct}
+        if rank == 0:
+            with open(args.copy_trace, "w") as f:
+                json.dump(copy_trace, f, indent=1)
 
     # ---- compute-only steps (no capture): the kernels alone, timed with HIP events recorded
     # on the stream they run on (torch's current stream, handed to the module); the roofline

@@ -40,6 +40,23 @@ namespace tk {
 
 constexpr int kImgNI = 12;  // most LDS-DMA wave-instructions per wave and stage
 
+// 32-bit LDS byte address of a pointer into the workgroup's LDS (the operand of an asm ds_read)
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// s_waitcnt lgkmcnt(n) for an n known once the K steps are unrolled (0..15)
+__device__ __forceinline__ void lgkm_wait(int n) {
+  switch (n) {
+#define TK_LGKM(k) \
+  case k: asm volatile("s_waitcnt lgkmcnt(" #k ")" ::: "memory"); break;
+    TK_LGKM(0) TK_LGKM(1) TK_LGKM(2) TK_LGKM(3) TK_LGKM(4) TK_LGKM(5) TK_LGKM(6) TK_LGKM(7) TK_LGKM(8)
+    TK_LGKM(9) TK_LGKM(10) TK_LGKM(11) TK_LGKM(12) TK_LGKM(13) TK_LGKM(14)
+#undef TK_LGKM
+    default: asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory"); break;
+  }
+}
+
 struct ImgArgs {
   const int8_t* wimg;          // weight rows: chunked packing (3x3) or the plain one (1x1)
   int32_t ldw;                 // bytes per weight row
@@ -97,6 +114,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   const int L = blockIdx.x;
   const int w = (L & 7) * (h.wgs8 >> 3) + (L >> 3);
   if (w >= h.wgs) return;
+  if (TK_ABL(1 << 23)) return;  // (ablation build: launch and wave start / end alone)
 #ifdef TK_ABLATION_BUILD
   // profiling: stagger the first round's workgroups ((L >> 3) % 4 quarters of h.skew x s_sleep(8))
   // so that CUs are in different phases (K loop / epilogue stores)
@@ -236,7 +254,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   v16i acc[CT];
 #pragma unroll
   for (int j = 0; j < CT; ++j) acc[j] = v16i{0};
-  auto compute = [&](const int8_t* base) __attribute__((always_inline)) {
+  auto compute_c = [&](const int8_t* base) __attribute__((always_inline)) {
     v4i a[2], b[2][CT];
     auto rd = [&](int ks, int u) __attribute__((always_inline)) {
       const int t = ks / SUB, s = ks - t * SUB, kh = t / KT, kw = t - kh * KT;
@@ -274,17 +292,79 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     }
   };
 
+  // The 3x3 K steps with the fragment reads software-pipelined by hand: the
+  // compiler's own waits drain every outstanding LDS read (lgkmcnt(0)) before each MFMA pair
+  // (DESIGN.md §9), so a wave exposed an LDS round trip about every other step.  Here the reads are
+  // inline-asm ds_read_b128 issued D - 1 steps ahead -- every column tile read each step (columns a
+  // wave does not own re-read its first tile) so that each step issues exactly NR reads -- and each
+  // step waits with a counted lgkmcnt for its own reads only (LDS returns in order), then pins its
+  // fragments (an empty "+v" asm per fragment after the wait, and sched_barrier(0)) so no MFMA is
+  // scheduled above the wait (cdna_hip_programming.md §5.7, rule 18).
+  constexpr int NR = 1 + CT;                  // ds_read_b128 per K step
+  constexpr int D = NR * 3 <= 12 ? 3 : 2;     // steps of reads in flight (<= 15 outstanding)
+  auto compute_asm = [&](const int8_t* base) __attribute__((always_inline)) {
+    const uint32_t lb = lds_u32(base);
+    v4i fa[D], fb[D][CT];
+    auto rd = [&](int ks, int u) __attribute__((always_inline)) {
+      if (TK_ABL(1 << 20)) return;  // (ablation build: no fragment reads, timing only)
+      const int t = ks / SUB, s = ks - t * SUB, kh = t / KT, kw = t - kh * KT;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(fa[u]) : "v"(lb + (uint32_t)(aoff + (s * TAPS + t) * 32)));
+      const int dx = KT == 3 && h.half ? (kw == 1 ? 0 : kw == 0 ? h.half - 1 : h.half) : kw - KT / 2;
+      const int gs = 2 * s * pl16, bo = ((kh - KT / 2) * hc + dx) * 16;
+      [[maybe_unused]] const uint32_t me =
+          KT == 3 ? (kh == 0 ? 1u : 0u) | (kh == 2 ? 2u : 0u) | (kw == 0 ? 4u : 0u) | (kw == 2 ? 8u : 0u) : 0u;
+#pragma unroll
+      for (int j = 0; j < CT; ++j) {
+        const int jj = j < jn ? j : 0;  // (wave-uniform)
+        int off = boff[jj] + bo;
+        if constexpr (KT == 3) {
+          if (me && (flg[jj] & me)) off = hb;
+        }
+        asm volatile("ds_read_b128 %0, %1" : "=v"(fb[u][j]) : "v"(lb + (uint32_t)(gs + off)));
+      }
+    };
+#pragma unroll
+    for (int k = 0; k < D - 1 && k < KS; ++k) rd(k, k);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int u = ks % D;
+      if (ks + D - 1 < KS) rd(ks + D - 1, (ks + D - 1) % D);
+      lgkm_wait(NR * (min(ks + D - 1, KS - 1) - ks));
+      asm volatile("" : "+v"(fa[u]));
+#pragma unroll
+      for (int j = 0; j < CT; ++j) asm volatile("" : "+v"(fb[u][j]));
+      __builtin_amdgcn_sched_barrier(0);
+      if (!TK_ABL(512)) {
+#pragma unroll
+        for (int j = 0; j < CT; ++j)
+          if (j < jn) acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[u], fb[u][j], acc[j], 0, 0, 0);
+      }
+    }
+  };
+  auto compute = [&](const int8_t* base) __attribute__((always_inline)) {
+    if constexpr (KT == 3) {
+      if (!TK_ABL(1 << 22)) {  // (ablation build: 1 << 22 runs the compiler-scheduled steps)
+        compute_asm(base);
+        return;
+      }
+    }
+    compute_c(base);
+  };
+
   // ---- K loop: an ns-slot ring with ns - 1 stages in flight (ns from the plan: as many slots as
   // the LDS holds, since one workgroup per CU has nothing else to hide the L2 -> LDS latency
   // with); after the barrier of stage it, the slot read in step it - 1 is free for stage
   // it + ns - 1
+  if (TK_ABL(1 << 24)) return;  // (ablation build: + the prologue: sources, offsets, row constants)
   if constexpr (MODE != 2) {
     const int nst = MODE == 1 ? (int)((int64_t)(zs + 1) * h.stages / S) - st_lo : h.stages, ns = h.ns;
     for (int st = 0; st < ns - 1 && st < nst; ++st) issue(st);
     int cur = 0, nxt = ns - 1;
     for (int it = 0; it < nst; ++it) {
-      wait_vm_any(min(ns - 2, nst - 1 - it) * ni);
-      lds_barrier();
+      if (!TK_ABL(1 << 21)) {  // (ablation build: 1 << 21 drops the stage waits, timing only)
+        wait_vm_any(min(ns - 2, nst - 1 - it) * ni);
+        lds_barrier();
+      }
       if (it + ns - 1 < nst) {
         issue(nxt);
         nxt = nxt == ns - 1 ? 0 : nxt + 1;
@@ -803,9 +883,18 @@ std::vector<ImgPlan> img_plans_build(const ConvGeom& g, const tk_conv2d_attrs* a
 using ImgPlans = std::shared_ptr<const std::vector<ImgPlan>>;
 
 ImgPlans img_plans(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, bool have_chunked) {
+  // Outside the ablation build tune_env() is compiled to nullptr (tk_conv.h), so every TK_IMG*
+  // knob read by img_plans_build / img_candidate / conv_img_split_scratch_bytes is its constant
+  // default and the geometry is the whole key.  The ablation build (plans follow TK_IMG_*
+  // variables set between calls) keys its cache by the knobs' values too, so that its launches
+  // cost a lookup like the product's (re-planning per launch made host time the measurement).
+  std::string knobs;
 #ifdef TK_ABLATION_BUILD
-  // (plans follow TK_IMG_* variables set between calls)
-  return std::make_shared<const std::vector<ImgPlan>>(img_plans_build(g, a, ga, have_chunked));
+  for (const char* k : {"TK_IMG", "TK_IMG3", "TK_IMG1", "TK_IMG_MAXHW", "TK_IMG_R", "TK_IMG_IPT", "TK_IMG_CC",
+                        "TK_IMG_TWO", "TK_IMG_SPLIT", "TK_IMG_NS", "TK_IMG_SKEW"}) {
+    const char* v = tune_env(k);
+    knobs += std::string(k) + "=" + (v ? v : "") + ";";
+  }
 #endif
   const std::array<int64_t, 27> key = {g.N, g.C, g.H, g.W, g.O, g.KH, g.KW, g.OH, g.OW, g.cin_pad, g.k_pad,
                                        g.rows_pad, a->strides[0], a->strides[1], a->padding[0], a->padding[1],
@@ -813,16 +902,17 @@ ImgPlans img_plans(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& 
                                        ga.bias_out != nullptr, ga.RB != nullptr, ga.zA_vec != nullptr, ga.zA,
                                        ga.has_add, ga.in_pix, have_chunked};
   static std::mutex mu;
-  static std::map<std::array<int64_t, 27>, ImgPlans> cache;
+  static std::map<std::pair<std::array<int64_t, 27>, std::string>, ImgPlans> cache;
+  const auto ck = std::make_pair(key, knobs);
   {
     std::lock_guard<std::mutex> lock(mu);
-    auto it = cache.find(key);
+    auto it = cache.find(ck);
     if (it != cache.end()) return it->second;
   }
   ImgPlans plans = std::make_shared<const std::vector<ImgPlan>>(img_plans_build(g, a, ga, have_chunked));
   std::lock_guard<std::mutex> lock(mu);
   if (cache.size() > 4096) cache.clear();
-  cache.emplace(key, plans);
+  cache.emplace(ck, plans);
   return plans;
 }
 

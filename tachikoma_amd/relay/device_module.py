@@ -932,6 +932,19 @@ class DeviceModule:
     def _node_kind(self, i: int) -> int:
         return self._node_kind_codes[i]
 
+    def set_copy_trace(self, enable: bool) -> None:
+        """Per-chunk copy timing of packed traced runs (tk_module_set_copy_trace)."""
+        _lib.check(self.lib.tk_module_set_copy_trace(self.handle, int(enable)), "tk_module_set_copy_trace")
+
+    def copy_trace(self) -> List[dict]:
+        """The last packed traced run's chunk copies: bytes, start / end ms after the run's first
+        launch (tk_module_copy_trace; waits for those copies)."""
+        n = self.lib.tk_module_copy_trace(self.handle, None, 0)
+        _lib.check(min(n, 0), "tk_module_copy_trace")
+        buf = (ctypes.c_double * max(1, 3 * n))()
+        _lib.check(min(self.lib.tk_module_copy_trace(self.handle, buf, n), 0), "tk_module_copy_trace")
+        return [{"bytes": int(buf[3 * c]), "start_ms": buf[3 * c + 1], "end_ms": buf[3 * c + 2]} for c in range(n)]
+
     def set_profiling(self, enable: bool) -> None:
         _lib.check(self.lib.tk_module_set_profiling(self.handle, int(enable)), "tk_module_set_profiling")
 

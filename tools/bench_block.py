@@ -33,7 +33,7 @@ SHAPES = [  # name, C, H, O, K, stride, pad
 ]
 
 
-def main(batch=64, iters=20, configs=None, reps=3, only=None, rotate=1):
+def main(batch=64, iters=20, configs=None, reps=3, only=None, rotate=1, marker=False):
     """configs: list of env-var dicts (TK_ABLATE / TK_NT are read per launch); each layer is
     timed for every config, interleaved `reps` times, and the minimum is reported."""
     import os
@@ -115,6 +115,11 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None, rotate=1):
                     call()
                 e1.record()
                 e1.synchronize()
+                if marker:
+                    # a fill kernel between configs: tools/abl_trace.py splits a rocprofv3 kernel
+                    # trace at these, so each config's GPU time is read without host overhead
+                    torch.empty(1, device=dev).fill_(ci)
+                    torch.cuda.synchronize()
                 best[ci] = min(best[ci], e0.elapsed_time(e1) / iters * 1e3)
                 for k, v in saved.items():
                     if v is None:
@@ -135,4 +140,4 @@ if __name__ == "__main__":
     import json
     cfgs = json.loads(sys.argv[1]) if len(sys.argv) > 1 else None
     main(configs=cfgs, only=sys.argv[2] if len(sys.argv) > 2 else None,
-         rotate=int(sys.argv[3]) if len(sys.argv) > 3 else 1)
+         rotate=int(sys.argv[3]) if len(sys.argv) > 3 else 1, marker="--marker" in sys.argv)
