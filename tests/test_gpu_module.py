@@ -242,8 +242,10 @@ def test_copy_trace_of_packed_runs(device):
         assert 1 <= len(ch) <= 8  # the default 8 chunks (fewer where records complete late)
         assert all(c["bytes"] > 0 and c["end_ms"] >= c["start_ms"] >= 0 for c in ch)
         assert all(b["start_ms"] >= a["end_ms"] - 1e-3 for a, b in zip(ch, ch[1:]))
-        recs = sum(int(np.prod(t.shape)) * np.dtype(t.dtype).itemsize for t in m.plan.records)
-        assert sum(c["bytes"] for c in ch) >= recs
+        # the chunks move the mirrored span of the op records (the graph inputs are copied by
+        # capture_inputs; records the pack cannot move in whole 16-byte pieces go by their own copies)
+        recs = sum(op.out.nbytes for op in m.plan.ops)
+        assert 0.9 * recs <= sum(c["bytes"] for c in ch) <= m.trace_capture().layout.total
     m.trace_capture().synchronize()
     assert bytes(m.trace_capture().bytes()) == ref_img
     m.module.set_copy_trace(False)
