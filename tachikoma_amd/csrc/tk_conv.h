@@ -217,6 +217,9 @@ __device__ __forceinline__ void wait_vm_any(int n) {
 
 
 __device__ __forceinline__ uint32_t fdiv40(uint32_t x, uint64_t mg) { return (uint32_t)(((uint64_t)x * mg) >> 40); }
+// x / d as one v_mul_hi_u32 with m = ceil(2^32 / d) (magic32): exact whenever x * d < 2^32, which
+// x, d < 2^16 guarantees (m * d = 2^32 + e, e < d, so the error x * e / (d * 2^32) stays below 1 / d)
+__device__ __forceinline__ uint32_t fdiv32(uint32_t x, uint32_t m) { return __umulhi(x, m); }
 
 
 struct ConvGeom {

@@ -75,7 +75,7 @@ struct ImgArgs {
   int32_t pstep;               // patch source bytes per stage (CC/16 shadow channel groups)
   int32_t tstride;             // int32 pitch of the epilogue staging rows
   int32_t rowc_off, lut_off, res_off;  // LDS byte offsets (the staging tile aliases the ring at 0)
-  uint64_t mg_pl, mg_img, mg_hc, mg_ws, mg_hw, mg_ow, mg_runq, mg_cw;  // (x * mg) >> 40 == x / d
+  uint32_t m_pl, m_img, m_hc, m_ws, m_hw, m_ow, m_runq, m_cw;  // fdiv32(x, m_d) == x / d (x, d < 2^16)
   int32_t runq;                // 4-element epilogue groups per image run and pass (R * cw / 4)
   int32_t npass, cw;           // epilogue passes over the tile's columns (npass > 1: one image per
                                // workgroup, cw = hw / npass pixels per pass), or 1 pass of cw = hw
@@ -149,9 +149,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       const int gi = q0 + lane;
       const int8_t* src = reinterpret_cast<const int8_t*>(tk_zero_words);
       if (gi < total) {
-        const int kk = (int)fdiv40((uint32_t)gi, h.mg_runq);
+        const int kk = (int)fdiv32((uint32_t)gi, h.m_runq);
         const int f = (gi - kk * runq) * 4;
-        const int r = (int)fdiv40((uint32_t)f, h.mg_cw), pp = f - r * W;  // row, pixel of the pass
+        const int r = (int)fdiv32((uint32_t)f, h.m_cw), pp = f - r * W;  // row, pixel of the pass
         src = reinterpret_cast<const int8_t*>(g.add_res) + (uint32_t)(((img0 + kk) * g.M + m0 + r) * hw + c0 + pp);
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (void*)(resw + q0), 4, 0, 0);
@@ -172,9 +172,15 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   // ---- LDS-DMA sources of this lane: slot q = (wave + 4k) * 64 + lane of every stage is patch
   // chunk (group q / pl, pixel q % pl) or weight chunk (row, 16-byte chunk) or slack; each source
   // advances by a fixed step per stage (0 for the zero-point fill and the pad chunks)
+  // (32-bit arithmetic throughout: one v_mul_hi_u32 per division and 24-bit products -- the 64-bit
+  // magic divisions and pointer products cost ~150 v_mad_u64_u32 before the first DMA; the byte
+  // offsets below stay under 2^31, img_candidate checks)
   const int ni = h.ni;
   const int8_t* srcs[kImgNI];
   uint32_t steps[kImgNI];
+  const int8_t* const pbase = g.B + (int64_t)img0 * g.H * g.W * 16;  // image img0 of channel group 0
+  const int8_t* const wbase = h.wimg + (int64_t)m0 * h.ldw;          // weight row m0
+  const uint32_t img_px = (uint32_t)(h.hr * h.hc), gstride = (uint32_t)g.in_pix * 16u;
 #pragma unroll
   for (int k = 0; k < kImgNI; ++k) {
     srcs[k] = fill_src;
@@ -182,25 +188,25 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     if (k < ni) {
       const uint32_t q = (uint32_t)((wave + 4 * k) * 64 + lane);
       if (q < (uint32_t)h.pslots) {
-        const uint32_t grp = fdiv40(q, h.mg_pl), pix0 = q - grp * h.pl;
+        const uint32_t grp = fdiv32(q, h.m_pl), pix0 = q - __umul24(grp, (uint32_t)h.pl);
         if (grp < (uint32_t)(CC / 16) && pix0 >= (uint32_t)h.lead) {  // else lead / trailing slack: fill
           const uint32_t pix = pix0 - h.lead;
-          const uint32_t kk = fdiv40(pix, h.mg_img), r = pix - kk * (h.hr * h.hc);
-          const uint32_t hrow = fdiv40(r, h.mg_hc), hcol = r - hrow * h.hc;
-          const int ih = h.ih0 + (int)hrow * h.ls;
+          const uint32_t kk = fdiv32(pix, h.m_img), r = pix - __umul24(kk, img_px);
+          const uint32_t hrow = fdiv32(r, h.m_hc), hcol = r - __umul24(hrow, (uint32_t)h.hc);
+          const int ih = h.ih0 + (int)__umul24(hrow, (uint32_t)h.ls);
           const int iw = h.half ? ((int)hcol < h.half ? 2 * (int)hcol : 2 * ((int)hcol - h.half) + 1)
-                                : h.iw0 + (int)hcol * h.ls;
-          const int img = img0 + (int)kk;
-          if (img < h.nimg && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
-            srcs[k] = g.B + ((int64_t)grp * g.in_pix + ((int64_t)img * g.H + ih) * g.W + iw) * 16;
+                                : h.iw0 + (int)__umul24(hcol, (uint32_t)h.ls);
+          if (img0 + (int)kk < h.nimg && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
+            const uint32_t px = __umul24(__umul24(kk, (uint32_t)g.H) + (uint32_t)ih, (uint32_t)g.W) + (uint32_t)iw;
+            srcs[k] = pbase + (grp * gstride + px * 16u);
             steps[k] = (uint32_t)h.pstep;
           }
         }
       } else if (q < (uint32_t)h.sslots) {
         const uint32_t wq = q - h.pslots;
-        const uint32_t row = fdiv40(wq, h.mg_ws), c = wq - row * h.wslot;
+        const uint32_t row = fdiv32(wq, h.m_ws), c = wq - __umul24(row, (uint32_t)h.wslot);
         if (c + 1 < (uint32_t)h.wslot) {
-          srcs[k] = h.wimg + (int64_t)(m0 + row) * h.ldw + c * 16;
+          srcs[k] = wbase + (__umul24(row, (uint32_t)h.ldw) + c * 16u);
           steps[k] = TAPS * CC;
         }
       }
@@ -239,8 +245,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
 #pragma unroll
   for (int j = 0; j < CT; ++j) {
     const uint32_t c = (uint32_t)min((wn + WN * j) * 32 + (lane & 31), h.p - 1);
-    const uint32_t kk = fdiv40(c, h.mg_hw), r = c - kk * hw;
-    const uint32_t oh = fdiv40(r, h.mg_ow), ow = r - oh * g.OW;
+    const uint32_t kk = fdiv32(c, h.m_hw), r = c - kk * hw;
+    const uint32_t oh = fdiv32(r, h.m_ow), ow = r - oh * g.OW;
     boff[j] = (int)(((lane >> 5) * h.pl + h.lead + kk * (h.hr * h.hc) + oh * h.hc * h.ps + ow * (h.half ? 1 : h.ps)) * 16);
     if constexpr (KT == 3) {
       const int ih = (int)oh * h.ps, iw = (int)ow * h.ps;  // the centre tap's input pixel
@@ -378,7 +384,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   // of the tile, column (wn + WN j) * 32 + lane % 32 (an image pixel of the tile)
   auto part_ptr = [&](int j, int32_t* base) __attribute__((always_inline)) -> int32_t* {
     const int col = min((wn + WN * j) * 32 + (lane & 31), h.p - 1);
-    const uint32_t kk = fdiv40((uint32_t)col, h.mg_hw);
+    const uint32_t kk = fdiv32((uint32_t)col, h.m_hw);
     const int pix = col - (int)kk * hw;
     const int img = min(img0 + (int)kk, h.nimg - 1);
     return base + ((int64_t)img * g.M + m0 + wm * 32 + 4 * (lane >> 5)) * hw + pix;
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     for (int j = 0; j < CT; ++j)
       if (j < jn) {
         const int col = (wn + WN * j) * 32 + (lane & 31);
-        const int kk = (int)fdiv40((uint32_t)min(col, h.p - 1), h.mg_hw);
+        const int kk = (int)fdiv32((uint32_t)min(col, h.p - 1), h.m_hw);
         if (col < h.p && img0 + kk < h.nimg) {
           int32_t* o = part_ptr(j, base);
 #pragma unroll
@@ -713,7 +719,7 @@ struct ImgPlan {
   int wm_b, ct_b;
 };
 
-uint64_t magic40(uint64_t d) { return ((1ull << 40) + d - 1) / d; }
+uint32_t magic32(uint32_t d) { return (uint32_t)(((1ull << 32) + d - 1) / d); }  // d >= 2
 
 // Most output columns a workgroup holds: 4 waves x 7 column tiles (R = 32), 2 x 4 (R = 64).
 constexpr int kImgMaxCols = 4 * 7 * 32;
@@ -797,14 +803,23 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   const size_t lds = (size_t)x.res_off + res_bytes;
   if (lds > (two ? 80 : 160) * 1024 - 64) return false;
   x.runq = R * cw / 4;
-  x.mg_cw = magic40(cw);
-  x.mg_pl = magic40(x.pl);
-  x.mg_img = magic40((uint64_t)x.hr * x.hc);
-  x.mg_hc = magic40(x.hc);
-  x.mg_ws = magic40(x.wslot);
-  x.mg_hw = magic40(hw);
-  x.mg_ow = magic40(g.OW);
-  x.mg_runq = magic40(x.runq);
+  // the kernel's 32-bit index arithmetic (fdiv32, 24-bit products): every divisor in [2, 2^16),
+  // every dividend below 2^16 (slots, tile columns, epilogue groups and their R * cw pixels), and
+  // the input's byte offsets (channel groups of a stage x in_pix x 16) below 2^31 (pstep, above)
+  for (int64_t d : {(int64_t)cw, (int64_t)x.pl, (int64_t)x.hr * x.hc, (int64_t)x.hc, (int64_t)x.wslot, (int64_t)hw,
+                    (int64_t)g.OW, (int64_t)x.runq})
+    if (d < 2 || d >= 65536) return false;
+  if ((int64_t)R * cw >= 65536 || p >= 65536 || x.ni * 256 >= 65536 || 9ll * g.cin_pad >= (1ll << 24) ||
+      ga.lda >= (1ll << 24))
+    return false;
+  x.m_cw = magic32(cw);
+  x.m_pl = magic32(x.pl);
+  x.m_img = magic32((uint32_t)(x.hr * x.hc));
+  x.m_hc = magic32(x.hc);
+  x.m_ws = magic32(x.wslot);
+  x.m_hw = magic32(hw);
+  x.m_ow = magic32(g.OW);
+  x.m_runq = magic32(x.runq);
   out->a = x;
   out->lds = lds;
   out->kt = kt;
