@@ -429,6 +429,30 @@ def main(argv=None) -> int:
     stream = torch.cuda.current_stream(device)
     path = shard.shard_file(args.out_dir, rank)
 
+    def teardown():
+        # while the HIP runtime is alive: device idle, native module destroyed, pinned images
+        # released -- nothing is left for finalisers or library static destructors at exit
+        caps.clear()
+        m.close()
+        import gc
+        gc.collect()
+        torch._C._host_emptyCache()  # the pinned trace images go back to the driver now, not at exit
+        dump_maps_at_exit()
+
+    # TK_BENCH_STOP=<phase>: end the run (same teardown) right after that phase -- bisects what in
+    # this process a profiler's exit trips over
+    stop_at = os.environ.get("TK_BENCH_STOP")
+
+    def stop(phase):
+        if stop_at == phase:
+            _log(f"TK_BENCH_STOP: ending after {phase}")
+            teardown()
+            return True
+        return False
+
+    if stop("setup"):
+        return 0
+
     import concurrent.futures
     writer = concurrent.futures.ThreadPoolExecutor(max_workers=1) if len(caps) > 1 else None
     pending = [None] * len(caps)
@@ -502,6 +526,8 @@ def main(argv=None) -> int:
         overlap_pick = {k: round(float(np.median(v)), 1) for k, v in rounds.items()}
         overlap_pick["rounds_ms"] = {k: [round(x, 1) for x in v] for k, v in rounds.items()}
         overlap_mode[0] = min(("on", "off"), key=lambda k: overlap_pick[k])
+    if stop("pick"):
+        return 0
     for i in range(args.warmup):
         step(i)
     drain()
@@ -528,6 +554,8 @@ def main(argv=None) -> int:
     elapsed = time.perf_counter() - t0
     step_gbps = [] if args.no_trace else \
         [rec_bytes / (a.elapsed_time(z) * 1e-3) / 1e9 for a, z in d2h_ev]
+    if stop("timed"):
+        return 0
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if pg:
@@ -575,6 +603,8 @@ def main(argv=None) -> int:
         m.run(trace=False)
     torch.cuda.synchronize(device)
     compute_ms = (time.perf_counter() - tc0) / max(args.steps, 1) * 1e3
+    if stop("compute"):
+        return 0
     # Block time from HIP events bracketing each maximal run of consecutive block nodes (52 of
     # ResNet-50's 54 blocks are one run): a timing event between every two nodes would add the
     # command processor's ~5.6 us per event to every node (rocprof: kernels back to back have
@@ -608,6 +638,8 @@ def main(argv=None) -> int:
         step_ms += step_ev[0].elapsed_time(step_ev[1])
     blk_ms /= max(args.steps, 1)
     step_ms /= max(args.steps, 1)
+    if stop("blocks"):
+        return 0
 
     # ---- roofline of the dominant kernel: the fused MFMA conv/dense layer block
     # (qnn.conv2d|dense -> bias_add -> requantize [-> qnn.add(residual)] [-> clip] in one
@@ -645,6 +677,8 @@ def main(argv=None) -> int:
     m.run(trace=not args.no_trace)
     torch.cuda.synchronize(device)
     digests = shard.gather_digests(m.module.records_digest(stream).to(coll_dev))
+    if stop("digest"):
+        return 0
     file_check = None
     if args.sink == "file" and not args.no_trace:
         caps[0].write(path)
@@ -666,6 +700,8 @@ def main(argv=None) -> int:
     # as two concurrent copies on two streams (do two SDMA engines beat one?)
     d2h_peak = d2h_probe(device)
     d2h_peak2 = d2h_probe(device, streams=2)
+    if stop("d2h"):
+        return 0
     trace_bytes = caps[0].layout.total
     d2h_achieved = trace_bytes / (elapsed_max / args.steps) / 1e9 if not args.no_trace else 0.0
 
@@ -844,15 +880,7 @@ def main(argv=None) -> int:
         dist.broadcast(flag, 0)
         rc = int(flag.item())
         dist.destroy_process_group()
-    # teardown while the HIP runtime is alive: device idle, native module destroyed, pinned images
-    # released -- nothing is left for finalisers or library static destructors at exit
-    caps.clear()
-    parity = None
-    m.close()
-    import gc
-    gc.collect()
-    torch._C._host_emptyCache()  # the pinned trace images go back to the driver now, not at exit
-    dump_maps_at_exit()
+    teardown()
     return rc
 
 

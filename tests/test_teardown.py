@@ -90,3 +90,25 @@ keep = m  # still referenced at exit
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.split("\n")[:2] == ["sync", "destroy 0xbeef live"], r.stdout
+
+
+def test_rocprof_one_hsa_wrapper(tmp_path):
+    """tools/rocprof_one_hsa.sh (the exit SIGSEGV's cause: two HSA runtimes under rocprofv3, DESIGN.md
+    §8) offers torch's bundled runtime under the soname the profiler's libraries ask for, first on
+    LD_LIBRARY_PATH, and hands every argument to rocprofv3 unchanged (a stand-in rocprofv3 here)."""
+    import torch
+    fake = tmp_path / "bin"
+    fake.mkdir()
+    (fake / "rocprofv3").write_text('#!/bin/bash\necho "LDP=$LD_LIBRARY_PATH"\nfor a in "$@"; do echo "ARG=$a"; done\n')
+    (fake / "rocprofv3").chmod(0o755)
+    env = dict(os.environ, PATH=f"{fake}:{os.environ['PATH']}", TMPDIR=str(tmp_path), LD_LIBRARY_PATH="/x")
+    out = subprocess.run(["bash", os.path.join(ROOT, "tools", "rocprof_one_hsa.sh"), "--memory-copy-trace", "-d",
+                          "a b", "--", "python3", "bench.py"], env=env, capture_output=True, text=True, check=True).stdout
+    lines = out.splitlines()
+    ldp = next(x for x in lines if x.startswith("LDP="))[4:].split(":")
+    assert ldp[0] == str(tmp_path / "tk_one_hsa") and ldp[1:] == ["/x"]
+    link = tmp_path / "tk_one_hsa" / "libhsa-runtime64.so.1"
+    want = os.path.join(os.path.dirname(torch.__file__), "lib", "libhsa-runtime64.so")
+    assert os.path.realpath(link) == os.path.realpath(want)
+    assert [x[4:] for x in lines if x.startswith("ARG=")] == ["--memory-copy-trace", "-d", "a b", "--", "python3",
+                                                             "bench.py"]

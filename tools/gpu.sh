@@ -6,9 +6,10 @@
 #   suite      pytest -m gpu (one process)          smoke     __graft_entry__.smoke()
 #   bench      default bench line (20/5 steps)      host      same, --run-mode host
 #   findstep   the find step on this GPU, written as a tune table (commit it as profiles/<tag>_tune_table.json)
-#   copytrace  rocprofv3 memory-copy trace of 3 traced steps, graph then host-issued
-#   copytrace1 the graph-mode copy trace alone (exit mapping dumped: TK_DUMP_MAPS)
-#   copytracetorch control: a torch-only process under the copy-trace flags
+#   copytrace  rocprofv3 memory-copy trace of bench.py's traced steps (graph mode), with one HSA
+#              runtime in the process (tools/rocprof_one_hsa.sh), summarised per step
+#   copytracetorch control: a torch-only process under plain rocprofv3 --memory-copy-trace (two HSA
+#              runtimes: the completion callbacks time out after 30 s and no copy is recorded)
 #   copytraceprobe  rocprofv3 memory-copy trace of tools/probe_copies (torch-free; bench under it crashes at exit)
 #   copyprobe  the step's 233 record copies isolated: host-issued, graph chains, packed chunks (tools/probe_copies)
 #   prof       rocprofv3 kernel-trace --stats of the default bench (compute + traced steps)
@@ -43,14 +44,11 @@ for r in "$@"; do
         --tune-table none --write-tune-table "$O/tune_table.json" --tune-report "$O/find_step.json" ;;
     host) run 400 bench_host.json python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --run-mode host ;;
     copytrace)
-      run 400 copytrace_graph.log rocprofv3 --memory-copy-trace --output-format csv -d "$O/copy_graph" -o run -- \
-        python3 -u bench.py --steps 3 --warmup 1 --skip-cpu
-      run 400 copytrace_host.log rocprofv3 --memory-copy-trace --output-format csv -d "$O/copy_host" -o run -- \
-        python3 -u bench.py --steps 3 --warmup 1 --skip-cpu --run-mode host ;;
-    copytrace1)  # graph mode only, with the exit mapping dumped for symbolising a crash at exit
-      run 400 copytrace_graph.log env TK_DUMP_MAPS="$O/maps.txt" rocprofv3 --memory-copy-trace --stats \
-        --output-format csv -d "$O/copy_graph" -o run -- python3 -u bench.py --steps 3 --warmup 1 --skip-cpu ;;
-    copytracetorch)  # control: torch alone (no libtachikoma) under the same profiler flags
+      run 400 copytrace.log bash tools/rocprof_one_hsa.sh --memory-copy-trace --kernel-trace --stats \
+        --output-format csv -d "$O/copy" -o run -- python3 -u bench.py --steps 3 --warmup 1 --skip-cpu \
+        --copy-trace "$O/copy_trace.json" &&
+      python3 tools/bench_copy_trace.py "$O/copy" "$O/copy_trace.json" "$O/bench_copy_trace.json" > /dev/null ;;
+    copytracetorch)  # control: torch alone under plain rocprofv3 (two HSA runtimes in the process)
       run 300 copytrace_torch.log rocprofv3 --memory-copy-trace --stats --output-format csv -d "$O/copy_torch" \
         -o run -- python3 -u tools/probe_torch_copies.py ;;
     copytraceprobe) run 300 copytrace_probe.log rocprofv3 --memory-copy-trace --stats --output-format csv \
