@@ -24,7 +24,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import subprocess
 import sys
 import time
@@ -322,6 +321,16 @@ def check_gpu_count(args) -> None:
                          f"RCCL), this host shows {have}; use --dist-backend gloo to rehearse N ranks on one GPU")
 
 
+def host_id() -> str:
+    """The physical host: its kernel's boot id (containers on one host share it; the hostname is
+    the container's).  Tells two boxes' runs apart in the line."""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            return f.read().strip()
+    except OSError:
+        return os.uname().nodename
+
+
 def mount_of(path: str):
     """(mount point, filesystem type, device) of the mount holding `path` (/proc/mounts)."""
     best = None
@@ -510,10 +519,13 @@ def main(argv=None) -> int:
     overlap_pick = None
     if writer is not None and args.file_overlap == "auto":
         # the sink's find step (untimed): overlapped vs serialised, 3 steps each, interleaved over
-        # 3 rounds (on, off, on, off, ...) so that a box's disk drifting between probes (10.5-16.7
-        # GB/s on one round-4 box) hits both modes alike; each mode's median round is compared
+        # 5 rounds (on, off, on, off, ...) so that a box's disk drifting between probes (10.5-16.7
+        # GB/s on one round-4 box) hits both modes alike; each mode's median over rounds 2-5 is
+        # compared (the first rounds run slow while the disk settles: r05r's on / off rounds were
+        # 860 / 985, 817 / 608, 555 / 606 ms per step, and a median over all three picked "off",
+        # frac 0.77, where the overlapped run reached 0.90)
         rounds = {"on": [], "off": []}
-        for _ in range(3):
+        for _ in range(5):
             for mode in ("on", "off"):
                 overlap_mode[0] = mode
                 step(0)
@@ -523,7 +535,7 @@ def main(argv=None) -> int:
                     step(i)
                 drain()
                 rounds[mode].append((time.perf_counter() - tp) / 3 * 1e3)
-        overlap_pick = {k: round(float(np.median(v)), 1) for k, v in rounds.items()}
+        overlap_pick = {k: round(float(np.median(v[1:])), 1) for k, v in rounds.items()}
         overlap_pick["rounds_ms"] = {k: [round(x, 1) for x in v] for k, v in rounds.items()}
         overlap_mode[0] = min(("on", "off"), key=lambda k: overlap_pick[k])
     if stop("pick"):
@@ -739,7 +751,7 @@ def main(argv=None) -> int:
             dist.barrier(group=host_group)
     per_step = {"min": round(min(step_gbps), 2), "max": round(max(step_gbps), 2),
                 "mean": round(sum(step_gbps) / len(step_gbps), 2)} if step_gbps else None
-    rank_info = {"rank": rank, "pci": placement["pci"], "numa_node": placement["numa_node"],
+    rank_info = {"rank": rank, "host": host_id(), "pci": placement["pci"], "numa_node": placement["numa_node"],
                  "cpus": placement["cpus"], "image_pages_per_node": image_pages,
                  "d2h": {"achieved_GBps": round(trace_bytes / (elapsed / args.steps) / 1e9, 2),
                          "measured_peak_GBps": round(d2h_peak, 2),
