@@ -474,6 +474,24 @@ typedef struct {
 int tk_qnn_conv2d_transpose(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
                             const tk_conv2d_transpose_attrs* attrs, void* stream);
 
+/* qnn.simulated_quantize / qnn.simulated_dequantize (src/relay/qnn/op/simulated_quantize.cc:36-78,
+ * simulated_dequantize.cc:36-76; compute python/tvm/topi/nn/qnn.py:40-190): float32 -> float32 of
+ * the same shape.  The dtype arrives as an int32 device scalar (SQNN codes: 1 int8, 2 uint8,
+ * 3 int32; any other value -- 0 "disable" -- passes the data through), so a graph may pick it at
+ * run time.  Element index i along `axis` uses scales[i % n_scales] and zero_points[i % n_zero_points]
+ * (tir.indexmod).  Per element, in float32 (the int32 zero point and integer bounds cast to float32):
+ *   quantize:   max(min(round(x / scale) + zp, qmax), qmin)     round = llvm.round (half away)
+ *   dequantize: (x - zp) * scale */
+typedef struct {
+  int32_t axis;                 /* -1 = last */
+  int32_t n_scales, n_zero_points;
+  const int32_t* dtype_code;    /* device, one int32 */
+  const float* scales;          /* device, n_scales */
+  const int32_t* zero_points;   /* device, n_zero_points */
+} tk_simq_attrs;
+int tk_qnn_simulated_quantize(const tk_tensor* data, tk_tensor* out, const tk_simq_attrs* attrs, void* stream);
+int tk_qnn_simulated_dequantize(const tk_tensor* data, tk_tensor* out, const tk_simq_attrs* attrs, void* stream);
+
 /* ---------------------------------------------------------------- executor
  * Native run loop replacing GraphExecutor::Run (graph_executor.cc:61-66) and
  * the debug executor's per-node copy-out (graph_executor_debug.cc:249-284).
@@ -510,6 +528,8 @@ enum {
   TK_NODE_LOOKUP = 27,     /* in: data; ext[0]: the 256-byte device table (qnn unary ops) */
   TK_NODE_BATCH_MATMUL = 28, /* in: x, y; attrs.dense (zero points); ext[0]: workspace */
   TK_NODE_CONV2D_TRANSPOSE = 29, /* in: data (NCHW), weight (IOHW); attrs.conv2d_transpose */
+  TK_NODE_SIM_QUANTIZE = 30,   /* in: data (float32); attrs.simq */
+  TK_NODE_SIM_DEQUANTIZE = 31, /* in: data (float32); attrs.simq */
 };
 
 #define TK_MAX_NODE_INPUTS 8
@@ -539,6 +559,7 @@ typedef struct {
     tk_transpose_attrs transpose;
     tk_leaky_relu_attrs leaky_relu;
     tk_conv2d_transpose_attrs conv2d_transpose;
+    tk_simq_attrs simq;
     struct { int64_t a_min, a_max; } clip;
     struct { int32_t axis; } bias_add;
   } attrs;

@@ -173,6 +173,12 @@ def eval_call(call, args, backend: str = "numpy", threads: int = 1):
                             out_dtype=a["out_dtype"])
     if op == "qnn.dequantize":
         return ref.dequantize(args[0], _const(call.args[1]), _const(call.args[2]), axis=a["axis"])
+    if op == "qnn.simulated_quantize":
+        return ref.simulated_quantize(args[0], int(np.asarray(args[1]).reshape(-1)[0]), args[2], args[3],
+                                      axis=a.get("axis", -1))
+    if op == "qnn.simulated_dequantize":
+        return ref.simulated_dequantize(args[0], int(np.asarray(args[1]).reshape(-1)[0]), args[2], args[3],
+                                        axis=a.get("axis", -1))
     if op == "transpose":
         return np.ascontiguousarray(np.transpose(args[0], a["axes"]))
     if op == "nn.bias_add":
@@ -243,6 +249,11 @@ def calibrate(mod, params: Dict[str, np.ndarray], inputs: Dict[str, np.ndarray],
             # a tuple is no op: it has no record and takes no symbol name (MRT's expr2symbol
             # names Calls and TupleGetItems, python/tvm/mrt/symbol.py:212-253)
             values[id(node)] = [values[id(f)] for f in node.fields]
+        elif kind == "Call" and node.op == "reshape" and type(node.args[0]).__name__ == "Constant":
+            # reshape of a constant (the [-1] reshapes the simulated_(de)quantize constructors put
+            # around their scale / zero point, relay/qnn/op/qnn.py:253-255): FoldConstant folds it
+            # into a constant when the reference builds the graph, so it is no op and no record
+            values[id(node)] = np.reshape(node.args[0].data, node.shape)
         elif kind == "Call":
             name = f"%{counter}"
             counter += 1

@@ -224,6 +224,17 @@ class tk_conv2d_transpose_attrs(ctypes.Structure):
     ]
 
 
+class tk_simq_attrs(ctypes.Structure):
+    _fields_ = [
+        ("axis", ctypes.c_int32),
+        ("n_scales", ctypes.c_int32),
+        ("n_zero_points", ctypes.c_int32),
+        ("dtype_code", ctypes.c_void_p),
+        ("scales", ctypes.c_void_p),
+        ("zero_points", ctypes.c_void_p),
+    ]
+
+
 class _clip(ctypes.Structure):
     _fields_ = [("a_min", ctypes.c_int64), ("a_max", ctypes.c_int64)]
 
@@ -250,6 +261,7 @@ class tk_node_attrs(ctypes.Union):
         ("transpose", tk_transpose_attrs),
         ("leaky_relu", tk_leaky_relu_attrs),
         ("conv2d_transpose", tk_conv2d_transpose_attrs),
+        ("simq", tk_simq_attrs),
         ("clip", _clip),
         ("bias_add", _bias_add),
     ]
@@ -289,6 +301,7 @@ NODE_KINDS = {
     "ewise": 17, "conv2d_f32": 18, "dense_f32": 19, "nn.pad": 20,
     "qnn.quantize": 21, "qnn.dequantize": 22, "qnn_binary": 23, "qnn.concatenate": 24, "transpose": 25,
     "qnn.leaky_relu": 26, "lookup": 27, "qnn.batch_matmul": 28, "qnn.conv2d_transpose": 29,
+    "qnn.simulated_quantize": 30, "qnn.simulated_dequantize": 31,
 }
 MAX_NODE_INPUTS = 8
 MAX_NODE_OUTPUTS = 6
@@ -347,6 +360,8 @@ SIGNATURES = {
     "tk_qnn_batch_matmul_workspace_bytes": (_I64, [_PT, _PT]),
     "tk_qnn_batch_matmul": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_dense_attrs), _VP, _VP]),
     "tk_qnn_conv2d_transpose": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_conv2d_transpose_attrs), _VP]),
+    "tk_qnn_simulated_quantize": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_simq_attrs), _VP]),
+    "tk_qnn_simulated_dequantize": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_simq_attrs), _VP]),
     "tk_find_scale_by_kl": (ctypes.c_int, [ctypes.POINTER(_I32), ctypes.POINTER(_F32), ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(_F32)]),
     "tk_module_create": (ctypes.c_int, [ctypes.POINTER(tk_node), ctypes.c_int, ctypes.POINTER(_VP)]),

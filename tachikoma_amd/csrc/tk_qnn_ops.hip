@@ -1,7 +1,8 @@
 // The QNN ops of a pre-quantized (frontend-produced) graph beside conv / dense / requantize / add:
-// qnn.quantize, qnn.dequantize, qnn.concatenate, qnn.mul, qnn.subtract (and qnn.add with
-// broadcasting / per-axis parameters), plus the transpose that carries NHWC / HWIO / OHWI / HWOI
-// qnn.conv2d operands to the NCHW / OIHW kernels.
+// qnn.quantize, qnn.dequantize, qnn.simulated_quantize / _dequantize, qnn.concatenate, qnn.mul,
+// qnn.subtract (and qnn.add with broadcasting / per-axis parameters), plus the transpose that
+// carries NHWC / HWIO / OHWI / HWOI qnn.conv2d operands to the NCHW / OIHW kernels (SURVEY.md §8(f)
+// row 1).
 //
 // All of them are HBM-bound streaming kernels (a few bytes in and out per element, a handful of
 // integer or float32 operations).  Integer steps wrap in int32 exactly where the reference's
@@ -601,6 +602,79 @@ int qnn_conv2d_transpose_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor*
   return is_int(w, 8) ? go((uint8_t)0, (int8_t)0) : go((uint8_t)0, (uint8_t)0);
 }
 
+// ---------------------------------------------------------------- simulated (de)quantize
+// topi.nn.simulated_quantize / simulated_dequantize (python/tvm/topi/nn/qnn.py:40-190), float32 in
+// and out.  The dtype code is read from device memory (a graph may compute it); every thread reads
+// the same word.  Float steps are single IEEE operations in topi's order: x / scale, llvm.round,
+// + float32(zp), min(., float32(qmax)), max(., float32(qmin)) -- TIR's binary-op type matching casts
+// the int32 zero point and the integer bounds to float32 (an int32 qmax of 2^31 - 1 becomes 2^31).
+__global__ __launch_bounds__(kQBlock) void sim_quantize_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                               int64_t n, const int32_t* __restrict__ code,
+                                                               const float* __restrict__ scales, int32_t ns,
+                                                               const int32_t* __restrict__ zps, int32_t nz,
+                                                               int32_t inner, int32_t C) {
+  const int32_t c0 = *code;
+  const bool on = c0 >= 1 && c0 <= 3;
+  const float qmin = c0 == 1 ? -128.0f : c0 == 2 ? 0.0f : -2147483648.0f;
+  const float qmax = c0 == 1 ? 127.0f : c0 == 2 ? 255.0f : 2147483648.0f;
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    float v = x[i];
+    if (on) {
+      const int c = chan(i, inner, C);
+      v = v / scales[c % ns];
+      v = roundf(v);  // llvm.round: halves away from zero
+      v = v + (float)zps[c % nz];
+      v = v < qmax ? v : qmax;
+      v = v > qmin ? v : qmin;
+    }
+    y[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(kQBlock) void sim_dequantize_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                                 int64_t n, const int32_t* __restrict__ code,
+                                                                 const float* __restrict__ scales, int32_t ns,
+                                                                 const int32_t* __restrict__ zps, int32_t nz,
+                                                                 int32_t inner, int32_t C) {
+  const int32_t c0 = *code;
+  const bool on = c0 >= 1 && c0 <= 3;
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    float v = x[i];
+    if (on) {
+      const int c = chan(i, inner, C);
+      v = (v - (float)zps[c % nz]) * scales[c % ns];
+    }
+    y[i] = v;
+  }
+}
+
+int qnn_simulated_impl(bool quant, const tk_tensor* x, tk_tensor* y, const tk_simq_attrs* a, hipStream_t s) {
+  const char* what = quant ? "qnn.simulated_quantize" : "qnn.simulated_dequantize";
+  TK_CHECK_ARG(x && y && a, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y) && numel(x) == numel(y), "bad tensors");
+  if (!is_f32(x) || !is_f32(y)) {
+    set_error(std::string(what) + ": float32 data and output expected");
+    return TK_ERR_DTYPE;
+  }
+  if (!a->dtype_code || !a->scales || !a->zero_points || a->n_scales < 1 || a->n_zero_points < 1) {
+    set_error(std::string(what) + ": dtype code, scales and zero points are required device arrays");
+    return TK_ERR_INVALID_ARG;
+  }
+  int32_t inner, C;
+  if (x->ndim < 1 || !axis_inner(x, a->axis, &inner, &C)) {
+    set_error(std::string(what) + ": bad axis");
+    return TK_ERR_INVALID_ARG;
+  }
+  const int64_t n = numel(x);
+  hipLaunchKernelGGL(quant ? sim_quantize_kernel : sim_dequantize_kernel, dim3(qgrid(n)), dim3(kQBlock), 0, s,
+                     (const float*)ptr(x), (float*)ptr(y), n, a->dtype_code, a->scales, a->n_scales, a->zero_points,
+                     a->n_zero_points, inner, C);
+  TK_LAUNCH_CHECK();
+  return TK_OK;
+}
+
 }  // namespace tk
 
 extern "C" {
@@ -631,6 +705,12 @@ int tk_qnn_lookup(const tk_tensor* data, tk_tensor* out, const void* table, void
 int tk_qnn_conv2d_transpose(const tk_tensor* data, const tk_tensor* weight, tk_tensor* out,
                             const tk_conv2d_transpose_attrs* attrs, void* stream) {
   return tk::qnn_conv2d_transpose_impl(data, weight, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_simulated_quantize(const tk_tensor* data, tk_tensor* out, const tk_simq_attrs* attrs, void* stream) {
+  return tk::qnn_simulated_impl(true, data, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_simulated_dequantize(const tk_tensor* data, tk_tensor* out, const tk_simq_attrs* attrs, void* stream) {
+  return tk::qnn_simulated_impl(false, data, out, attrs, tk::as_stream(stream));
 }
 
 }  // extern "C"

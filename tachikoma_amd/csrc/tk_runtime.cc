@@ -67,6 +67,7 @@ int transpose_impl(const tk_tensor* x, tk_tensor* y, const tk_transpose_attrs* a
 int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, const tk_block_attrs* attrs,
                             int32_t* algos, int max_algos);
 int qnn_leaky_relu_impl(const tk_tensor* x, tk_tensor* y, const tk_leaky_relu_attrs* a, hipStream_t s);
+int qnn_simulated_impl(bool quant, const tk_tensor* x, tk_tensor* y, const tk_simq_attrs* a, hipStream_t s);
 int qnn_lookup_impl(const tk_tensor* x, tk_tensor* y, const void* table, hipStream_t s);
 int qnn_conv2d_transpose_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, const tk_conv2d_transpose_attrs* a,
                               hipStream_t s);
@@ -220,6 +221,9 @@ static int run_node(Node& n, hipStream_t s) {
       return batch_matmul_impl(i0, i1, o, &d.attrs.dense, d.ext[0], s);
     case TK_NODE_CONV2D_TRANSPOSE:
       return qnn_conv2d_transpose_impl(i0, i1, o, &d.attrs.conv2d_transpose, s);
+    case TK_NODE_SIM_QUANTIZE:
+    case TK_NODE_SIM_DEQUANTIZE:
+      return qnn_simulated_impl(d.kind == TK_NODE_SIM_QUANTIZE, i0, o, &d.attrs.simq, s);
   }
   set_error("tk_module: unknown node kind " + std::to_string(d.kind));
   return TK_ERR_INVALID_ARG;

@@ -181,6 +181,10 @@ def lower(mod, params: Optional[Dict[str, Any]] = None) -> Plan:
                 inputs.append(t)
         elif isinstance(node, (Constant, Tuple)):
             continue  # a tuple is no op: no record, no symbol name (expr.Tuple)
+        elif _folded_const(node) is not None:
+            # reshape of a constant (the simulated_(de)quantize constructors' [-1] reshapes): the
+            # reference's FoldConstant makes it a constant when the graph is built -- no op, no name
+            names[id(node)] = None
         elif isinstance(node, Call):
             name = f"%{counter}"
             counter += 1
@@ -193,10 +197,19 @@ def lower(mod, params: Optional[Dict[str, Any]] = None) -> Plan:
     return Plan(inputs, plist, ops, [out])
 
 
+def _folded_const(e: Expr) -> Optional[np.ndarray]:
+    """The value of a constant or of ``reshape(constant)`` (which FoldConstant folds), else None."""
+    if isinstance(e, Constant):
+        return e.data
+    if isinstance(e, Call) and e.op == "reshape" and isinstance(e.args[0], Constant):
+        return np.reshape(e.args[0].data, e.shape)
+    return None
+
+
 def _tensor_args(call: Call, k: int, names) -> List[str]:
     out = []
     for a in call.args[:k]:
-        if isinstance(a, Constant):
+        if isinstance(a, Constant) or names.get(id(a), "") is None:
             raise UnsupportedError(f"{call.op}: constant tensor operands must be passed as params (MRT symbols)")
         out.append(names[id(a)])
     return out
@@ -407,6 +420,34 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
         else:
             a["zero_point"] = 0
             consts["zero_points"] = zv.reshape(-1)
+    elif op in ("qnn.simulated_quantize", "qnn.simulated_dequantize"):
+        # topi.nn.simulated_(de)quantize (python/tvm/topi/nn/qnn.py:40-190): the dtype code, scale
+        # and zero point are tensors -- constants (folded, uploaded with the node) or graph tensors
+        # (read on the device when the node runs, so the dtype may be chosen at run time)
+        ins = _tensor_args(call, 1, names)
+        if call.args[0].dtype != "float32" or len(call.shape) < 1:
+            raise UnsupportedError(f"{op}: float32 data of rank >= 1")
+        a["axis"] = _norm_axis(a.get("axis", -1), len(call.shape))
+        if not 0 <= a["axis"] < len(call.shape):
+            raise TypeError(f"{op}: axis {a['axis']} out of range for {call.shape}")
+        srcs = {}
+        for k, (key, dt) in enumerate((("dtype_code", np.int32), ("scales", np.float32), ("zero_points", np.int32)),
+                                      start=1):
+            arg = call.args[k]
+            v = _folded_const(arg)
+            if arg.dtype != np.dtype(dt).name:
+                raise TypeError(f"{op}: {key} must be {np.dtype(dt).name}, got {arg.dtype}")
+            if v is not None:
+                consts[key] = np.asarray(v, dt).reshape(-1)
+                srcs[key] = -1
+            else:
+                ins.append(names[id(arg)])
+                srcs[key] = len(ins) - 1
+            n = int(np.prod(arg.shape)) if arg.shape else 1
+            if n < 1 or (key == "dtype_code" and n != 1):
+                raise TypeError(f"{op}: {key} has {n} values")
+            a["n_" + key] = n
+        a["sources"] = srcs
     elif op == "qnn.leaky_relu":
         # QnnLeakyReluCanonicalize (leaky_relu.cc:85-140): RequantizeOrUpcast to the output params,
         # then the alpha / (1 - alpha) fixed-point multiplies

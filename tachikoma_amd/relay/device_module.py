@@ -212,6 +212,12 @@ class DeviceModule:
         self._keep.append(r)
         return r
 
+    def _dev_const(self, arr: np.ndarray):
+        """A node constant on the device in its own dtype (kept alive with the module)."""
+        t = _torch().from_numpy(np.ascontiguousarray(arr)).to(self.device)
+        self._keep.append(t)
+        return t
+
     def _dev_i32(self, arr: np.ndarray):
         torch = _torch()
         t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int32)).to(self.device)
@@ -424,6 +430,16 @@ class DeviceModule:
                     self._keep.append(table)
                     self.tables[op.name] = table
                     n.ext[0] = table.data_ptr()
+                elif kind in ("qnn.simulated_quantize", "qnn.simulated_dequantize"):
+                    n.kind = _lib.NODE_KINDS[kind]
+                    sq = n.attrs.simq
+                    sq.axis = a["axis"]
+                    sq.n_scales, sq.n_zero_points = a["n_scales"], a["n_zero_points"]
+                    # each parameter is a folded constant uploaded here or a graph tensor's buffer
+                    # (read on the device when the node runs)
+                    src = {key: (self._dev_const(op.consts[key]) if k < 0 else self.buffers[op.inputs[k]]).data_ptr()
+                           for key, k in a["sources"].items()}
+                    sq.dtype_code, sq.scales, sq.zero_points = src["dtype_code"], src["scales"], src["zero_points"]
                 elif kind == "qnn.batch_matmul":
                     n.kind = _lib.NODE_KINDS[kind]
                     self._dense_attrs(n.attrs.dense, op)

@@ -56,6 +56,8 @@ _PATTERNS = {
     # the unary ops to take (injective), batch_matmul / conv2d_transpose to their nn ops
     "qnn.leaky_relu": kBroadcast, "qnn.batch_matmul": kOutEWiseFusable, "qnn.conv2d_transpose": kOutEWiseFusable,
     **{f"qnn.{u}": kInjective for u in ("sqrt", "rsqrt", "exp", "erf", "sigmoid", "hardswish", "tanh", "log", "abs")},
+    # the simulated ops register OpPattern.ELEMWISE themselves (relay/qnn/op/_qnn.py:39,53)
+    "qnn.simulated_quantize": kElemWise, "qnn.simulated_dequantize": kElemWise,
     "annotation.stop_fusion": kOpaque, "annotation.cast_hint": kOpaque,
     "tachikoma.qnn.conv2d": kOpaque, "tachikoma.qnn.dense": kOpaque,  # external (BYOC) functions
 }

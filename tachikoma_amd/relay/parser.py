@@ -175,6 +175,8 @@ def _call(op: str, args: List[Expr], attrs: Dict[str, Any]) -> Expr:
             if op == "qnn.leaky_relu":  # alpha is an attribute, the constructor's second argument
                 return _qnn.leaky_relu(args[0], a.pop("alpha"), *args[1:], **a)
             return getattr(_qnn, op.split(".")[1])(*args, **a)
+        if op in ("qnn.simulated_quantize", "qnn.simulated_dequantize"):
+            return _qnn.simulated_call(op, *args, **a)
         if op == "transpose":
             return _op.transpose(*args, **a)
         if op == "nn.bias_add":

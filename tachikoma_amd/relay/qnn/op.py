@@ -14,6 +14,7 @@ import numpy as np
 
 from ..expr import Call, Constant, Expr, TensorType, Tuple, const
 from ..op import _broadcast_shape, _check_int, _tuple2, get_pad_tuple2d
+from ..op import reshape as _reshape
 
 _cfg = threading.local()
 
@@ -256,6 +257,55 @@ def dequantize(data: Expr, input_scale, input_zero_point, axis: int = -1) -> Cal
     _axis_param(s, data.shape, axis, "qnn.dequantize")
     _axis_param(z, data.shape, axis, "qnn.dequantize")
     return Call("qnn.dequantize", [data, s, z], {"axis": int(axis)}, TensorType(data.shape, "float32"))
+
+
+# SQNN_DTYPE_TO_CODE (python/tvm/topi/nn/qnn.py:22-33): the simulated ops take their dtype as an
+# int32 tensor, so a graph may choose it at run time
+SQNN_DTYPE_TO_CODE = {"disable": 0, "int8": 1, "uint8": 2, "int32": 3}
+
+
+def _sqnn(data: Expr, dtype, scale, zero_point, op: str):
+    if data.dtype != "float32":
+        raise TypeError(f"{op}: float32 data expected, got {data.dtype}")
+    if isinstance(dtype, str):
+        if dtype not in SQNN_DTYPE_TO_CODE:
+            raise ValueError(f"{op}: dtype must be one of {sorted(SQNN_DTYPE_TO_CODE)}, got {dtype!r}")
+        code = const(SQNN_DTYPE_TO_CODE[dtype], "int32")
+    else:
+        code = _c(dtype, "int32")
+        if code.dtype != "int32" or int(np.prod(code.checked_type.shape)) != 1:
+            raise TypeError(f"{op}: the dtype code must be one int32 value")
+    # the constructor wraps both parameters in reshape(-1) (relay/qnn/op/qnn.py:253-255, 320-322)
+    s = _reshape(_c(scale, "float32"), [-1])
+    z = _reshape(_c(zero_point, "int32"), [-1])
+    if s.dtype != "float32" or z.dtype != "int32":
+        raise TypeError(f"{op}: float32 scale and int32 zero point expected")
+    return code, s, z
+
+
+def simulated_quantize(data: Expr, output_scale, output_zero_point, axis: int = -1, out_dtype="int8") -> Call:
+    """``qnn.simulated_quantize`` (src/relay/qnn/op/simulated_quantize.cc:36-78, constructor
+    python/tvm/relay/qnn/op/qnn.py:221-256): float32 → float32 holding the quantized values;
+    ``out_dtype`` is a dtype name or an int32 tensor of an SQNN code, the scale / zero point a
+    scalar or one value per channel along ``axis`` (taken modulo their length)."""
+    code, s, z = _sqnn(data, out_dtype, output_scale, output_zero_point, "qnn.simulated_quantize")
+    return Call("qnn.simulated_quantize", [data, code, s, z], {"axis": int(axis)}, TensorType(data.shape, data.dtype))
+
+
+def simulated_call(op: str, data: Expr, dtype_code: Expr, scale: Expr, zero_point: Expr, axis: int = -1) -> Call:
+    """The simulated op as Relay text spells it -- (data, dtype code, scale, zero point), the
+    parameters already 1-D (MakeSimulatedQuantize / MakeSimulatedDequantize) -- for the parser."""
+    if data.dtype != "float32":
+        raise TypeError(f"{op}: float32 data expected, got {data.dtype}")
+    return Call(op, [data, dtype_code, scale, zero_point], {"axis": int(axis)}, TensorType(data.shape, data.dtype))
+
+
+def simulated_dequantize(data: Expr, input_scale, input_zero_point, axis: int = -1, in_dtype="int8") -> Call:
+    """``qnn.simulated_dequantize`` (src/relay/qnn/op/simulated_dequantize.cc:36-76, constructor
+    python/tvm/relay/qnn/op/qnn.py:288-323): float32 → float32, ``(x - zp) * scale``."""
+    code, s, z = _sqnn(data, in_dtype, input_scale, input_zero_point, "qnn.simulated_dequantize")
+    return Call("qnn.simulated_dequantize", [data, code, s, z], {"axis": int(axis)},
+                TensorType(data.shape, data.dtype))
 
 
 def _scalar_param(p: Expr, what: str) -> None:

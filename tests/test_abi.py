@@ -50,7 +50,8 @@ int main(void) {
   O(tk_qparams_attrs, zero_points) O(tk_qnn_binary_attrs, out) O(tk_qnn_binary_attrs, output_zero_point)
   O(tk_concat_attrs, rq)
   P(tk_leaky_relu_attrs) P(tk_conv2d_transpose_attrs) O(tk_leaky_relu_attrs, alpha_multiplier)
-  O(tk_leaky_relu_attrs, zp_shift) O(tk_conv2d_transpose_attrs, kernel_zero_points)
+  O(tk_leaky_relu_attrs, zp_shift) O(tk_conv2d_transpose_attrs, kernel_zero_points) P(tk_simq_attrs)
+  O(tk_simq_attrs, dtype_code) O(tk_simq_attrs, zero_points)
   return 0;
 }
 """
@@ -93,6 +94,9 @@ def test_ctypes_layout_matches_c(tmp_path):
         "tk_leaky_relu_attrs.alpha_multiplier": _lib.tk_leaky_relu_attrs.alpha_multiplier.offset,
         "tk_leaky_relu_attrs.zp_shift": _lib.tk_leaky_relu_attrs.zp_shift.offset,
         "tk_conv2d_transpose_attrs.kernel_zero_points": _lib.tk_conv2d_transpose_attrs.kernel_zero_points.offset,
+        "tk_simq_attrs": ctypes.sizeof(_lib.tk_simq_attrs),
+        "tk_simq_attrs.dtype_code": _lib.tk_simq_attrs.dtype_code.offset,
+        "tk_simq_attrs.zero_points": _lib.tk_simq_attrs.zero_points.offset,
     }
     for k, v in py.items():
         assert int(got[k]) == v, (k, got[k], v)

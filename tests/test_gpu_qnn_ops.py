@@ -456,3 +456,47 @@ def test_round5_ops_in_one_graph_text(device, tmp_path):
         m.dump_trace(path)
         _check(read_trace(path, copy=True).records, exp)
         m.close()
+
+
+# ---------------------------------------------------------------- simulated (de)quantize
+
+@pytest.mark.parametrize("dt", ["int8", "uint8", "int32", "disable"])
+@pytest.mark.parametrize("axis,ns,nz", [(1, 7, 7), (-1, 1, 1), (2, 2, 3)])
+def test_simulated_ops_random(device, tmp_path, dt, axis, ns, nz):
+    """qnn.simulated_quantize -> qnn.simulated_dequantize with constant parameters: per-tensor,
+    per-channel, and fewer values than the axis has (taken modulo their count)."""
+    rng = np.random.default_rng(13)
+    shape = (3, 7, 5, 9)
+    s = rng.uniform(0.01, 0.3, ns).astype(np.float32)
+    z = rng.integers(-10, 10, nz).astype(np.int32) + (100 if dt == "uint8" else 0)
+    x = (rng.standard_normal(shape) * 40).astype(np.float32)
+    # exact halves, values past every clip bound, -0.0 (all in channel 0 of the three axes)
+    x.reshape(-1)[:6] = [0.5 * s[0], -0.5 * s[0], 1e10, -1e10, -0.0, 2.5 * s[0]]
+    v = relay.var("x", shape, "float32")
+    q = qnn.op.simulated_quantize(v, relay.const(s), relay.const(z), axis=axis, out_dtype=dt)
+    d = qnn.op.simulated_dequantize(q, relay.const(s), relay.const(z), axis=axis, in_dtype=dt)
+    rec, exp = _trace(d, {"x": x}, tmp_path)
+    _check(rec, exp)
+
+
+def test_simulated_ops_dynamic_params(device, tmp_path):
+    """The dtype code, scales and zero points as graph inputs (test_op_qnn_simulated_quantize.py's
+    dynamic dtype / dynamic channels cases): one module, run with several codes and parameter sets
+    without rebuilding; each trace bit-exact vs the oracle."""
+    rng = np.random.default_rng(17)
+    shape = (2, 5, 8)
+    x = (rng.standard_normal(shape) * 30).astype(np.float32)
+    vx = relay.var("x", shape, "float32")
+    vs, vz, vc = relay.var("scale", (2,), "float32"), relay.var("zp", (2,), "int32"), relay.var("dtype", (1,), "int32")
+    q = qnn.op.simulated_quantize(vx, vs, vz, axis=1, out_dtype=vc)
+    d = qnn.op.simulated_dequantize(q, vs, vz, axis=1, in_dtype=vc)
+    mod = relay.IRModule.from_expr(d)
+    m = graph_executor.GraphModule(relay.build(mod, target="mi355x", params={})["default"]())
+    for code, s, z in [(2, [0.5, 0.25], [127, 123]), (3, [0.5, 0.5], [127, 127]), (1, [0.1, 0.3], [-3, 4]),
+                       (0, [0.5, 0.25], [1, 2])]:
+        inputs = {"x": x, "scale": np.array(s, np.float32), "zp": np.array(z, np.int32),
+                  "dtype": np.array([code], np.int32)}
+        m.set_input(**inputs)
+        path = str(tmp_path / f"t{code}.tkt")
+        m.dump_trace(path)
+        _check(read_trace(path, copy=True).records, graph_ref.calibrate(mod, {}, inputs))

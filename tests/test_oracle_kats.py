@@ -245,3 +245,69 @@ def test_conv2d_transpose_oracle_matches_topi_definition(cfg):
                                    groups=groups)
     exp = _conv2d_transpose_topi(d, w, zd, zw, st, pad, opad, groups)
     np.testing.assert_array_equal(got, exp)
+
+
+# ---------------------------------------------------------------- simulated (de)quantize
+# test_op_qnn_simulated_{quantize,dequantize}.py hold no literals: each case checks that the
+# simulated op equals qnn.quantize / qnn.dequantize on the same data and parameters (allowing 3
+# mismatches for GPU float32).  The same cases, seeded, and the equality exact -- both sides are
+# restated from the reference's float32 steps (quantize.cc:113-149 vs topi/nn/qnn.py:40-190).
+SIM_CASES = [
+    # (name, data range, shape, data dtype, scale, zero point, axis, dtype)
+    ("simple_uint8", (-128, 127), (2, 5), "float32", 0.5, 127, -1, "uint8"),
+    ("simple_int8", (-128, 127), (2, 5), "float32", 0.5, 127, -1, "int8"),
+    ("simple_int32", (-128, 127), (2, 5), "float32", 0.5, 127, -1, "int32"),
+    ("dynamic_channels_scalar", (-64, 64), (2, 5), "float32", [0.5], [127], 0, "uint8"),
+    ("dynamic_channels_per_channel", (-64, 64), (2, 5), "float32", [0.5, 0.25], [127, 123], 0, "uint8"),
+    ("dynamic_dtype_uint8", (-64, 64), (2, 5), "float32", [0.5], [127], -1, "uint8"),
+    ("dynamic_dtype_int32", (-64, 64), (2, 5), "float32", [0.5], [127], -1, "int32"),
+]
+
+
+@pytest.mark.parametrize("case", SIM_CASES, ids=lambda c: c[0])
+def test_simulated_quantize_equals_quantize(case):
+    _, (lo, hi), shape, _, s, z, axis, dt = case
+    x = np.random.default_rng(3).uniform(lo, hi, shape).astype(np.float32)
+    x.reshape(-1)[:3] = [0.25, -0.75, 1e10]  # exact halves after / 0.5, past the int32 bound
+    code = ref.SQNN_DTYPE_TO_CODE[dt]
+    sim = ref.simulated_quantize(x, code, np.asarray(s, np.float32), np.asarray(z, np.int32), axis=axis)
+    sv, zv = np.asarray(s, np.float32), np.asarray(z, np.int32)
+    q = ref.quantize(x, sv if sv.size > 1 else sv.reshape(()), zv if zv.size > 1 else zv.reshape(()), axis=axis,
+                     out_dtype=dt)
+    if dt == "int32":
+        # quantize's fptosi of the clipped 2^31 is INT32_MIN (x86 cvttss2si); the simulated op keeps
+        # the float 2^31 -- the one place the two differ, where the reference test allows mismatches
+        big = sim >= 2.0 ** 31
+        assert big.sum() == 1 and q[big][0] == np.iinfo(np.int32).min
+        q = np.where(big, np.float32(2.0 ** 31), q.astype(np.float32))
+    np.testing.assert_array_equal(sim, q.astype(np.float32))
+
+
+@pytest.mark.parametrize("case", [
+    ("simple_uint8", (-128, 127), "uint8", 0.5, 127, -1),
+    ("simple_int8", (-128, 127), "int8", 0.5, 127, -1),
+    ("dynamic_channels_scalar", (-64, 64), "int8", [0.5], [0], 0),
+    ("dynamic_channels_per_channel", (-64, 64), "int8", [0.5, 0.25], [127, 123], 0),
+    ("dynamic_dtype_uint8", (0, 255), "uint8", [0.5], [127], -1),
+    ("dynamic_dtype_int8", (0, 255), "int8", [0.5], [127], -1),
+], ids=lambda c: c[0])
+def test_simulated_dequantize_equals_dequantize(case):
+    _, (lo, hi), dt, s, z, axis = case
+    d = np.random.default_rng(4).uniform(lo, hi, (2, 5)).astype(dt)
+    sim = ref.simulated_dequantize(d.astype(np.float32), ref.SQNN_DTYPE_TO_CODE[dt], np.asarray(s, np.float32),
+                                   np.asarray(z, np.int32), axis=axis)
+    sv, zv = np.asarray(s, np.float32), np.asarray(z, np.int32)
+    dq = ref.dequantize(d, sv if sv.size > 1 else sv.reshape(()), zv if zv.size > 1 else zv.reshape(()), axis=axis)
+    np.testing.assert_array_equal(sim, dq)
+
+
+def test_simulated_ops_pass_through_and_modulo_indexing():
+    x = np.array([[1.3, -2.5, 7.0, 300.0, -0.5]], np.float32)
+    for code in (0, 4, -1):  # "disable" and any code outside the if_then_else chain
+        np.testing.assert_array_equal(ref.simulated_quantize(x, code, [0.5], [1]), x)
+        np.testing.assert_array_equal(ref.simulated_dequantize(x, code, [0.5], [1]), x)
+    # 2 scales / 3 zero points on a 5-wide axis: element i takes scale[i % 2], zp[i % 3] (tir.indexmod)
+    got = ref.simulated_quantize(x, 1, [0.5, 1.0], [0, 1, 2], axis=1)
+    np.testing.assert_array_equal(got, np.array([[3.0, -2.0, 16.0, 127.0, 0.0]], np.float32))
+    got = ref.simulated_dequantize(np.array([[4.0, 4.0, 4.0, 4.0, 4.0]], np.float32), 2, [0.5, 1.0], [0, 1, 2], axis=1)
+    np.testing.assert_array_equal(got, np.array([[2.0, 3.0, 1.0, 4.0, 1.5]], np.float32))

@@ -147,3 +147,42 @@ def test_type_errors():
     with pytest.raises(NotImplementedError):
         qnn.op.conv2d(relay.var("d", (1, 4, 4, 3), "int8"), relay.var("k", (3, 3, 3, 4), "int8"), 0, 0, 1.0, 1.0,
                       kernel_size=(3, 3), channels=4, data_layout="NCWH")
+
+
+def test_simulated_ops_lowering_and_text():
+    """qnn.simulated_quantize / _dequantize: the constructor's reshape(-1) of constant parameters
+    folds (FoldConstant) -- no op, no MRT name -- and the constants ride with the node; graph-tensor
+    parameters stay tensors the node reads; Relay text round-trips to the same plan."""
+    from tachikoma_amd.relay.build_module import lower
+    x = relay.var("x", shape=(2, 3, 4), dtype="float32")
+    y = qnn.op.simulated_quantize(x, relay.const(np.array([0.5, 0.25, 0.125], np.float32)), relay.const(3), axis=1,
+                                  out_dtype="int8")
+    code = relay.var("code", shape=(1,), dtype="int32")
+    zp = relay.var("zp", shape=(2,), dtype="int32")
+    z = qnn.op.simulated_dequantize(y, relay.const(0.5), zp, axis=-1, in_dtype=code)
+    mod = relay.IRModule.from_expr(relay.Function([x, code, zp], z))
+    plan = lower(mod, {})
+    assert [o.op for o in plan.ops] == ["qnn.simulated_quantize", "reshape", "qnn.simulated_dequantize"]
+    q, r, d = plan.ops
+    assert q.name == "%0" and q.attrs["axis"] == 1 and q.attrs["sources"] == {"dtype_code": -1, "scales": -1,
+                                                                                  "zero_points": -1}
+    np.testing.assert_array_equal(q.consts["dtype_code"], [1])
+    np.testing.assert_array_equal(q.consts["scales"], np.array([0.5, 0.25, 0.125], np.float32))
+    assert r.inputs == ["zp"] and d.inputs == ["%0", "code", "%1"]
+    assert d.attrs["axis"] == 2 and d.attrs["sources"] == {"dtype_code": 1, "scales": -1, "zero_points": 2}
+    assert d.attrs["n_zero_points"] == 2 and "zero_points" not in d.consts
+    again = lower(relay.parse(mod.astext()), {})
+    assert [o.describe() for o in again.ops] == [o.describe() for o in plan.ops]
+    # the oracle walker folds the same reshape and names the same records
+    rng = np.random.default_rng(2)
+    inputs = {"x": rng.standard_normal((2, 3, 4)).astype(np.float32) * 9, "code": np.array([2], np.int32),
+              "zp": np.array([1, -1], np.int32)}
+    rec = graph_ref.calibrate(mod, {}, inputs)
+    assert sorted(rec) == sorted(["x", "code", "zp", "%0", "%1", "%2"])
+    e0 = ref.simulated_quantize(inputs["x"], 1, [0.5, 0.25, 0.125], [3], axis=1)
+    np.testing.assert_array_equal(rec["%0"], e0)
+    np.testing.assert_array_equal(rec["%2"], ref.simulated_dequantize(e0, 2, [0.5], [1, -1], axis=-1))
+    with pytest.raises(TypeError):
+        qnn.op.simulated_quantize(relay.var("i", shape=(2,), dtype="int8"), 0.5, 0)
+    with pytest.raises(ValueError):
+        qnn.op.simulated_quantize(x, 0.5, 0, out_dtype="int16")
