@@ -824,8 +824,11 @@ def lift_constants(mod, params: Dict[str, np.ndarray]):
         if not isinstance(n, Call):
             continue
         # tensor operands only: a QNN op's scale / zero-point arguments stay constants
-        if n.op in ("qnn.requantize", "qnn.quantize", "qnn.dequantize", "qnn.concatenate"):
+        if n.op in ("qnn.requantize", "qnn.quantize", "qnn.dequantize", "qnn.concatenate", "qnn.simulated_quantize",
+                    "qnn.simulated_dequantize"):
             k = 1
+        elif n.op == "reshape" and isinstance(n.args[0], Constant):
+            k = 0  # a reshaped constant (the simulated ops' parameters) folds in lower(), like FoldConstant
         elif n.op.startswith("qnn."):
             k = 2
         else:

@@ -186,3 +186,14 @@ def test_simulated_ops_lowering_and_text():
         qnn.op.simulated_quantize(relay.var("i", shape=(2,), dtype="int8"), 0.5, 0)
     with pytest.raises(ValueError):
         qnn.op.simulated_quantize(x, 0.5, 0, out_dtype="int16")
+
+
+def test_simulated_ops_build_keeps_parameter_constants():
+    """relay.build lifts tensor constants of ordinary ops into params; the simulated ops' reshaped
+    per-channel parameters must stay constants (folded, no reshape op, no record)."""
+    x = relay.var("x", shape=(2, 7, 3), dtype="float32")
+    s = np.linspace(0.1, 0.7, 7).astype(np.float32)
+    q = qnn.op.simulated_quantize(x, relay.const(s), relay.const(np.arange(7, dtype=np.int32)), axis=1)
+    lib = build(relay.IRModule.from_expr(q), target="mi355x", params={})
+    assert [o.op for o in lib.plan.ops] == ["qnn.simulated_quantize"]
+    np.testing.assert_array_equal(lib.plan.ops[0].consts["scales"], s)
