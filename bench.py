@@ -322,6 +322,15 @@ def check_gpu_count(args) -> None:
                          f"RCCL), this host shows {have}; use --dist-backend gloo to rehearse N ranks on one GPU")
 
 
+def pick_overlap(rounds: dict) -> dict:
+    """The file sink's overlap pick from interleaved rounds of ms per step, {"on": [...], "off":
+    [...]}: each mode's median over the rounds after the first (the disk settles during the first
+    round), the faster mode picked (ties go to "on")."""
+    med = {k: round(float(np.median(v[1:] if len(v) > 1 else v)), 1) for k, v in rounds.items()}
+    return dict(med, pick=min(("on", "off"), key=lambda k: med[k]),
+                rounds_ms={k: [round(x, 1) for x in v] for k, v in rounds.items()})
+
+
 def host_id() -> str:
     """The physical host: its kernel's boot id (containers on one host share it; the hostname is
     the container's).  Tells two boxes' runs apart in the line."""
@@ -536,9 +545,8 @@ def main(argv=None) -> int:
                     step(i)
                 drain()
                 rounds[mode].append((time.perf_counter() - tp) / 3 * 1e3)
-        overlap_pick = {k: round(float(np.median(v[1:])), 1) for k, v in rounds.items()}
-        overlap_pick["rounds_ms"] = {k: [round(x, 1) for x in v] for k, v in rounds.items()}
-        overlap_mode[0] = min(("on", "off"), key=lambda k: overlap_pick[k])
+        overlap_pick = pick_overlap(rounds)
+        overlap_mode[0] = overlap_pick["pick"]
     if stop("pick"):
         return 0
     for i in range(args.warmup):

@@ -130,3 +130,17 @@ def test_pmc_traffic_picks_library_then_stamp(tmp_path, monkeypatch):
     assert got["source"] == os.path.join("profiles", "r01_pmc_block.json") and got["library_match"]
     assert got["per_launch"] == 1.0
     assert bench.pmc_traffic("resnet18", 64, "current") is None
+
+
+def test_file_sink_overlap_pick():
+    """The r05r box: on / off rounds 860 / 985, 817 / 608, 555 / 606 ms per step -- a median over
+    all rounds picked "off" (frac 0.77 where overlap reached 0.90); without the first round the
+    later rounds decide."""
+    import bench
+    r05r = bench.pick_overlap({"on": [860.4, 817.3, 554.9, 550.0, 548.0], "off": [985.5, 607.9, 606.0, 605.0, 607.0]})
+    assert r05r["pick"] == "on" and r05r["on"] < r05r["off"]
+    r05q = bench.pick_overlap({"on": [647.1, 539.9, 546.4, 541.0, 543.0], "off": [586.8, 589.6, 589.4, 588.0, 590.0]})
+    assert r05q["pick"] == "on"
+    slow_disk = bench.pick_overlap({"on": [700.0, 690.0, 705.0, 698.0, 702.0], "off": [650.0, 640.0, 655.0, 645.0, 650.0]})
+    assert slow_disk["pick"] == "off"
+    assert bench.pick_overlap({"on": [500.0], "off": [600.0]})["pick"] == "on"
