@@ -489,6 +489,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     // walk position of a group past the end still lies inside the staging tile)
     auto load = [&](int r, int base, int p, int gi, v4u& v, EpiRow& ra, EpiRow& rb, uint32_t& res)
         __attribute__((always_inline)) {
+      if (TK_ABL(1 << 25)) {  // (ablation build: no LDS reads in the walk -- values from registers)
+        v = v4u{(uint32_t)base, (uint32_t)gi, 7u, (uint32_t)r};
+        ra = rb = row_pre;
+        res = 0x01010101u;
+        return;
+      }
       ra = rowc[min(r, R - 1)];
       if constexpr (ROWU) {
         v = *reinterpret_cast<const v4u*>(tileI + base);
