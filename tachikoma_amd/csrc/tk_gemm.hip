@@ -262,36 +262,50 @@ gemm_i8_kernel(GemmArgs g) {
       row_pre.zp = raw(g.rq.zps, g.rq.zps != nullptr);
     }
   }
-  // residual bytes of every row this thread writes (4-column epilogue paths), issued before
-  // the main loop: they are older than every stage load, so the first stage wait also
-  // covers them and the epilogue never waits on HBM latency
+  // residual bytes of every row this thread writes (4-column and flat epilogue paths).  kNR
+  // loads, every one issued (a thread with nothing to join reads the zero words), so that the
+  // counted waits below know them: on the LDS-DMA path they go out right after the prologue's
+  // stages -- the stage waits let them stay in flight, the epilogue stores its conv / bias_add /
+  // requantize records before it needs them -- because in the network the residual is a record
+  // written several kernels earlier and comes from HBM behind the CU's stores (the 56x56
+  // expands ran 115 us with a cached residual and 153 us with a cold one, r05w); elsewhere
+  // they are issued here, before the main loop.
+  static_assert(kFlat == kRows, "one residual word per 4-element group");
+  constexpr int kNR = kBlock && kMode != 1 ? kFlat : 0;
+  constexpr bool kLateResid = kNR > 0 && kIm2col && kMode != 2;
   uint32_t resid_pre[kFlat > kRows ? kFlat : kRows];
-  if constexpr (kBlock && kMode != 1) {
-    if (g.has_add && g.ipt) {
-      // flat epilogue: 4 consecutive elements of an image run per group (see there)
+  auto issue_resid = [&]() __attribute__((always_inline)) {
+    if constexpr (kNR > 0) {
+      const uint32_t* zw = reinterpret_cast<const uint32_t*>(tk_zero_words);
       const int hw = g.OH * g.OW;
-      const int run = min(BM, g.M - m0) * hw;
+      if (g.has_add && g.ipt) {
+        // flat epilogue: 4 consecutive elements of an image run per group (see there)
+        const int run = min(BM, g.M - m0) * hw;
 #pragma unroll
-      for (int k = 0; k < kFlat; ++k) {
-        const int gi = tid + kGemmThreads * k;
-        const int kk = gi / (16 * hw), f = (gi - kk * 16 * hw) * 4;
-        const int img = n0 / hw + kk;
-        const bool ok = kk < g.ipt && img < g.N / hw && f < run;
-        resid_pre[k] = ok ? ldg(reinterpret_cast<const uint32_t*>(g.add_res + ((int64_t)img * g.M + m0) * hw + f)) : 0u;
-      }
-    } else if (g.has_add && g.vecw >= 4) {
-      const int hw = g.OH * g.OW;
-      const int col = n0 + (tid % kLPR) * 4;
-      const int img = col / hw;
-      const int64_t cbase = (int64_t)img * g.M * hw + (col - img * hw);
+        for (int k = 0; k < kFlat; ++k) {
+          const int gi = tid + kGemmThreads * k;
+          const int kk = gi / (16 * hw), f = (gi - kk * 16 * hw) * 4;
+          const int img = n0 / hw + kk;
+          const bool ok = kk < g.ipt && img < g.N / hw && f < run;
+          resid_pre[k] = ldg(ok ? reinterpret_cast<const uint32_t*>(g.add_res + ((int64_t)img * g.M + m0) * hw + f) : zw);
+        }
+      } else if (g.has_add && g.vecw >= 4) {
+        const int col = n0 + (tid % kLPR) * 4;
+        const int img = col / hw;
+        const int64_t cbase = (int64_t)img * g.M * hw + (col - img * hw);
 #pragma unroll
-      for (int k = 0; k < kRows; ++k) {
-        const int row = m0 + tid / kLPR + kRPI * k;
-        const bool ok = col < g.N && row < g.M;
-        resid_pre[k] = ldg(reinterpret_cast<const uint32_t*>(g.add_res + (ok ? cbase + (int64_t)row * hw : 0)));
+        for (int k = 0; k < kRows; ++k) {
+          const int row = m0 + tid / kLPR + kRPI * k;
+          const bool ok = col < g.N && row < g.M;
+          resid_pre[k] = ldg(reinterpret_cast<const uint32_t*>(g.add_res + (ok ? cbase + (int64_t)row * hw : 0)));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < kNR; ++k) resid_pre[k] = ldg(zw);
       }
     }
-  }
+  };
+  if constexpr (!kLateResid) issue_resid();
   const int kc = tid & 3;  // this thread's 16-byte chunk within a K stage
 
   // ---- per-thread im2col state for the B rows it loads
@@ -463,13 +477,16 @@ gemm_i8_kernel(GemmArgs g) {
 #pragma unroll
       for (int st = 0; st < kRing - 1; ++st)
         if (st < nst) issue(st);
+      if constexpr (kLateResid) issue_resid();  // younger than the prologue's stages (see there)
       int cur = 0, nxt = kRing - 1;  // ring slots of stage it and of stage it + kRing - 1
       // one step: retire stage it (A_DMA + B_DMA LDS-DMAs per thread and stage) with `pending`
       // later stages still in flight, barrier (stage it visible to all waves; the slot read in
       // step it-1 is free), fragments of stage it first so that their LDS latency overlaps the
       // next issue, then the MFMAs
-      auto step = [&](int it, int pending) __attribute__((always_inline)) {
-        wait_vm(pending * (A_DMA + B_DMA));
+      // extra: the residual loads still allowed in flight (steps retiring a prologue stage)
+      auto step = [&](int it, int pending, int extra) __attribute__((always_inline)) {
+        if (extra) wait_vm_any(pending * (A_DMA + B_DMA) + extra);
+        else wait_vm(pending * (A_DMA + B_DMA));
         if (ablate & 4096) {
         } else if (ablate & 1024) asm volatile("s_barrier" ::: "memory");
         else lds_barrier();
@@ -487,9 +504,11 @@ gemm_i8_kernel(GemmArgs g) {
       };
       // steady state with a compile-time wait count, then the last kRing - 2 stages
       const int steady = nst - (kRing - 2);
+      constexpr int kLate = kLateResid ? kNR : 0;
       int it = 0;
-      for (; it < steady; ++it) step(it, kRing - 2);
-      for (; it < nst; ++it) step(it, nst - 1 - it);
+      for (; it < steady && it < kRing - 1; ++it) step(it, kRing - 2, kLate);
+      for (; it < steady; ++it) step(it, kRing - 2, 0);
+      for (; it < nst; ++it) step(it, nst - 1 - it, it < kRing - 1 ? kLate : 0);
     };
     auto issue_a = [&](int8_t* sa) {
 #pragma unroll
@@ -612,8 +631,13 @@ gemm_i8_kernel(GemmArgs g) {
   }  // plain path
   // every load issued so far (LDS-DMA stages, the row constants) has landed: a wait the
   // compiler sees (the ring's counted waits are inline asm), so that it does not add
-  // conservative vmcnt(0) waits before the epilogue's LDS reads
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  // conservative vmcnt(0) waits before the epilogue's LDS reads.  The late residual loads (the
+  // youngest, see issue_resid) may stay in flight: vmcnt(kNR)
+  if constexpr (kLateResid) {
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (kNR & 15) | ((kNR >> 4) << 14));
+  } else {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  }
   if constexpr (kMode == 1) {
     v4i* dst = reinterpret_cast<v4i*>(g.ws + (tile * gridDim.z + blockIdx.z) * kTileInts);
 #pragma unroll
@@ -941,6 +965,51 @@ gemm_i8_kernel(GemmArgs g) {
       auto rows = [&](auto add_c, auto clip_c, auto aux_c) __attribute__((always_inline)) {
         constexpr bool ADD = decltype(add_c)::value, CLIP = decltype(clip_c)::value;
         constexpr int AUX = decltype(aux_c)::value;
+        if constexpr (ADD) {
+          if (!TK_ABL(262144 | 2 | 8192 | 16384)) {
+            // residual join: every row's conv / bias_add / requantize records first (3 kRows
+            // stores), then the joins, whose residual words (issue_resid) land under those stores
+            int32_t qs[kRows][4];
+#pragma unroll
+            for (int k = 0; k < kRows; ++k) {
+              const int lr = tid / kLPR + kRPI * k;
+              const EpiRow r = rowc[lr];
+              const v4i t = *reinterpret_cast<const v4i*>(tileI + lr * kStr + c4);
+              const uint32_t o = offs[k];
+              v4u v = __builtin_bit_cast(v4u, t) + r.fold;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_conv, o * 4u, 0, AUX);
+              v += (uint32_t)r.bias;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r_bias, o * 4u, 0, AUX);
+              const int sh2 = -r.s - 1;
+              const uint32_t rnd = 1u << (sh2 - 1);
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                qs[k][e] = clamp_i32(zpo + ((int32_t)((uint32_t)__mulhi((int32_t)(v[e] - (uint32_t)r.zp), r.m) + rnd) >> sh2),
+                                     qmin, qmax);
+              __builtin_amdgcn_raw_buffer_store_b32(pack4u(qs[k][0], qs[k][1], qs[k][2], qs[k][3]), r_rq, o, 0, AUX);
+            }
+#pragma unroll
+            for (int k = 0; k < kRows; ++k) {
+              const int lr = tid / kLPR + kRPI * k;
+              const uint32_t o = offs[k];
+              int32_t q[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                // qnn.add (src/relay/qnn/op/add.cc:40-96): RQ(block) + RQ(residual) - zp_out
+                const uint32_t rb = (resid_pre[k] >> (8 * e)) & 0xFFu;
+                q[e] = clamp_i32(lut[qs[k][e] & 0xFF] + lut[256 + rb] - add_zp, qmin, qmax);
+              }
+              __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_add, o, 0, AUX);
+              if constexpr (CLIP) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
+                __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, AUX);
+              }
+              if (want_shadow) *reinterpret_cast<v4i*>(tileI + lr * kStr + c4) = v4i{q[0], q[1], q[2], q[3]};
+            }
+            return;
+          }
+        }
 #pragma unroll
         for (int k = 0; k < kRows; ++k) {
           const int lr = tid / kLPR + kRPI * k;

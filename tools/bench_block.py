@@ -33,7 +33,7 @@ SHAPES = [  # name, C, H, O, K, stride, pad
 ]
 
 
-def main(batch=64, iters=20, configs=None, reps=3, only=None, rotate=1, marker=False):
+def main(batch=64, iters=20, configs=None, reps=3, only=None, rotate=1, marker=False, rotate_res=1):
     """configs: list of env-var dicts (TK_ABLATE / TK_NT are read per launch); each layer is
     timed for every config, interleaved `reps` times, and the minimum is reported."""
     import os
@@ -69,11 +69,16 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None, rotate=1, marker=F
         a.requantize.output_zero_point = 2
         a.has_clip, a.clip_min, a.clip_max = 1, 2, 127
         keep = []
+        res_refs = []
         if res:
-            resid = torch.from_numpy(rng.integers(-128, 128, size=(batch, O, OH, OH)).astype(np.int8)).to(dev)
-            rr = _lib.TensorRef.from_torch(resid)
-            keep += [resid, rr]
-            a.has_add, a.block_is_rhs, a.residual = 1, 0, rr.ptr
+            # rotate_res > 1: that many residual operands in turn (in the network the residual is a
+            # record written several kernels earlier, no longer in the MALL; here it would be)
+            for _ in range(rotate_res):
+                resid = torch.from_numpy(rng.integers(-128, 128, size=(batch, O, OH, OH)).astype(np.int8)).to(dev)
+                rr = _lib.TensorRef.from_torch(resid)
+                keep += [resid, rr]
+                res_refs.append(rr)
+            a.has_add, a.block_is_rhs, a.residual = 1, 0, res_refs[0].ptr
             for side, ratio in ((a.add.lhs, 0.71), (a.add.rhs, 1.37)):
                 m_, ms_, ss_ = requantize_plan(np.float32(ratio * 0.05), np.float32(0.05), "UPWARD")
                 side.mode, side.axis = m_, -1
@@ -98,6 +103,8 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None, rotate=1, marker=F
 
         def call():
             arr = arrs[turn[0] % rotate]
+            if len(res_refs) > 1:
+                a.residual = res_refs[turn[0] % len(res_refs)].ptr
             turn[0] += 1
             _lib.check(lib.tk_qnn_conv2d_block(rx.ptr, ctypes.c_void_p(shadow.data_ptr()), rw.ptr,
                                                ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(sums.data_ptr()),
@@ -140,4 +147,5 @@ if __name__ == "__main__":
     import json
     cfgs = json.loads(sys.argv[1]) if len(sys.argv) > 1 else None
     main(configs=cfgs, only=sys.argv[2] if len(sys.argv) > 2 else None,
-         rotate=int(sys.argv[3]) if len(sys.argv) > 3 else 1, marker="--marker" in sys.argv)
+         rotate=int(sys.argv[3]) if len(sys.argv) > 3 else 1, marker="--marker" in sys.argv,
+         rotate_res=int(sys.argv[4]) if len(sys.argv) > 4 and not sys.argv[4].startswith("--") else 1)
