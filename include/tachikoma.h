@@ -633,7 +633,9 @@ int tk_module_node_times(tk_module* mod, float* node_ms);
 /* Find step (MIOpen-style, replacing the reference's compile-time schedule choice): for every
  * MFMA conv-block node, times its first max_candidates kernels (tk_conv2d_block_algos; one
  * warm-up + `reps` back-to-back launches each, HIP events on `stream`) and keeps the fastest in
- * the node (block.algo).  Nodes with equal shapes and attributes share one measurement.
+ * the node (block.algo).  Residual-join nodes (block.has_add) time each launch alone after a
+ * 512 MiB cache-evicting fill, since their residual operand arrives from HBM in a network run.
+ * Nodes with equal shapes and attributes share one measurement.
  * Overwrites node outputs (run afterwards); synchronises `stream`.  Optional reports, n_nodes x
  * (max_candidates + 1) each: algo_out[i][0] = the chosen algo (-1: node not tuned), [i][1 + c]
  * = candidate c (-1 past the last); us_out likewise in microseconds per launch. */

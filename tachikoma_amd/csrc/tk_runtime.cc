@@ -1104,6 +1104,34 @@ int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, i
   };
   std::map<std::string, Result> seen;
   int rc = TK_OK;
+  // A residual-join node reads the qnn.add operand, which in the network is a record written
+  // several kernels earlier and comes from HBM; timed back to back it stays in the MALL and the
+  // kernels that expose its load latency look faster than they run (the 56x56 expand: 115 us
+  // cached, 136-153 cold, profiles/r05x_residual_cold_vs_cached.txt).  So each of its timed
+  // launches follows a 512 MiB fill of a scratch buffer that evicts the caches, and is timed alone.
+  void* flush = nullptr;
+  const size_t flush_bytes = (size_t)512 << 20;
+  auto timed_cold = [&](tk::Node& node, float* us) -> int {
+    if (!flush && hipMalloc(&flush, flush_bytes) != hipSuccess) {
+      flush = nullptr;
+      (void)hipGetLastError();
+      return TK_ERR_HIP;
+    }
+    float total = 0.0f;
+    for (int k = 0; k < reps; ++k) {
+      if (hipMemsetAsync(flush, k & 0xFF, flush_bytes, s) != hipSuccess || hipEventRecord(e0, s) != hipSuccess)
+        return TK_ERR_HIP;
+      const int r = tk::run_node(node, s);
+      if (r) return r;
+      float ms = 0.0f;
+      if (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+          hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+        return TK_ERR_HIP;
+      total += ms;
+    }
+    *us = total * 1e3f / (float)reps;
+    return TK_OK;
+  };
   for (size_t i = 0; i < n && rc == TK_OK; ++i) {
     tk::Node& node = mod->nodes[i];
     if (node.desc.kind != TK_NODE_CONV_BLOCK) continue;
@@ -1127,13 +1155,17 @@ int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, i
           continue;
         }
         if (rc) break;
-        if (hipEventRecord(e0, s) != hipSuccess) rc = TK_ERR_HIP;
-        for (int k = 0; k < reps && rc == TK_OK; ++k) rc = tk::run_node(node, s);
-        if (rc == TK_OK && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess)) rc = TK_ERR_HIP;
-        float ms = 0.0f;
-        if (rc == TK_OK && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = TK_ERR_HIP;
+        if (node.desc.attrs.block.has_add) {
+          rc = timed_cold(node, &r.us[c]);
+        } else {
+          if (hipEventRecord(e0, s) != hipSuccess) rc = TK_ERR_HIP;
+          for (int k = 0; k < reps && rc == TK_OK; ++k) rc = tk::run_node(node, s);
+          if (rc == TK_OK && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess)) rc = TK_ERR_HIP;
+          float ms = 0.0f;
+          if (rc == TK_OK && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = TK_ERR_HIP;
+          if (rc == TK_OK) r.us[c] = ms * 1e3f / (float)reps;
+        }
         if (rc) break;
-        r.us[c] = ms * 1e3f / (float)reps;
         if (best_us <= 0.0f || r.us[c] < best_us) best_us = r.us[c], r.best = r.algos[c];
       }
       if (rc) {
@@ -1160,6 +1192,10 @@ int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, i
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  if (flush) {
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(flush);
+  }
   return rc;
 }
 

@@ -68,6 +68,7 @@ def main(batch=64, iters=20, configs=None, reps=3, only=None, rotate=1, marker=F
         a.requantize.multipliers, a.requantize.shifts = md.data_ptr(), sd.data_ptr()
         a.requantize.output_zero_point = 2
         a.has_clip, a.clip_min, a.clip_max = 1, 2, 127
+        a.algo = int(os.environ.get("TK_BB_ALGO", "0"))  # a tk_conv2d_block_algos entry (0: the library's choice)
         keep = []
         res_refs = []
         if res:
