@@ -408,7 +408,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     (the source digest compiled in by build.py) is compared with the digest of the in-tree
     sources, and a stale library is refused.  ``TK_LIB_PATH`` substitutes the ablation build
     of the same sources (A/B kernel timing in tools/, one process per build on one box); it
-    is announced on stderr and reported by ``build_info()``."""
+    is announced on stderr and reported by ``build_info()``; with ``TK_LIB_ANY_SOURCES=1`` it may
+    be a build of other sources (A/B of two versions)."""
     global _LIB
     if _LIB is not None:
         return _LIB
@@ -430,7 +431,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     except OSError:
         # a deployment that ships the library without its sources: nothing to compare with
         want = None
-    if want is not None and built.split("+")[0] != want:
+    # TK_LIB_ANY_SOURCES=1 (with TK_LIB_PATH only): A/B timing of another source version's build
+    # on the same box (the C ABI and the planner's algo numbering must be unchanged between them)
+    any_src = bool(override) and os.environ.get("TK_LIB_ANY_SOURCES") == "1"
+    if want is not None and built.split("+")[0] != want and not any_src:
         raise TachikomaError(
             f"{path} was built from other sources (library {built}, tree {want}): rebuild it with "
             "`python tachikoma_amd/build.py`")

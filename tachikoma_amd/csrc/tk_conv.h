@@ -201,7 +201,8 @@ __device__ __forceinline__ void wait_vm(int n) {
 }
 
 // the same for any count up to 40 (a count known only at run time: the image-tile kernel's
-// DMA instructions per stage); larger counts wait for everything
+// DMA instructions per stage, plus its residual words on the plans that issue them early);
+// larger counts wait for everything
 __device__ __forceinline__ void wait_vm_any(int n) {
   switch (n) {
 #define TK_WVM(k) \

@@ -80,6 +80,8 @@ struct ImgArgs {
   int32_t npass, cw;           // epilogue passes over the tile's columns (npass > 1: one image per
                                // workgroup, cw = hw / npass pixels per pass), or 1 pass of cw = hw
   int32_t skew;                // profiling: first-round workgroups start up to 3 x skew x s_sleep(8) late
+  int32_t early_res;           // residual words issued after the prologue's stages (two workgroups
+                               // per CU), else during the last K step
   // split K (3x3): MODE 1 workgroups reduce stages [z * stages / ksplit, (z + 1) * stages / ksplit)
   // of their tile and store the raw sums as partial record z (NCHW int32, the conv record's layout,
   // part + z * part_stride); MODE 2 workgroups (their own tiling) sum the ksplit partial records
@@ -141,9 +143,14 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   const int total = (npass > 1 ? 1 : nimg) * runq;  // epilogue groups per pass
   if (tid == 0) s_fast = 1;       // visible after the first barrier; only cleared at the epilogue
 
-  // ---- residual words of every epilogue group (qnn.add joins), LDS-DMA'd in group order during
-  // the last K step (after its barrier: no counted ring wait follows, the epilogue's full wait
-  // covers them), so that they neither delay the first stages nor expose their latency
+  // ---- residual words of every epilogue group (qnn.add joins), LDS-DMA'd in group order.  With
+  // two workgroups per CU (h.early_res) right after the prologue's stages: the stage waits of
+  // those stages let them stay in flight, so they land during the K loop -- the residual is a
+  // record written several kernels earlier and comes from HBM (profiles/r05ae_residual_cold_per_
+  // kernel.txt; the 14x14 joins 45-46 -> 40-41 us) -- while the other workgroup computes.  With
+  // one workgroup per CU they would slow its own stage loads (the 28x28 joins: 101.5 -> 112.6 us
+  // cached), so there they go out during the last K step, after its barrier (no counted ring wait
+  // follows).  Either way the epilogue's full wait covers them.
   auto issue_residual = [&](int c0) __attribute__((always_inline)) {
     for (int q0 = wave * 64; q0 < total; q0 += kGemmThreads) {
       const int gi = q0 + lane;
@@ -365,17 +372,27 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   if constexpr (MODE != 2) {
     const int nst = MODE == 1 ? (int)((int64_t)(zs + 1) * h.stages / S) - st_lo : h.stages, ns = h.ns;
     for (int st = 0; st < ns - 1 && st < nst; ++st) issue(st);
+    // the residual words, younger than the prologue's stages: this wave's count of them stays
+    // allowed in flight while those stages are retired
+    // (1x1 kernels only -- the joins of the bottleneck expands -- so that the 3x3 kernels' stage
+    // loop is unchanged)
+    const bool early_res = KT == 1 && MODE == 0 && has_add && h.early_res && !TK_ABL(65536);
+    const int nres = early_res && total > wave * 64 ? (total - wave * 64 + kGemmThreads - 1) / kGemmThreads : 0;
+    if constexpr (KT == 1) {
+      if (early_res) issue_residual(0);
+    }
     int cur = 0, nxt = ns - 1;
     for (int it = 0; it < nst; ++it) {
       if (!TK_ABL(1 << 21)) {  // (ablation build: 1 << 21 drops the stage waits, timing only)
-        wait_vm_any(min(ns - 2, nst - 1 - it) * ni);
+        if constexpr (KT == 1) wait_vm_any(min(ns - 2, nst - 1 - it) * ni + (it < ns - 1 ? nres : 0));
+        else wait_vm_any(min(ns - 2, nst - 1 - it) * ni);
         lds_barrier();
       }
       if (it + ns - 1 < nst) {
         issue(nxt);
         nxt = nxt == ns - 1 ? 0 : nxt + 1;
       }
-      if (MODE == 0 && has_add && it == nst - 1 && !TK_ABL(65536)) issue_residual(0);
+      if (MODE == 0 && has_add && !early_res && it == nst - 1 && !TK_ABL(65536)) issue_residual(0);
       compute(smem + cur * h.stage_bytes);
       cur = cur == ns - 1 ? 0 : cur + 1;
     }
@@ -784,6 +801,7 @@ bool img_candidate(const ConvGeom& g, const GemmArgs& ga, int kt, int st, int R,
   x.npass = npass;
   x.cw = cw;
   x.skew = env_int("TK_IMG_SKEW", 0);
+  x.early_res = two ? 1 : 0;
   x.tstride = npass > 1 ? cw + 4 : nct * 32 + 4;
   // ring depth: every slot the LDS budget holds (up to 8, no more than the stages need), at least
   // 3 where there are more than 2 stages and one workgroup per CU.  The budget is the CU's 160 KB, or half of it for two
