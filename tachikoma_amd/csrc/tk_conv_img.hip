@@ -96,7 +96,9 @@ struct ImgArgs {
 // 64 for 3x3 -- 64 halves the barrier-separated stages of the 7x7 / 14x14 layers' long K loops;
 // 32, 64 or 128 for 1x1: smaller stages for larger planes or two workgroups per CU).
 // MODE: 0 = the whole block; 1 = split-K partial sums (no epilogue); 2 = sum the partials + the
-// block epilogue (no K loop).
+// block epilogue (no K loop); 3 = the whole block of a 1x1 join with two workgroups per CU, its
+// residual words issued after the prologue's stages (a separate instantiation, so that the stage
+// loop of every other kernel is unchanged).
 template <int KT, int WM, int CT, int CC, int MODE = 0>
 __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, ImgArgs h) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -374,17 +376,15 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     for (int st = 0; st < ns - 1 && st < nst; ++st) issue(st);
     // the residual words, younger than the prologue's stages: this wave's count of them stays
     // allowed in flight while those stages are retired
-    // (1x1 kernels only -- the joins of the bottleneck expands -- so that the 3x3 kernels' stage
-    // loop is unchanged)
-    const bool early_res = KT == 1 && MODE == 0 && has_add && h.early_res && !TK_ABL(65536);
+    const bool early_res = MODE == 3 && has_add && !TK_ABL(65536);
     const int nres = early_res && total > wave * 64 ? (total - wave * 64 + kGemmThreads - 1) / kGemmThreads : 0;
-    if constexpr (KT == 1) {
+    if constexpr (MODE == 3) {
       if (early_res) issue_residual(0);
     }
     int cur = 0, nxt = ns - 1;
     for (int it = 0; it < nst; ++it) {
       if (!TK_ABL(1 << 21)) {  // (ablation build: 1 << 21 drops the stage waits, timing only)
-        if constexpr (KT == 1) wait_vm_any(min(ns - 2, nst - 1 - it) * ni + (it < ns - 1 ? nres : 0));
+        if constexpr (MODE == 3) wait_vm_any(min(ns - 2, nst - 1 - it) * ni + (it < ns - 1 ? nres : 0));
         else wait_vm_any(min(ns - 2, nst - 1 - it) * ni);
         lds_barrier();
       }
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
         issue(nxt);
         nxt = nxt == ns - 1 ? 0 : nxt + 1;
       }
-      if (MODE == 0 && has_add && !early_res && it == nst - 1 && !TK_ABL(65536)) issue_residual(0);
+      if ((MODE == 0 || MODE == 3) && has_add && !early_res && it == nst - 1 && !TK_ABL(65536)) issue_residual(0);
       compute(smem + cur * h.stage_bytes);
       cur = cur == ns - 1 ? 0 : cur + 1;
     }
@@ -713,6 +713,14 @@ ImgKernel img_kernel(int ct, int cc) {
   } else {
     return cc == 32 ? img_kernel_cc<1, WM, 32>(ct) : cc == 64 ? img_kernel_cc<1, WM, 64>(ct) : img_kernel_cc<1, WM, 128>(ct);
   }
+}
+
+// 1x1 joins with two workgroups per CU: residual words issued early (MODE 3)
+template <int WM>
+ImgKernel img_kernel_early(int ct, int cc) {
+  if (cc == 128) return ct == 2 ? conv_img_kernel<1, WM, 2, 128, 3> : conv_img_kernel<1, WM, 4, 128, 3>;
+  if (cc == 64) return ct == 2 ? conv_img_kernel<1, WM, 2, 64, 3> : conv_img_kernel<1, WM, 4, 64, 3>;
+  return ct == 2 ? conv_img_kernel<1, WM, 2, 32, 3> : conv_img_kernel<1, WM, 4, 32, 3>;
 }
 
 // Split-K kernels: the partial pass (MODE 1) and the epilogue pass (MODE 2: one 32-row tiling for
@@ -1123,7 +1131,9 @@ int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga
     hipLaunchKernelGGL(kb, dim3((unsigned)best.b.wgs8), dim3(kGemmThreads), best.lds_b, s, ga, best.b);
   } else {
     best.a.ksplit = 1;
+    const bool early = kt == 1 && ga.has_add && best.a.early_res && best.ct != 7;
     ImgKernel kern = kt == 3 ? (best.wm == 2 ? img_kernel<3, 2>(best.ct, best.cc) : img_kernel<3, 1>(best.ct, best.cc))
+                   : early   ? (best.wm == 2 ? img_kernel_early<2>(best.ct, best.cc) : img_kernel_early<1>(best.ct, best.cc))
                              : (best.wm == 2 ? img_kernel<1, 2>(best.ct, best.cc) : img_kernel<1, 1>(best.ct, best.cc));
     if (set_lds(kern, best.lds, rc)) return 1;
     hipLaunchKernelGGL(kern, dim3((unsigned)best.a.wgs8), dim3(kGemmThreads), best.lds, s, ga, best.a);
