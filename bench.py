@@ -38,6 +38,19 @@ import numpy as np  # noqa: E402
 INT8_MFMA_PEAK_OPS = 5.0e15  # gfx950 dense int8 (2x the 2.5 PF dense bf16 peak), MI355X_MICROARCH.md
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (6.3 TB/s measured streaming copy), MI355X_MICROARCH.md
 METRIC = "ResNet-50 int8 op-traces/sec at 1/2/4/8 GPU; bit-exact vs CPU"
+# the BASELINE.json config each --model measures (configs 3 and 5 are single-GPU batch-64 workloads)
+WORKLOADS = {
+    "resnet50": ("BASELINE config 4 shard", "ResNet-50 v1"),
+    "resnet18": ("BASELINE config 3", "ResNet-18 (torchvision v1)"),
+    "mobilenet_v2": ("BASELINE config 5", "MobileNetV2 1.0"),
+}
+
+
+def metric_for(model: str) -> str:
+    """BASELINE.json's metric for the headline model; the same unit named for configs 3 and 5."""
+    if model == "resnet50":
+        return METRIC
+    return f"{WORKLOADS.get(model, ('', model))[1]} int8 op-traces/sec; bit-exact vs CPU"
 BLOCK_KINDS = ("conv_block", "dense_block", "qnn.conv2d", "qnn.dense")
 
 
@@ -282,7 +295,7 @@ def pmc_traffic(model: str, batch: int, library: str, tune_digest: str | None = 
     launches = int(doc["launches_per_step"])  # dispatches: a split-K node launches twice
     return {"per_launch": doc["hbm_bytes_per_step"] / max(launches, 1), "per_step": doc["hbm_bytes_per_step"],
             "launches": launches, "source": os.path.relpath(path, ROOT), "library_match": same,
-            "kernel_match": kern, "library": doc.get("library")}
+            "kernel_match": kern, "library": doc.get("library"), "mfma": doc.get("mfma")}
 
 
 def find_tune_table(model: str, batch: int):
@@ -808,7 +821,7 @@ def main(argv=None) -> int:
             _log("FILE SINK FAILURE: a written trace file's digest differs from its device digest")
             rc = 1
         line = {
-            "metric": METRIC,
+            "metric": metric_for(args.model),
             "value": round(value, 3),
             "unit": "op-traces/s",
             "n_gpus": world,
@@ -819,8 +832,10 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int8",
-            "data": "synthetic (seeded int8 inputs, random-init int8 weights of the ResNet-50 v1 topology)",
-            "config": {"workload": f"{args.model} int8 224x224, {B} samples per GPU (BASELINE config 4 shard), "
+            "data": f"synthetic (seeded int8 inputs, random-init int8 weights of the "
+                    f"{WORKLOADS.get(args.model, ('', args.model))[1]} topology)",
+            "config": {"workload": f"{args.model} int8 224x224, {B} samples per GPU "
+                                   f"({WORKLOADS.get(args.model, ('custom',))[0]}), "
                                    f"full per-op trace to pinned host memory",
                        "model": args.model, "global_batch": B * world, "samples_per_gpu": B, "seq_len": None,
                        "parallelism": f"batch-shard x{world}", "sink": args.sink,
@@ -839,11 +854,16 @@ def main(argv=None) -> int:
                          "kernel": "fused conv/dense layer blocks, the find step's pick per node: conv_img_kernel "
                                    "(whole-image tiles on 28x28/14x14/7x7 planes, 3x3 split-K as a partial and an "
                                    "epilogue pass), gemm_i8_kernel<*,*,block> (im2col tiles), conv_pf_kernel "
-                                   "(persistent im2col), dense_tile_kernel (classifier); v_mfma_i32_32x32x32_i8",
+                                   "(persistent im2col), dw3x3_kernel (depthwise LDS band, MobileNetV2), "
+                                   "dense_tile_kernel (classifier); v_mfma_i32_32x32x32_i8",
                          "nodes_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
                          "algorithmic_bytes_per_step": int(blk_bytes),
                          "mfma_tops": round(achieved_ops / 1e12, 1),
                          "mfma_frac": round(achieved_ops / INT8_MFMA_PEAK_OPS, 4),
+                         # counted: rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per XCD x 1024
+                         # SIMDs) over the block kernels, from the same PMC summary as `traffic`
+                         "mfma_busy": None if pmc is None or not pmc.get("mfma") else pmc["mfma"]["mfma_busy"],
+                         "mfma_counters": None if pmc is None else pmc.get("mfma"),
                          "d2h": {"achieved_GBps": round(d2h_achieved, 2), "measured_peak_GBps": round(d2h_peak, 2),
                                  "frac": round(d2h_achieved / d2h_peak, 4) if d2h_peak else None,
                                  "measured_peak_2streams_GBps": round(d2h_peak2, 2),

@@ -492,6 +492,46 @@ typedef struct {
 int tk_qnn_simulated_quantize(const tk_tensor* data, tk_tensor* out, const tk_simq_attrs* attrs, void* stream);
 int tk_qnn_simulated_dequantize(const tk_tensor* data, tk_tensor* out, const tk_simq_attrs* attrs, void* stream);
 
+/* qnn.requantize with compute_dtype "float32" / "float64": RequantizeLowerFP<Bits>
+ * (src/relay/qnn/op/requantize.cc:293-373, dispatch :392-403), chosen by
+ * requantize_config(compute_dtype=...) or the op's own attribute (requantize_config.h:53-72).  As
+ * the MRT llvm target without -mcpu runs it (no SSE4.1: the Upward / Tonearest forms of :127-173),
+ * per element, every step one IEEE operation in the compute type, no contraction:
+ *   t = F(x) - F(zp_in);  t = M * t (per-tensor, skipped when `scaled` == 0, i.e. the scales are
+ *   structurally equal, :313-318) or t * M[c] (per-axis, always);  t = t + F(zp_out);
+ *   UPWARD:    b = t + 0.5; f = F(I(b)); t = (b == f || b >= 0) ? f : f - 1
+ *   TONEAREST: s = t < 0 ? -1 : 1; b = (t + 0.5 * s) * s; t = F(I(b)) * s     (t kept if not finite)
+ *   q = int32(t), clipped to the output dtype unless it is int32.
+ * F = float / double, I = int32 / int64 (Cast(.., Int(Bits))), M = the double multiplier
+ * double(s_in) / double(s_out) converted to F.  Float -> int casts follow x86-64's cvtt* (what the
+ * reference's LLVM code runs): truncation, and INT_MIN of the target width for NaN or out-of-range
+ * values. */
+typedef struct {
+  int32_t bits;                 /* 32 (float32) or 64 (float64) */
+  int32_t rounding;             /* TK_ROUND_* */
+  int32_t axis;                 /* channel axis of per-axis multipliers / zero points */
+  int32_t scaled;               /* per-tensor: 1 = multiply by `multiplier`, 0 = equal scales */
+  double multiplier;            /* per-tensor double(s_in) / double(s_out) */
+  const double* multipliers;    /* device, per-axis (len = shape[axis]); NULL = per-tensor */
+  int32_t input_zero_point;     /* used when input_zero_points == NULL */
+  const int32_t* input_zero_points; /* device, optional per-axis */
+  int32_t output_zero_point;
+} tk_requantize_fp_attrs;
+int tk_requantize_fp(const tk_tensor* data, tk_tensor* out, const tk_requantize_fp_attrs* attrs, void* stream);
+
+/* qnn.add / qnn.subtract / qnn.mul built under a float compute_dtype: tk_qnn_binary with every
+ * inner Requantize (RequantizeOrUpcast's, op_common.h:193-207, and mul's, mul.cc:60-63) in the
+ * RequantizeLowerFP form above, int32 output (no clip inside the requantize). */
+typedef struct {
+  int32_t op;                   /* TK_QB_* */
+  tk_requantize_fp_attrs lhs, rhs;
+  int32_t lhs_upcast, rhs_upcast;
+  tk_requantize_fp_attrs out;   /* TK_QB_MUL only */
+  int32_t output_zero_point;    /* add / subtract */
+} tk_qnn_binary_fp_attrs;
+int tk_qnn_binary_fp(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const tk_qnn_binary_fp_attrs* attrs,
+                     void* stream);
+
 /* ---------------------------------------------------------------- executor
  * Native run loop replacing GraphExecutor::Run (graph_executor.cc:61-66) and
  * the debug executor's per-node copy-out (graph_executor_debug.cc:249-284).
@@ -530,6 +570,8 @@ enum {
   TK_NODE_CONV2D_TRANSPOSE = 29, /* in: data (NCHW), weight (IOHW); attrs.conv2d_transpose */
   TK_NODE_SIM_QUANTIZE = 30,   /* in: data (float32); attrs.simq */
   TK_NODE_SIM_DEQUANTIZE = 31, /* in: data (float32); attrs.simq */
+  TK_NODE_REQUANTIZE_FP = 32,  /* in: data; attrs.requantize_fp (float compute_dtype) */
+  TK_NODE_QNN_BINARY_FP = 33,  /* in: lhs, rhs; attrs.qnn_binary_fp (float compute_dtype) */
 };
 
 #define TK_MAX_NODE_INPUTS 8
@@ -560,6 +602,8 @@ typedef struct {
     tk_leaky_relu_attrs leaky_relu;
     tk_conv2d_transpose_attrs conv2d_transpose;
     tk_simq_attrs simq;
+    tk_requantize_fp_attrs requantize_fp;
+    tk_qnn_binary_fp_attrs qnn_binary_fp;
     struct { int64_t a_min, a_max; } clip;
     struct { int32_t axis; } bias_add;
   } attrs;

@@ -98,6 +98,15 @@ def _resolve_rounding(attrs):
     return r
 
 
+def _resolve_compute_dtype(attrs):
+    """SelectRequntizeParameter for compute_dtype (qnn/utils.cc:231-245): the op's own attribute,
+    else the requantize_config in effect, else int64 (llvm without -mcpu, requantize_config.h:53-72)."""
+    cd = attrs.get("compute_dtype", "None")
+    if cd in (None, "None"):
+        cd = attrs.get("cfg_compute_dtype") or "int64"
+    return cd
+
+
 def eval_call(call, args, backend: str = "numpy", threads: int = 1):
     op = call.op
     a = call.attrs
@@ -137,13 +146,15 @@ def eval_call(call, args, backend: str = "numpy", threads: int = 1):
     if op == "qnn.requantize":
         return ref.requantize(args[0], _const(call.args[1]), _const(call.args[2]), _const(call.args[3]),
                               _const(call.args[4]), axis=a["axis"], rounding=_resolve_rounding(a),
-                              out_dtype=a["out_dtype"])
+                              out_dtype=a["out_dtype"], compute_dtype=_resolve_compute_dtype(a))
     if op in ("qnn.add", "qnn.subtract", "qnn.mul"):
         c = [_const(call.args[i]) for i in range(2, 8)]
         fn = {"qnn.add": ref.qnn_add, "qnn.subtract": ref.qnn_subtract, "qnn.mul": ref.qnn_mul}[op]
         # every inner Requantize takes the requantize_config's rounding (qnn/utils.h:106-122)
         return fn(args[0], args[1], *c, lhs_axis=a.get("lhs_axis", -1), rhs_axis=a.get("rhs_axis", -1),
-                  rounding=_resolve_rounding(a))
+                  rounding=_resolve_rounding(a), compute_dtype=_resolve_compute_dtype(a))
+    if op in ("qnn.concatenate", "qnn.leaky_relu") and _resolve_compute_dtype(a) != "int64":
+        raise NotImplementedError(f"{op} under compute_dtype={_resolve_compute_dtype(a)}: not restated")
     if op == "qnn.concatenate":
         scales = [_const(f) for f in call.args[1].fields]
         zps = [_const(f) for f in call.args[2].fields]

@@ -235,6 +235,32 @@ class tk_simq_attrs(ctypes.Structure):
     ]
 
 
+class tk_requantize_fp_attrs(ctypes.Structure):
+    _fields_ = [
+        ("bits", ctypes.c_int32),
+        ("rounding", ctypes.c_int32),
+        ("axis", ctypes.c_int32),
+        ("scaled", ctypes.c_int32),
+        ("multiplier", ctypes.c_double),
+        ("multipliers", ctypes.c_void_p),
+        ("input_zero_point", ctypes.c_int32),
+        ("input_zero_points", ctypes.c_void_p),
+        ("output_zero_point", ctypes.c_int32),
+    ]
+
+
+class tk_qnn_binary_fp_attrs(ctypes.Structure):
+    _fields_ = [
+        ("op", ctypes.c_int32),
+        ("lhs", tk_requantize_fp_attrs),
+        ("rhs", tk_requantize_fp_attrs),
+        ("lhs_upcast", ctypes.c_int32),
+        ("rhs_upcast", ctypes.c_int32),
+        ("out", tk_requantize_fp_attrs),
+        ("output_zero_point", ctypes.c_int32),
+    ]
+
+
 class _clip(ctypes.Structure):
     _fields_ = [("a_min", ctypes.c_int64), ("a_max", ctypes.c_int64)]
 
@@ -262,6 +288,8 @@ class tk_node_attrs(ctypes.Union):
         ("leaky_relu", tk_leaky_relu_attrs),
         ("conv2d_transpose", tk_conv2d_transpose_attrs),
         ("simq", tk_simq_attrs),
+        ("requantize_fp", tk_requantize_fp_attrs),
+        ("qnn_binary_fp", tk_qnn_binary_fp_attrs),
         ("clip", _clip),
         ("bias_add", _bias_add),
     ]
@@ -301,7 +329,7 @@ NODE_KINDS = {
     "ewise": 17, "conv2d_f32": 18, "dense_f32": 19, "nn.pad": 20,
     "qnn.quantize": 21, "qnn.dequantize": 22, "qnn_binary": 23, "qnn.concatenate": 24, "transpose": 25,
     "qnn.leaky_relu": 26, "lookup": 27, "qnn.batch_matmul": 28, "qnn.conv2d_transpose": 29,
-    "qnn.simulated_quantize": 30, "qnn.simulated_dequantize": 31,
+    "qnn.simulated_quantize": 30, "qnn.simulated_dequantize": 31, "requantize_fp": 32, "qnn_binary_fp": 33,
 }
 MAX_NODE_INPUTS = 8
 MAX_NODE_OUTPUTS = 6
@@ -362,6 +390,8 @@ SIGNATURES = {
     "tk_qnn_conv2d_transpose": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_conv2d_transpose_attrs), _VP]),
     "tk_qnn_simulated_quantize": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_simq_attrs), _VP]),
     "tk_qnn_simulated_dequantize": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_simq_attrs), _VP]),
+    "tk_requantize_fp": (ctypes.c_int, [_PT, _PT, ctypes.POINTER(tk_requantize_fp_attrs), _VP]),
+    "tk_qnn_binary_fp": (ctypes.c_int, [_PT, _PT, _PT, ctypes.POINTER(tk_qnn_binary_fp_attrs), _VP]),
     "tk_find_scale_by_kl": (ctypes.c_int, [ctypes.POINTER(_I32), ctypes.POINTER(_F32), ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(_F32)]),
     "tk_module_create": (ctypes.c_int, [ctypes.POINTER(tk_node), ctypes.c_int, ctypes.POINTER(_VP)]),

@@ -163,9 +163,10 @@ class GraphModuleDebug(GraphModule):
     def dump_path(self) -> str:
         return self._dump_path
 
-    def _node_times(self, repeat: int) -> List[List[float]]:
-        """Device seconds per graph node: each device node's time goes to the graph node that
-        holds its first record's op (a shadow node's to the next device node's)."""
+    def _graph_node_of(self) -> List[Optional[int]]:
+        """Graph node charged with each device node's time: the node holding its first record's
+        op; a shadow node (no record) and a node whose records no graph node holds are charged to
+        the next device node's graph node (None when no later one exists)."""
         node_of: Dict[str, int] = {}
         if self.granularity == "fused":
             from ...relay.fuse import fused_nodes
@@ -184,26 +185,127 @@ class GraphModuleDebug(GraphModule):
         else:
             for i, n in enumerate(self._nodes):
                 node_of[n["name"]] = i
+        direct = [next((node_of[r] for r in recs if r in node_of), None) for recs in self.module.node_records]
+        out: List[Optional[int]] = [None] * len(direct)
+        nxt = None
+        for i in range(len(direct) - 1, -1, -1):  # carried nodes take the next charged node's
+            if direct[i] is not None:
+                nxt = direct[i]
+            out[i] = nxt
+        return out
+
+    def _node_times(self, repeat: int) -> List[List[float]]:
+        """Device seconds per graph node from whole-graph profiled runs (tk_module_run_profiled:
+        HIP events around every device node of one run)."""
+        owner = self._graph_node_of()
         per_node: List[List[float]] = [[] for _ in self._nodes]
         for _ in range(max(1, repeat)):
-            times = self.module.run_profiled()  # ms per device node, keyed by "+".join(records)
+            times = list(self.module.run_profiled().values())  # ms per device node, in node order
             acc = [0.0] * len(self._nodes)
-            carry = 0.0
-            for key, ms in times.items():
-                if key.startswith("<"):
-                    carry += ms  # shadow nodes carry no op: charged to the consumer
-                    continue
-                # the first of its records that has a graph node (a canonical graph can simplify
-                # a plan op away entirely, e.g. a cast back to the clip's own type)
-                gi = next((node_of[r] for r in key.split("+") if r in node_of), None)
-                if gi is None:
-                    carry += ms
-                    continue
-                acc[gi] += (ms + carry) * 1e-3
-                carry = 0.0
+            for gi, ms in zip(owner, times):
+                if gi is not None:
+                    acc[gi] += ms * 1e-3
             for i, t in enumerate(acc):
                 per_node[i].append(t)
         return per_node
+
+    def _node_index(self, node) -> int:
+        """debug_executor.py:252-276: a graph node index, or a node name (AttributeError when none
+        has it)."""
+        if isinstance(node, str):
+            for i, n in enumerate(self._nodes):
+                if n["name"] == node:
+                    return i
+            raise AttributeError(f"Could not find a node named {node} in this graph.")
+        if isinstance(node, (int, np.integer)):
+            if not 0 <= int(node) < len(self._nodes):
+                raise IndexError(f"node index {node} out of range [0, {len(self._nodes)})")
+            return int(node)
+        raise RuntimeError("Require node index or name only.")
+
+    def debug_get_output(self, node, out=None):
+        """debug_executor.py:252-276 (GraphExecutorDebug::DebugGetNodeOutput): run the graph and
+        return graph node ``node``'s value (an index or a name); copied into ``out`` (a numpy
+        array) when given.  Every node's value is kept in its own device buffer, so the whole graph
+        runs and the node's buffer is read -- the value the reference computes by running up to
+        the node."""
+        i = self._node_index(node)
+        GraphModule.run(self)
+        if self.canon is not None:
+            from .canonical_values import CanonicalValues
+            t = CanonicalValues(self.module, self.canon).value(self._node_outputs[i])
+        else:
+            t = self.module.buffers[self._node_outputs[i]]
+        if out is not None:
+            out[...] = t.detach().cpu().numpy()
+            return out
+        from ..graph_executor import NDArrayView
+        return NDArrayView(t)
+
+    def run_individual_node(self, index: int, number: int = 10, repeat: int = 1, min_repeat_ms: int = 0,
+                            limit_zero_time_iterations: int = 100, cooldown_interval_ms: int = 0,
+                            repeats_to_cooldown: int = 1):
+        """debug_executor.py:415-480 (GraphExecutorDebug::RunIndividualNode,
+        graph_executor_debug.cc:118-144): time graph node ``index`` alone on data already on the
+        device -- its device nodes (and the shadow nodes charged to it) re-run back to back,
+        ``number`` times per measurement, ``repeat`` measurements, HIP-event timed on the current
+        stream.  A param / input node runs nothing: ``repeat`` zeros.  Returns a BenchmarkResult
+        of seconds per run."""
+        from ..graph_executor import BenchmarkResult, time_evaluator
+        i = self._node_index(index)
+        owner = self._graph_node_of()
+        mine = [k for k, gi in enumerate(owner) if gi == i]
+        if not mine:
+            return BenchmarkResult([0.0] * max(1, repeat))
+        spans: List[List[int]] = []
+        for k in mine:  # consecutive device nodes -> one tk_module_run_range
+            if spans and spans[-1][1] == k:
+                spans[-1][1] = k + 1
+            else:
+                spans.append([k, k + 1])
+        import torch
+        stream = torch.cuda.current_stream(self.module.device)
+
+        def call():
+            for b, e in spans:
+                self.module.run_range(b, e, stream)
+        return BenchmarkResult(time_evaluator(call, self.module.device, number, repeat, min_repeat_ms,
+                                              limit_zero_time_iterations, cooldown_interval_ms, repeats_to_cooldown))
+
+    def run_individual(self, number: int, repeat: int = 1, min_repeat_ms: int = 0,
+                       limit_zero_time_iterations: int = 100, cooldown_interval_ms: int = 0,
+                       repeats_to_cooldown: int = 1) -> List[List[float]]:
+        """debug_executor.py:349-413 (GraphExecutorDebug::RunIndividual, graph_executor_debug.cc:
+        70-116): one warm-up run of the graph, then every graph node timed alone
+        (run_individual_node); a list with one entry per graph node -- ``repeat`` seconds-per-run
+        values each, zeros for param / input nodes."""
+        GraphModule.run(self)
+        return [self.run_individual_node(i, number, repeat, min_repeat_ms, limit_zero_time_iterations,
+                                         cooldown_interval_ms, repeats_to_cooldown).results
+                for i in range(len(self._nodes))]
+
+    def profile(self, collectors=None, **input_dict) -> "Report":
+        """debug_executor.py:482-503 (GraphExecutorDebug::Profile): run the graph once and report
+        per-call device time (one call per executed graph node, in execution order) and the
+        whole-graph time.  ``collectors`` (hardware metric collectors) are not supported: pass
+        None; rocprofv3 counters are this engine's collectors (tools/pmc.sh)."""
+        if collectors:
+            raise NotImplementedError("profile(collectors=...): use rocprofv3 --pmc (tools/pmc.sh)")
+        if input_dict:
+            self.set_input(**input_dict)
+        times = self._node_times(1)
+        calls = []
+        for node, t in zip(self._nodes, times):
+            if node["op"] == "param":
+                continue
+            calls.append({"Name": node["name"], "Duration (us)": t[0] * 1e6, "Count": 1,
+                          "Device": f"rocm{self.module.device.index or 0}", "Hash": node["op"],
+                          "Argument Shapes": str(tuple(node["shape"]))})
+        total = sum(c["Duration (us)"] for c in calls)
+        for c in calls:
+            c["Percent"] = c["Duration (us)"] / total * 100 if total else 0.0
+        return Report(calls, {"Executor": "GraphModuleDebug", "Granularity": self.granularity,
+                              "Duration (us)": total})
 
     def run(self, repeat: int = 1, sort_by_time: bool = True, **inputs):  # noqa: D401  (debug_executor.run)
         """Execute, time every node, dump the output tensors and the Chrome trace, print the table."""
@@ -275,6 +377,55 @@ class GraphModuleDebug(GraphModule):
         """Remove the dump root (debug_executor.py:505-510)."""
         if os.path.isdir(self._dump_root):
             shutil.rmtree(self._dump_root)
+
+
+class Report:
+    """What profile() returns (python/tvm/runtime/profiling/__init__.py Report): ``calls`` (one
+    dict per call: Name, Duration (us), Percent, Count, Device, Hash, Argument Shapes) and
+    ``configuration``; ``table()`` / ``csv()`` / ``json()`` renderings."""
+
+    COLUMNS = ("Name", "Duration (us)", "Percent", "Count", "Device", "Argument Shapes")
+
+    def __init__(self, calls: List[dict], configuration: dict):
+        self.calls = calls
+        self.configuration = configuration
+
+    def table(self, sort: bool = True, aggregate: bool = True, col_sums: bool = True) -> str:
+        rows = list(self.calls)
+        if aggregate:
+            agg: Dict[str, dict] = {}
+            for c in rows:
+                a = agg.setdefault(c["Name"], dict(c, **{"Duration (us)": 0.0, "Percent": 0.0, "Count": 0}))
+                a["Duration (us)"] += c["Duration (us)"]
+                a["Percent"] += c["Percent"]
+                a["Count"] += c["Count"]
+            rows = list(agg.values())
+        if sort:
+            rows.sort(key=lambda c: -c["Duration (us)"])
+        if col_sums:
+            rows.append({"Name": "Sum", "Duration (us)": sum(c["Duration (us)"] for c in rows),
+                         "Percent": sum(c["Percent"] for c in rows), "Count": sum(c["Count"] for c in rows),
+                         "Device": "", "Argument Shapes": ""})
+        cells = [[f"{c[k]:.2f}" if isinstance(c[k], float) else str(c[k]) for k in self.COLUMNS] for c in rows]
+        widths = [max(len(h), *(len(r[i]) for r in cells)) for i, h in enumerate(self.COLUMNS)] if cells else \
+            [len(h) for h in self.COLUMNS]
+        lines = ["  ".join(h.ljust(w) for h, w in zip(self.COLUMNS, widths))]
+        lines += ["  ".join(v.ljust(w) for v, w in zip(r, widths)) for r in cells]
+        lines.append("Configuration")
+        lines.append("-------------")
+        lines += [f"{k}: {v}" for k, v in self.configuration.items()]
+        return "\n".join(lines)
+
+    def csv(self) -> str:
+        out = [",".join(f'"{h}"' for h in self.COLUMNS)]
+        out += [",".join(f'"{c[k]}"' for k in self.COLUMNS) for c in self.calls]
+        return "\n".join(out)
+
+    def json(self) -> str:
+        return json.dumps({"calls": self.calls, "configuration": self.configuration})
+
+    def __str__(self) -> str:
+        return self.table()
 
 
 def create(lib_factory, dev=None, dump_root: Optional[str] = None, granularity: str = "fused") -> GraphModuleDebug:

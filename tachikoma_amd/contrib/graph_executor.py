@@ -109,6 +109,73 @@ class TraceCapture:
         return memoryview(self.image.numpy())
 
 
+class BenchmarkResult:
+    """Runtimes from benchmarking, in seconds (python/tvm/runtime/module.py:34-98): ``results``
+    and their mean / std / median / min / max."""
+
+    def __init__(self, results):
+        self.results = list(results)
+        self.mean = float(np.mean(self.results))
+        self.std = float(np.std(self.results))
+        self.median = float(np.median(self.results))
+        self.min = float(np.min(self.results))
+        self.max = float(np.max(self.results))
+
+    def __repr__(self):
+        return (f"BenchmarkResult(min={self.min}, mean={self.mean}, median={self.median}, max={self.max}, "
+                f"std={self.std}, results={self.results})")
+
+    def __str__(self):
+        head = "".join(f"{h:^12} " for h in ("mean (ms)", "median (ms)", "max (ms)", "min (ms)", "std (ms)"))
+        vals = "".join(f"{v * 1000:^12.4f} " for v in (self.mean, self.median, self.max, self.min, self.std))
+        return f"Execution time summary:\n{head}\n{vals}\n"
+
+
+def time_evaluator(fn, device, number: int, repeat: int, min_repeat_ms: int = 0,
+                   limit_zero_time_iterations: int = 100, cooldown_interval_ms: int = 0,
+                   repeats_to_cooldown: int = 1, device_timer: bool = True):
+    """``WrapTimeEvaluator`` (src/runtime/profiling.cc): one warm-up call, then ``repeat``
+    measurements of ``number`` back-to-back calls each (seconds per call).  A measurement shorter
+    than ``min_repeat_ms`` is redone with ``number`` grown (x1.618 at least, to the count the last
+    one implies, as the reference does); a zero-time one at most ``limit_zero_time_iterations``
+    times.  Device timer: HIP events on the device's current stream around the calls (the
+    reference's Timer on ROCm); else wall clock with a device synchronize on both sides."""
+    import torch
+    stream = torch.cuda.current_stream(device)
+    fn()
+    torch.cuda.synchronize(device)
+    out = []
+    for r in range(max(1, repeat)):
+        n = max(1, int(number))
+        zeros = 0
+        while True:
+            if device_timer:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(n):
+                    fn()
+                e1.record(stream)
+                e1.synchronize()
+                ms = e0.elapsed_time(e1)
+            else:
+                torch.cuda.synchronize(device)
+                t0 = time.perf_counter()
+                for _ in range(n):
+                    fn()
+                torch.cuda.synchronize(device)
+                ms = (time.perf_counter() - t0) * 1e3
+            if ms <= 0.0 and zeros < limit_zero_time_iterations:
+                zeros += 1
+                continue
+            if ms >= (min_repeat_ms or 0) or ms <= 0.0:
+                break
+            n = max(int(min_repeat_ms / (ms / n) + 1), int(n * 1.618))
+        out.append(ms * 1e-3 / n)
+        if cooldown_interval_ms and repeats_to_cooldown and (r + 1) % repeats_to_cooldown == 0:
+            time.sleep(cooldown_interval_ms * 1e-3)
+    return out
+
+
 class GraphModule:
     def __init__(self, module: DeviceModule):
         self.module = module
@@ -117,7 +184,7 @@ class GraphModule:
         self._meta = {"format": "tachikoma-trace", "version": tf.TRACE_VERSION, "model": "graph",
                       "target": "mi355x", "sample_offset": 0, "rank": 0, "world": 1,
                       "semantics": {"reference": "tvm llvm target without -mcpu", "requantize_compute_dtype":
-                                    "int64", "rounding_default": "UPWARD"},
+                                    _compute_dtypes(self.plan), "rounding_default": "UPWARD"},
                       "inputs": [t.name for t in self.plan.inputs],
                       "params": [t.name for t in self.plan.params],
                       "outputs": list(self.plan.outputs),
@@ -192,6 +259,81 @@ class GraphModule:
 
     def get_num_outputs(self) -> int:
         return len(self.plan.outputs)
+
+    def get_input_index(self, name: str) -> int:
+        """graph_executor.py:247-260: the input's index, -1 when no input has that name."""
+        return next((i for i, t in enumerate(self.plan.inputs) if t.name == name), -1)
+
+    def get_input_info(self):
+        """graph_executor.py:262-287: ({input: shape}, {input: dtype}) of the graph inputs (the
+        arg nodes that are not params)."""
+        return ({t.name: tuple(int(d) for d in t.shape) for t in self.plan.inputs},
+                {t.name: t.dtype for t in self.plan.inputs})
+
+    def debug_get_output(self, node, out=None):
+        """graph_executor.py:305-316: only the debug executor runs a graph up to a node."""
+        raise NotImplementedError("Please use debugger.debug_executor as graph_executor instead.")
+
+    def share_params(self, other: "GraphModule", params_bytes: bytes) -> None:
+        """graph_executor.py:328-339 (GraphExecutor::ShareParams, graph_executor.cc:293-310): take
+        the params named in ``params_bytes`` (only the names are read) from ``other``, a module of
+        the same graph.  The reference aliases the other executor's storage; here each node's
+        tensors are the module's own device buffers, bound into its native node list, so the values
+        are copied device to device (no host round trip) and the buffers derived from them (packed
+        MFMA weights, weight sums) re-derived.  Every name must be a param of both modules with the
+        same shape and dtype, checked before the first copy."""
+        names = list(tf.parse_ndarray_list(params_bytes, copy=False))
+        mine = {t.name: t for t in self.plan.params}
+        theirs = {t.name: t for t in other.plan.params}
+        sel = {}
+        for name in names:
+            if name not in mine or name not in theirs:
+                raise _lib.TachikomaError(f"share_params: {name} is not a param of both modules")
+            a, b = mine[name], theirs[name]
+            if tuple(a.shape) != tuple(b.shape) or a.dtype != b.dtype:
+                raise _lib.TachikomaError(f"share_params: {name} is {b.dtype}{list(b.shape)} in the other module, "
+                                          f"{a.dtype}{list(a.shape)} here")
+            sel[name] = other.module.buffers[name]
+        self.module.set_inputs(sel)
+        if self._capture is not None:
+            self._capture.refresh_params([n for n in sel if n in self._capture.param_offsets])
+
+    _FUNCTIONS = ("set_input", "run", "get_output", "get_input", "get_num_outputs", "get_num_inputs",
+                  "load_params", "share_params", "get_input_index", "get_input_info", "debug_get_output")
+
+    def __getitem__(self, key: str):
+        """graph_executor.py:341-349: the module function ``key`` (module["run"]() etc.)."""
+        if key not in self._FUNCTIONS:
+            raise AttributeError(f"Module has no function '{key}'")
+        return getattr(self, key)
+
+    def benchmark(self, device=None, func_name: str = "run", repeat: int = 5, number: int = 5,
+                  min_repeat_ms=None, limit_zero_time_iterations: int = 100, end_to_end: bool = False,
+                  cooldown_interval_ms: int = 0, repeats_to_cooldown: int = 1, **kwargs) -> BenchmarkResult:
+        """graph_executor.py:351-459: runtimes of ``func_name`` (seconds per call), ``repeat``
+        results of ``number`` calls each, timed with device timers (HIP events) so that input
+        transfers are not counted.  ``kwargs`` are set as inputs first (not timed).  With
+        ``end_to_end`` every call also copies ``kwargs`` host -> device and the outputs back,
+        timed by the wall clock."""
+        from ..relay.device_module import _as_torch_device
+        dev = self.module.device if device is None else _as_torch_device(device)
+        min_ms = 0 if min_repeat_ms is None else min_repeat_ms
+        if end_to_end:
+            host = {k: np.asarray(v.numpy() if hasattr(v, "numpy") else v) for k, v in kwargs.items()}
+
+            def call():
+                if host:
+                    self.set_input(**host)
+                self.run()
+                for i in range(self.get_num_outputs()):
+                    self.get_output(i).numpy()
+            return BenchmarkResult(time_evaluator(call, dev, number, repeat, min_ms, limit_zero_time_iterations,
+                                                  cooldown_interval_ms, repeats_to_cooldown, device_timer=False))
+        if kwargs:
+            self.set_input(**kwargs)
+        fn = self[func_name]
+        return BenchmarkResult(time_evaluator(fn, dev, number, repeat, min_ms, limit_zero_time_iterations,
+                                              cooldown_interval_ms, repeats_to_cooldown))
 
     def get_num_inputs(self) -> int:
         return len(self.plan.inputs)
@@ -282,6 +424,13 @@ class GraphModule:
             t += us
         with open(path, "w") as f:
             json.dump({"traceEvents": events, "displayTimeUnit": "ns"}, f)
+
+
+def _compute_dtypes(plan) -> str:
+    """The requantize compute dtype(s) the plan's ops were built with (the trace header's claim):
+    "int64" (the pinned default), "float32" / "float64", or a "+"-joined list when mixed."""
+    cds = sorted({o.attrs.get("compute_dtype", "int64") for o in plan.ops if "compute_dtype" in o.attrs})
+    return "+".join(cds) if cds else "int64"
 
 
 def create(lib_factory, dev=None) -> GraphModule:

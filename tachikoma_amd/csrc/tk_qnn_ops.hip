@@ -202,6 +202,61 @@ struct BinGeom {
   int32_t lax, rax, oax;
 };
 
+// numpy broadcasting of a and b to y (BroadcastRel): per-dimension element strides, 0 where an
+// operand broadcasts; `same` when no operand broadcasts at all
+static int bin_geometry(const tk_tensor* a, const tk_tensor* b, const tk_tensor* y, BinGeom* g, bool* same) {
+  g->nd = y->ndim;
+  *same = a->ndim == y->ndim && b->ndim == y->ndim;
+  int64_t sa = 1, sb = 1;
+  for (int d = y->ndim - 1; d >= 0; --d) {
+    g->shape[d] = y->shape[d];
+    const int da = d - (y->ndim - a->ndim), db = d - (y->ndim - b->ndim);
+    const int64_t ea = da >= 0 ? a->shape[da] : 1, eb = db >= 0 ? b->shape[db] : 1;
+    if ((ea != 1 && ea != y->shape[d]) || (eb != 1 && eb != y->shape[d])) {
+      set_error("tk_qnn_binary: operands do not broadcast to the output shape");
+      return TK_ERR_SHAPE;
+    }
+    *same = *same && ea == y->shape[d] && eb == y->shape[d];
+    g->ls[d] = ea == 1 ? 0 : sa;
+    g->rs[d] = eb == 1 ? 0 : sb;
+    sa *= ea;
+    sb *= eb;
+  }
+  return TK_OK;
+}
+
+// the output dimension a per-axis parameter set of operand t indexes (its axis, right-aligned)
+static int bin_out_axis(const tk_tensor* t, const tk_tensor* y, int axis) {
+  if (t->ndim == 0) return -1;
+  const int ax = axis < 0 ? t->ndim + axis : axis;
+  if (ax < 0 || ax >= t->ndim || t->shape[ax] == 1) return -1;
+  return ax + (y->ndim - t->ndim);
+}
+
+// element i of the output -> operand offsets and channel indices (the broadcast walk)
+template <bool FLAT>
+__device__ __forceinline__ void bin_walk(int64_t i, const BinGeom& g, int64_t* ia, int64_t* ib, int* ca, int* cb,
+                                         int* co) {
+  *ia = i;
+  *ib = i;
+  *ca = *cb = *co = 0;
+  if constexpr (!FLAT) {
+    *ia = 0;
+    *ib = 0;
+    int64_t r = i;
+    for (int d = g.nd - 1; d >= 0; --d) {
+      const int64_t q = r / g.shape[d];
+      const int64_t k = r - q * g.shape[d];
+      r = q;
+      *ia += k * g.ls[d];
+      *ib += k * g.rs[d];
+      if (d == g.lax) *ca = (int)k;
+      if (d == g.rax) *cb = (int)k;
+      if (d == g.oax) *co = (int)k;
+    }
+  }
+}
+
 template <typename T, int OP, bool FLAT>
 __global__ __launch_bounds__(kQBlock) void qnn_binary_kernel(const T* __restrict__ a, const T* __restrict__ b,
                                                               T* __restrict__ y, int64_t n, BinGeom g, RqParams pa,
@@ -209,23 +264,9 @@ __global__ __launch_bounds__(kQBlock) void qnn_binary_kernel(const T* __restrict
                                                               int32_t up_b) {
   const int64_t stride = (int64_t)gridDim.x * kQBlock;
   for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
-    int64_t ia = i, ib = i;
-    int ca = 0, cb = 0, co = 0;
-    if constexpr (!FLAT) {
-      ia = 0;
-      ib = 0;
-      int64_t r = i;
-      for (int d = g.nd - 1; d >= 0; --d) {
-        const int64_t q = r / g.shape[d];
-        const int64_t k = r - q * g.shape[d];
-        r = q;
-        ia += k * g.ls[d];
-        ib += k * g.rs[d];
-        if (d == g.lax) ca = (int)k;
-        if (d == g.rax) cb = (int)k;
-        if (d == g.oax) co = (int)k;
-      }
-    }
+    int64_t ia, ib;
+    int ca, cb, co;
+    bin_walk<FLAT>(i, g, &ia, &ib, &ca, &cb, &co);
     const int32_t x0 = (int32_t)a[ia], x1 = (int32_t)b[ib];
     int32_t o;
     if constexpr (OP == TK_QB_MUL) {
@@ -255,32 +296,9 @@ int qnn_binary_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* y, const 
   TK_CHECK_ARG(at->op >= TK_QB_ADD && at->op <= TK_QB_MUL, "bad op");
   TK_CHECK_ARG(y->ndim <= 6 && a->ndim <= y->ndim && b->ndim <= y->ndim, "up to 6-D, operands no wider than the output");
   BinGeom g{};
-  g.nd = y->ndim;
-  bool same = a->ndim == y->ndim && b->ndim == y->ndim;
-  {
-    int64_t sa = 1, sb = 1;
-    for (int d = y->ndim - 1; d >= 0; --d) {
-      g.shape[d] = y->shape[d];
-      const int da = d - (y->ndim - a->ndim), db = d - (y->ndim - b->ndim);
-      const int64_t ea = da >= 0 ? a->shape[da] : 1, eb = db >= 0 ? b->shape[db] : 1;
-      if ((ea != 1 && ea != y->shape[d]) || (eb != 1 && eb != y->shape[d])) {
-        set_error("tk_qnn_binary: operands do not broadcast to the output shape");
-        return TK_ERR_SHAPE;
-      }
-      same = same && ea == y->shape[d] && eb == y->shape[d];
-      g.ls[d] = ea == 1 ? 0 : sa;
-      g.rs[d] = eb == 1 ? 0 : sb;
-      sa *= ea;
-      sb *= eb;
-    }
-  }
-  // the output dimension a per-axis parameter set indexes (axis of the operand, right-aligned)
-  auto out_axis = [&](const tk_tensor* t, int axis) -> int {
-    if (t->ndim == 0) return -1;
-    const int ax = axis < 0 ? t->ndim + axis : axis;
-    if (ax < 0 || ax >= t->ndim || t->shape[ax] == 1) return -1;
-    return ax + (y->ndim - t->ndim);
-  };
+  bool same = false;
+  if (bin_geometry(a, b, y, &g, &same) != TK_OK) return TK_ERR_SHAPE;
+  auto out_axis = [&](const tk_tensor* t, int axis) { return bin_out_axis(t, y, axis); };
   RqParams pa = rq_params(at->lhs), pb = rq_params(at->rhs), po = rq_params(at->out);
   const bool mul = at->op == TK_QB_MUL;
   const bool axis_a = pa.zps || (!mul && !at->lhs_upcast && per_axis_mode(pa.mode));
@@ -675,6 +693,203 @@ int qnn_simulated_impl(bool quant, const tk_tensor* x, tk_tensor* y, const tk_si
   return TK_OK;
 }
 
+// ---------------------------------------------------------------- float-compute requantize
+// RequantizeLowerFP<Bits> (src/relay/qnn/op/requantize.cc:293-373) for compute_dtype float32 /
+// float64, with the non-SSE4.1 rounding forms of :127-173 (the MRT llvm target has no -mcpu).
+// Every step is one IEEE operation in F (this file compiles with fp contract off); the float ->
+// int casts reproduce x86-64's cvtt* instructions, which the reference's LLVM fptosi lowers to:
+// truncation, INT_MIN of the target width for NaN / out-of-range input.
+struct RqFp {
+  int32_t rounding, scaled;
+  double m;
+  const double* ms;
+  int32_t zp_in;
+  const int32_t* zps;
+  int32_t zp_out;
+};
+
+template <typename F> struct FpInt;                 // Cast(.., Int(Bits))
+template <> struct FpInt<float> { using T = int32_t; };
+template <> struct FpInt<double> { using T = int64_t; };
+
+template <typename I, typename F>
+__device__ __forceinline__ I fptosi_x86(F v) {
+  constexpr F lim = sizeof(I) == 4 ? (F)2147483648.0 : (F)9223372036854775808.0;
+  return (v >= -lim && v < lim) ? (I)v : std::numeric_limits<I>::min();  // NaN fails both compares
+}
+
+template <typename F>
+__device__ __forceinline__ F fp_upward(F t) {  // requantize.cc:154-172
+  using I = typename FpInt<F>::T;
+  const F biased = t + (F)0.5;
+  const F bf = (F)fptosi_x86<I>(biased);
+  const F r = (biased == bf || biased >= (F)0) ? bf : bf - (F)1;
+  return __builtin_isfinite(t) ? r : t;
+}
+
+template <typename F>
+__device__ __forceinline__ F fp_tonearest(F t) {  // requantize.cc:129-146
+  using I = typename FpInt<F>::T;
+  const F mult = t < (F)0 ? (F)-1 : (F)1;
+  const F biased = t + (F)0.5 * mult;
+  const F bm = biased * mult;
+  const F r = (F)fptosi_x86<I>(bm) * mult;
+  return __builtin_isfinite(t) ? r : t;
+}
+
+// one element: int32 input (already cast from the data dtype) -> int32 (before any output clip)
+template <typename F>
+__device__ __forceinline__ int32_t rq_fp(int32_t x, int c, const RqFp& p) {
+  F t = (F)x;
+  t = t - (F)(p.zps ? p.zps[c] : p.zp_in);
+  if (p.ms) t = t * (F)p.ms[c];
+  else if (p.scaled) t = (F)p.m * t;
+  t = t + (F)p.zp_out;
+  t = p.rounding == TK_ROUND_UPWARD ? fp_upward(t) : fp_tonearest(t);
+  return fptosi_x86<int32_t>(t);
+}
+
+static RqFp rq_fp_params(const tk_requantize_fp_attrs& a) {
+  RqFp p{};
+  p.rounding = a.rounding;
+  p.scaled = a.scaled;
+  p.m = a.multiplier;
+  p.ms = a.multipliers;
+  p.zp_in = a.input_zero_point;
+  p.zps = a.input_zero_points;
+  p.zp_out = a.output_zero_point;
+  return p;
+}
+
+static bool fp_attrs_ok(const tk_requantize_fp_attrs& a) {
+  return (a.bits == 32 || a.bits == 64) && (a.rounding == TK_ROUND_UPWARD || a.rounding == TK_ROUND_TONEAREST);
+}
+
+template <typename F, typename Tin, typename Tout>
+__global__ __launch_bounds__(kQBlock) void requantize_fp_kernel(const Tin* __restrict__ x, Tout* __restrict__ y,
+                                                                 int64_t n, RqFp p, int32_t inner, int32_t C,
+                                                                 int32_t clip) {
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    const int c = (p.ms || p.zps) ? chan(i, inner, C) : 0;
+    int32_t q = rq_fp<F>((int32_t)x[i], c, p);
+    if (clip) q = (int32_t)std::min<int64_t>(std::max<int64_t>(q, Lim<Tout>::lo), Lim<Tout>::hi);
+    y[i] = (Tout)q;
+  }
+}
+
+int requantize_fp_impl(const tk_tensor* x, tk_tensor* y, const tk_requantize_fp_attrs* a, hipStream_t s) {
+  TK_CHECK_ARG(x && y && a, "null argument");
+  TK_CHECK_ARG(compact(x) && compact(y) && numel(x) == numel(y), "bad tensors");
+  if (!fp_attrs_ok(*a)) {
+    set_error("tk_requantize_fp: bits must be 32 or 64 and rounding UPWARD or TONEAREST");
+    return TK_ERR_INVALID_ARG;
+  }
+  int32_t inner = 1, C = 1;
+  if ((a->multipliers || a->input_zero_points) && !axis_inner(x, a->axis, &inner, &C)) {
+    set_error("tk_requantize_fp: bad axis");
+    return TK_ERR_INVALID_ARG;
+  }
+  const RqFp p = rq_fp_params(*a);
+  const int64_t n = numel(x);
+  const int clip = !is_int(y, 32);
+  return dispatch_q(x, [&](auto ti) -> int {
+    return dispatch_q(y, [&](auto to) -> int {
+      using Tin = decltype(ti);
+      using Tout = decltype(to);
+      if (a->bits == 32)
+        hipLaunchKernelGGL((requantize_fp_kernel<float, Tin, Tout>), dim3(qgrid(n)), dim3(kQBlock), 0, s,
+                           (const Tin*)ptr(x), (Tout*)ptr(y), n, p, inner, C, clip);
+      else
+        hipLaunchKernelGGL((requantize_fp_kernel<double, Tin, Tout>), dim3(qgrid(n)), dim3(kQBlock), 0, s,
+                           (const Tin*)ptr(x), (Tout*)ptr(y), n, p, inner, C, clip);
+      TK_LAUNCH_CHECK();
+      return TK_OK;
+    });
+  });
+}
+
+// qnn.add / subtract / mul with RequantizeLowerFP inner requantizes (int32 results, no clip)
+template <typename F, typename T, int OP, bool FLAT>
+__global__ __launch_bounds__(kQBlock) void qnn_binary_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                                 T* __restrict__ y, int64_t n, BinGeom g, RqFp pa,
+                                                                 RqFp pb, RqFp po, int32_t zp_c, int32_t up_a,
+                                                                 int32_t up_b) {
+  const int64_t stride = (int64_t)gridDim.x * kQBlock;
+  for (int64_t i = blockIdx.x * (int64_t)kQBlock + threadIdx.x; i < n; i += stride) {
+    int64_t ia, ib;
+    int ca, cb, co;
+    bin_walk<FLAT>(i, g, &ia, &ib, &ca, &cb, &co);
+    const int32_t x0 = (int32_t)a[ia], x1 = (int32_t)b[ib];
+    int32_t o;
+    if constexpr (OP == TK_QB_MUL) {
+      const int32_t sa = (int32_t)((uint32_t)x0 - (uint32_t)(pa.zps ? pa.zps[ca] : pa.zp_in));
+      const int32_t sb = (int32_t)((uint32_t)x1 - (uint32_t)(pb.zps ? pb.zps[cb] : pb.zp_in));
+      o = rq_fp<F>((int32_t)((uint32_t)sa * (uint32_t)sb), co, po);
+    } else {
+      const int32_t ra = up_a ? x0 : rq_fp<F>(x0, ca, pa);
+      const int32_t rb = up_b ? x1 : rq_fp<F>(x1, cb, pb);
+      if constexpr (OP == TK_QB_ADD) {
+        o = (int32_t)((uint32_t)ra + (uint32_t)rb - (uint32_t)zp_c);
+      } else {
+        o = (int32_t)((uint32_t)ra - (uint32_t)rb + (uint32_t)zp_c);
+      }
+    }
+    y[i] = (T)std::min<int64_t>(std::max<int64_t>(o, Lim<T>::lo), Lim<T>::hi);
+  }
+}
+
+int qnn_binary_fp_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* y, const tk_qnn_binary_fp_attrs* at,
+                       hipStream_t s) {
+  TK_CHECK_ARG(a && b && y && at, "null argument");
+  TK_CHECK_ARG(compact(a) && compact(b) && compact(y), "strided tensors are not supported");
+  TK_CHECK_ARG(dt_of(a) == dt_of(b) && dt_of(a) == dt_of(y), "dtype mismatch");
+  TK_CHECK_ARG(at->op >= TK_QB_ADD && at->op <= TK_QB_MUL, "bad op");
+  TK_CHECK_ARG(y->ndim <= 6 && a->ndim <= y->ndim && b->ndim <= y->ndim, "up to 6-D, operands no wider than the output");
+  const bool mul = at->op == TK_QB_MUL;
+  const int bits = mul ? at->out.bits : at->lhs.bits;
+  TK_CHECK_ARG(fp_attrs_ok(mul ? at->out : at->lhs) && (mul || fp_attrs_ok(at->rhs)) &&
+               (mul || at->rhs.bits == bits), "bits must be 32 or 64 on every side, rounding UPWARD or TONEAREST");
+  BinGeom g{};
+  bool same = false;
+  if (bin_geometry(a, b, y, &g, &same) != TK_OK) return TK_ERR_SHAPE;
+  const RqFp pa = rq_fp_params(at->lhs), pb = rq_fp_params(at->rhs), po = rq_fp_params(at->out);
+  const bool axis_a = pa.zps || (!mul && !at->lhs_upcast && pa.ms);
+  const bool axis_b = pb.zps || (!mul && !at->rhs_upcast && pb.ms);
+  const bool axis_o = mul && po.ms;
+  g.lax = axis_a ? bin_out_axis(a, y, at->lhs.axis) : -1;
+  g.rax = axis_b ? bin_out_axis(b, y, at->rhs.axis) : -1;
+  g.oax = axis_o ? bin_out_axis(a, y, at->out.axis) : -1;
+  const bool flat = same && !axis_a && !axis_b && !axis_o;
+  const int64_t n = numel(y);
+  return dispatch_q(y, [&](auto tag) -> int {
+    using T = decltype(tag);
+    auto go = [&](auto f_tag, auto op_tag, auto flat_tag) -> int {
+      using F = decltype(f_tag);
+      constexpr int OP = decltype(op_tag)::value;
+      constexpr bool FLAT = decltype(flat_tag)::value;
+      hipLaunchKernelGGL((qnn_binary_fp_kernel<F, T, OP, FLAT>), dim3(qgrid(n)), dim3(kQBlock), 0, s,
+                         (const T*)ptr(a), (const T*)ptr(b), (T*)ptr(y), n, g, pa, pb, po, at->output_zero_point,
+                         at->lhs_upcast, at->rhs_upcast);
+      TK_LAUNCH_CHECK();
+      return TK_OK;
+    };
+    auto by_op = [&](auto f_tag) -> int {
+      using TF = std::true_type;
+      using FF = std::false_type;
+      switch (at->op) {
+        case TK_QB_ADD: return flat ? go(f_tag, std::integral_constant<int, TK_QB_ADD>{}, TF{})
+                                    : go(f_tag, std::integral_constant<int, TK_QB_ADD>{}, FF{});
+        case TK_QB_SUBTRACT: return flat ? go(f_tag, std::integral_constant<int, TK_QB_SUBTRACT>{}, TF{})
+                                         : go(f_tag, std::integral_constant<int, TK_QB_SUBTRACT>{}, FF{});
+        default: return flat ? go(f_tag, std::integral_constant<int, TK_QB_MUL>{}, TF{})
+                             : go(f_tag, std::integral_constant<int, TK_QB_MUL>{}, FF{});
+      }
+    };
+    return bits == 32 ? by_op(0.0f) : by_op(0.0);
+  });
+}
+
 }  // namespace tk
 
 extern "C" {
@@ -711,6 +926,13 @@ int tk_qnn_simulated_quantize(const tk_tensor* data, tk_tensor* out, const tk_si
 }
 int tk_qnn_simulated_dequantize(const tk_tensor* data, tk_tensor* out, const tk_simq_attrs* attrs, void* stream) {
   return tk::qnn_simulated_impl(false, data, out, attrs, tk::as_stream(stream));
+}
+int tk_requantize_fp(const tk_tensor* data, tk_tensor* out, const tk_requantize_fp_attrs* attrs, void* stream) {
+  return tk::requantize_fp_impl(data, out, attrs, tk::as_stream(stream));
+}
+int tk_qnn_binary_fp(const tk_tensor* lhs, const tk_tensor* rhs, tk_tensor* out, const tk_qnn_binary_fp_attrs* attrs,
+                     void* stream) {
+  return tk::qnn_binary_fp_impl(lhs, rhs, out, attrs, tk::as_stream(stream));
 }
 
 }  // extern "C"

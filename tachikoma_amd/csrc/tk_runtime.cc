@@ -68,6 +68,9 @@ int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, cons
                             int32_t* algos, int max_algos);
 int qnn_leaky_relu_impl(const tk_tensor* x, tk_tensor* y, const tk_leaky_relu_attrs* a, hipStream_t s);
 int qnn_simulated_impl(bool quant, const tk_tensor* x, tk_tensor* y, const tk_simq_attrs* a, hipStream_t s);
+int requantize_fp_impl(const tk_tensor* x, tk_tensor* y, const tk_requantize_fp_attrs* a, hipStream_t s);
+int qnn_binary_fp_impl(const tk_tensor* a, const tk_tensor* b, tk_tensor* y, const tk_qnn_binary_fp_attrs* at,
+                       hipStream_t s);
 int qnn_lookup_impl(const tk_tensor* x, tk_tensor* y, const void* table, hipStream_t s);
 int qnn_conv2d_transpose_impl(const tk_tensor* x, const tk_tensor* w, tk_tensor* y, const tk_conv2d_transpose_attrs* a,
                               hipStream_t s);
@@ -224,6 +227,10 @@ static int run_node(Node& n, hipStream_t s) {
     case TK_NODE_SIM_QUANTIZE:
     case TK_NODE_SIM_DEQUANTIZE:
       return qnn_simulated_impl(d.kind == TK_NODE_SIM_QUANTIZE, i0, o, &d.attrs.simq, s);
+    case TK_NODE_REQUANTIZE_FP:
+      return requantize_fp_impl(i0, o, &d.attrs.requantize_fp, s);
+    case TK_NODE_QNN_BINARY_FP:
+      return qnn_binary_fp_impl(i0, i1, o, &d.attrs.qnn_binary_fp, s);
   }
   set_error("tk_module: unknown node kind " + std::to_string(d.kind));
   return TK_ERR_INVALID_ARG;

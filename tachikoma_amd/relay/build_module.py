@@ -112,11 +112,38 @@ def _resolve_rounding(attrs) -> Tuple[str, str]:
         cd = attrs.get("cfg_compute_dtype") or "int64"
     if r not in ("UPWARD", "TONEAREST"):
         raise ValueError(f"qnn.requantize: rounding must be UPWARD or TONEAREST, got {r}")
-    if cd != "int64":
-        raise UnsupportedError(
-            f"qnn.requantize compute_dtype={cd}: the reference selects the float path only for llvm "
-            "targets with an SSE4.1 -mcpu; this engine implements the pinned integer (int64) path")
+    if cd not in ("int64", "float32", "float64"):
+        # RequantizeLower's check (requantize.cc:389-392)
+        raise ValueError(f"qnn.requantize: compute_dtype must be int64, float32 or float64, got {cd}")
     return r, cd
+
+
+def fp_requantize_plan(input_scale, output_scale) -> Tuple[int, float, Optional[np.ndarray]]:
+    """RequantizeLowerFP's constants (src/relay/qnn/op/requantize.cc:310-341): per-tensor, the
+    double multiplier double(s_in) / double(s_out) and whether it is applied at all (skipped when
+    the two float32 scales are structurally equal, :313); per-axis, one double per channel (always
+    applied).  The kernel converts them to the compute type as MakeConstantScalar /
+    MakeConstantTensor do.  Returns (scaled, multiplier, multipliers or None)."""
+    s_in = np.asarray(input_scale, dtype=np.float32)
+    s_out = np.float32(output_scale)
+    if s_in.ndim == 0:
+        scaled = int(not _is_equal_scalar(s_in, np.asarray(s_out)))
+        return scaled, float(np.float64(s_in)) / float(np.float64(s_out)), None
+    ms = np.array([float(np.float64(v)) / float(np.float64(s_out)) for v in s_in.reshape(-1)], dtype=np.float64)
+    return 1, 0.0, ms
+
+
+def _fp_side(a: Dict[str, Any], consts: Dict[str, np.ndarray], side: str, s_in, s_out, axis: int, nd: int,
+             cd: str) -> None:
+    """The RequantizeLowerFP constants of one inner requantize into attrs ``{side}_fp_*`` and the
+    per-axis const ``{side}_fp_multipliers`` (zero points stay in ``{side}_zero_point(s)``)."""
+    scaled, m, ms = fp_requantize_plan(s_in, s_out)
+    a[f"{side}_fp_bits"] = 32 if cd == "float32" else 64
+    a[f"{side}_fp_scaled"] = scaled
+    a[f"{side}_fp_multiplier"] = m
+    a[f"{side}_axis"] = _norm_axis(axis, nd)
+    if ms is not None:
+        consts[f"{side}_fp_multipliers"] = ms
 
 
 def requantize_plan(input_scale: np.ndarray, output_scale, rounding: str):
@@ -248,13 +275,19 @@ def _rq_side(a: Dict[str, Any], consts: Dict[str, np.ndarray], side: str, s_in, 
     a["output_zero_point"] = int(np.asarray(zp_out))
 
 
-def _qnn_rounding(a: Dict[str, Any]) -> str:
+def _qnn_rounding(a: Dict[str, Any], float_ok: bool = False) -> str:
     """The requantize rounding a QNN canonicalization's inner ``Requantize`` gets: the
-    requantize_config in effect when the op was built, else UPWARD (qnn/utils.h:106-122)."""
+    requantize_config in effect when the op was built, else UPWARD (qnn/utils.h:106-122).  The
+    config's compute_dtype goes to ``a["compute_dtype"]``; a float one is implemented for
+    qnn.add / subtract / mul (``float_ok``) and refused elsewhere."""
     r = a.pop("cfg_rounding", None) or "UPWARD"
     cd = a.pop("cfg_compute_dtype", None) or "int64"
-    if cd != "int64":
-        raise UnsupportedError(f"compute_dtype={cd}: only the pinned integer (int64) requantize path is implemented")
+    if cd not in ("int64", "float32", "float64"):
+        raise ValueError(f"compute_dtype must be int64, float32 or float64, got {cd}")
+    if cd != "int64" and not float_ok:
+        raise UnsupportedError(f"compute_dtype={cd}: the float requantize form is implemented for qnn.requantize, "
+                               "qnn.add, qnn.subtract and qnn.mul only")
+    a["compute_dtype"] = cd
     return r
 
 
@@ -265,8 +298,9 @@ def _lower_binary(call: Call, a: Dict[str, Any], consts: Dict[str, np.ndarray]) 
     lhs, rhs = call.args[0], call.args[1]
     vals = [_scalar(call.args[i], f"{op} param") for i in range(2, 8)]
     ls, lz, rs, rz, os_, oz = [np.asarray(v) for v in vals]
-    rounding = _qnn_rounding(a)
+    rounding = _qnn_rounding(a, float_ok=True)
     a["rounding"] = rounding
+    cd = a["compute_dtype"]
     ln, rn = len(lhs.shape), len(rhs.shape)
     if op in ("qnn.add", "qnn.subtract"):
         for side, s_, z_, ax, nd in (("lhs", ls, lz, a["lhs_axis"], ln), ("rhs", rs, rz, a["rhs_axis"], rn)):
@@ -278,6 +312,8 @@ def _lower_binary(call: Call, a: Dict[str, Any], consts: Dict[str, np.ndarray]) 
                           f"{side}_zero_point": int(z_), f"{side}_axis": 0})
             else:
                 _rq_side(a, consts, side, s_, z_, os_, oz, ax, nd, rounding)
+                if cd != "int64":
+                    _fp_side(a, consts, side, s_, os_, ax, nd, cd)
         a["output_zero_point"] = int(oz)
         # scalar floats for the fused residual-join kernels (add_block / conv-block join)
         a.update(lhs_scale=float(np.float32(ls)) if ls.ndim == 0 else None,
@@ -312,6 +348,8 @@ def _lower_binary(call: Call, a: Dict[str, Any], consts: Dict[str, np.ndarray]) 
             a[f"{side}_zero_point"] = 0
             consts[f"{side}_zero_points"] = z_.reshape(-1).astype(np.int32)
     _rq_side(a, consts, "out", new_scale, np.int32(0), os_, oz, out_axis, ln, rounding)
+    if cd != "int64":
+        _fp_side(a, consts, "out", new_scale, os_, out_axis, ln, cd)
     a["per_tensor"] = 0
 
 
@@ -375,6 +413,12 @@ def _lower_call(index: int, name: str, call: Call, names) -> PlanOp:
         else:
             a["multiplier"] = int(ms[0])
             a["shift"] = int(ss[0])
+        if cd != "int64":
+            # RequantizeLowerFP<32|64> (requantize.cc:293-373): the device runs tk_requantize_fp
+            scaled, m, fms = fp_requantize_plan(s_in, s_out)
+            a.update(fp_bits=32 if cd == "float32" else 64, fp_scaled=scaled, fp_multiplier=m)
+            if fms is not None:
+                consts["fp_multipliers"] = fms
         if np.ndim(zp_in) == 0:
             a["input_zero_point"] = int(zp_in)
         else:
@@ -655,7 +699,8 @@ def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
         if len(cs) != 1 or cs[0].op != "qnn.add" or cs[0].name in taken:
             return None
         add = cs[0]
-        if add.out.dtype != rq.out.dtype or add.inputs[0] == add.inputs[1] or not add.attrs.get("per_tensor"):
+        if add.out.dtype != rq.out.dtype or add.inputs[0] == add.inputs[1] or not add.attrs.get("per_tensor") \
+                or add.attrs.get("compute_dtype", "int64") != "int64":
             return None
         other = add.inputs[1] if add.inputs[0] == rq.name else add.inputs[0]
         if plan.tensor(other).shape != rq.out.shape or plan.tensor(other).dtype != rq.out.dtype:
@@ -679,7 +724,7 @@ def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
             b = first_consumer(op, ("nn.bias_add",))
             rq = first_consumer(b, ("qnn.requantize",)) if b is not None and b.attrs["axis"] == 1 else None
             if rq is not None and rq.out.dtype in ("int8", "uint8") and rq.attrs["channel_axis"] == 1 \
-                    and b.out.dtype == "int32":
+                    and b.out.dtype == "int32" and rq.attrs.get("compute_dtype", "int64") == "int64":
                 chain = [op, b, rq]
                 add = residual_add(rq, chain) if op.op == "qnn.conv2d" else None
                 if add is not None:
@@ -695,6 +740,7 @@ def exec_groups(plan: Plan, fuse: bool = True) -> List[ExecGroup]:
                 place(pos[add.name] if add is not None else pos[op.name], ExecGroup(kind, chain))
                 continue
         if fuse and op.op == "qnn.add" and op.out.dtype in ("int8", "uint8") and op.attrs.get("per_tensor") and \
+                op.attrs.get("compute_dtype", "int64") == "int64" and \
                 all(plan.tensor(x).shape == op.out.shape for x in op.inputs[:2]):
             chain = [op]
             cl = first_consumer(op, ("clip", "nn.relu"))

@@ -227,6 +227,10 @@ class _Builder:
     def lower(self, p) -> None:
         self.origin, self.k = p.name, 0
         a = p.attrs
+        if a.get("compute_dtype", "int64") != "int64":
+            # RequantizeLowerFP's float op sequence (requantize.cc:293-373) is not restated here
+            from .build_module import UnsupportedError
+            raise UnsupportedError(f"canonical dump of {p.op} under compute_dtype={a['compute_dtype']}")
         ins = [self.val[x] for x in p.inputs]
         if p.op in ("qnn.conv2d", "qnn.dense"):
             d = self.subtract_scalar(self.cast(ins[0], "int16"), a["input_zero_point"])

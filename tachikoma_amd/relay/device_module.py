@@ -263,6 +263,48 @@ class DeviceModule:
             r.input_zero_points = self._dev_i32(op.consts["input_zero_points"]).data_ptr()
         r.output_zero_point = a["output_zero_point"]
 
+    def _fp_side(self, r, a, consts, prefix: str, axis: int, zp_key: str, zps_key: str, zp_out: int) -> None:
+        """One tk_requantize_fp_attrs from a lowered plan's ``{prefix}fp_*`` attrs / consts."""
+        r.bits = a[f"{prefix}fp_bits"]
+        r.rounding = _lib.TK_ROUND_UPWARD if a["rounding"] == "UPWARD" else _lib.TK_ROUND_TONEAREST
+        r.axis = axis
+        r.scaled = a[f"{prefix}fp_scaled"]
+        r.multiplier = a[f"{prefix}fp_multiplier"]
+        if f"{prefix}fp_multipliers" in consts:
+            r.multipliers = self._dev_const(np.asarray(consts[f"{prefix}fp_multipliers"], np.float64)).data_ptr()
+        r.input_zero_point = a[zp_key]
+        if zps_key in consts:
+            r.input_zero_points = self._dev_i32(consts[zps_key]).data_ptr()
+        r.output_zero_point = zp_out
+
+    def _fill_rq_fp(self, r, op: PlanOp):
+        """tk_requantize_fp_attrs of a qnn.requantize built under a float compute_dtype."""
+        a = op.attrs
+        self._fp_side(r, a, op.consts, "", a["channel_axis"], "input_zero_point", "input_zero_points",
+                      a["output_zero_point"])
+
+    def _fill_binary_fp(self, qb, op: PlanOp) -> None:
+        """tk_qnn_binary_fp_attrs from a lowered qnn.add / subtract / mul (float compute_dtype)."""
+        a = op.attrs
+        qb.op = _lib.TK_QB[op.op]
+        mul = op.op == "qnn.mul"
+        for side in ("lhs", "rhs", "out"):
+            if f"{side}_mode" not in a:
+                continue
+            r = getattr(qb, side)
+            if f"{side}_fp_bits" in a:
+                self._fp_side(r, a, op.consts, f"{side}_", a[f"{side}_axis"], f"{side}_zero_point", f"{side}_zero_points",
+                              0 if mul and side != "out" else a["output_zero_point"])
+            else:  # an upcast side (add / subtract) or a mul operand: only its zero point(s) are read
+                r.bits = 32 if a["compute_dtype"] == "float32" else 64
+                r.axis = a[f"{side}_axis"]
+                r.input_zero_point = a[f"{side}_zero_point"]
+                if f"{side}_zero_points" in op.consts:
+                    r.input_zero_points = self._dev_i32(op.consts[f"{side}_zero_points"]).data_ptr()
+        qb.lhs_upcast = a.get("lhs_upcast", 0)
+        qb.rhs_upcast = a.get("rhs_upcast", 0)
+        qb.output_zero_point = a["output_zero_point"]
+
     def _is_mfma_conv(self, op: PlanOp) -> bool:
         ca = _lib.tk_conv2d_attrs()
         self._conv_attrs(ca, op)
@@ -378,9 +420,15 @@ class DeviceModule:
                     n.kind = _lib.NODE_KINDS["qnn.dense"]
                     self._dense_attrs(n.attrs.dense, op)
                     n.ext[0] = self._scratch(self.lib.tk_qnn_dense_workspace_bytes(ins[0].ptr, ins[1].ptr)).data_ptr()
+                elif kind == "qnn.requantize" and a.get("compute_dtype", "int64") != "int64":
+                    n.kind = _lib.NODE_KINDS["requantize_fp"]
+                    self._fill_rq_fp(n.attrs.requantize_fp, op)
                 elif kind == "qnn.requantize":
                     n.kind = _lib.NODE_KINDS["qnn.requantize"]
                     self._fill_rq(n.attrs.requantize, op)
+                elif kind in ("qnn.add", "qnn.subtract", "qnn.mul") and a.get("compute_dtype", "int64") != "int64":
+                    n.kind = _lib.NODE_KINDS["qnn_binary_fp"]
+                    self._fill_binary_fp(n.attrs.qnn_binary_fp, op)
                 elif kind == "qnn.add" and a.get("per_tensor"):
                     n.kind = _lib.NODE_KINDS["qnn.add"]
                     _fill_qnn_add(n.attrs.qnn_add, a)

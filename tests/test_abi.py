@@ -52,6 +52,9 @@ int main(void) {
   P(tk_leaky_relu_attrs) P(tk_conv2d_transpose_attrs) O(tk_leaky_relu_attrs, alpha_multiplier)
   O(tk_leaky_relu_attrs, zp_shift) O(tk_conv2d_transpose_attrs, kernel_zero_points) P(tk_simq_attrs)
   O(tk_simq_attrs, dtype_code) O(tk_simq_attrs, zero_points)
+  P(tk_requantize_fp_attrs) P(tk_qnn_binary_fp_attrs) O(tk_requantize_fp_attrs, multiplier)
+  O(tk_requantize_fp_attrs, input_zero_points) O(tk_requantize_fp_attrs, output_zero_point)
+  O(tk_qnn_binary_fp_attrs, rhs) O(tk_qnn_binary_fp_attrs, out) O(tk_qnn_binary_fp_attrs, output_zero_point)
   return 0;
 }
 """
@@ -97,6 +100,14 @@ def test_ctypes_layout_matches_c(tmp_path):
         "tk_simq_attrs": ctypes.sizeof(_lib.tk_simq_attrs),
         "tk_simq_attrs.dtype_code": _lib.tk_simq_attrs.dtype_code.offset,
         "tk_simq_attrs.zero_points": _lib.tk_simq_attrs.zero_points.offset,
+        "tk_requantize_fp_attrs": ctypes.sizeof(_lib.tk_requantize_fp_attrs),
+        "tk_qnn_binary_fp_attrs": ctypes.sizeof(_lib.tk_qnn_binary_fp_attrs),
+        "tk_requantize_fp_attrs.multiplier": _lib.tk_requantize_fp_attrs.multiplier.offset,
+        "tk_requantize_fp_attrs.input_zero_points": _lib.tk_requantize_fp_attrs.input_zero_points.offset,
+        "tk_requantize_fp_attrs.output_zero_point": _lib.tk_requantize_fp_attrs.output_zero_point.offset,
+        "tk_qnn_binary_fp_attrs.rhs": _lib.tk_qnn_binary_fp_attrs.rhs.offset,
+        "tk_qnn_binary_fp_attrs.out": _lib.tk_qnn_binary_fp_attrs.out.offset,
+        "tk_qnn_binary_fp_attrs.output_zero_point": _lib.tk_qnn_binary_fp_attrs.output_zero_point.offset,
     }
     for k, v in py.items():
         assert int(got[k]) == v, (k, got[k], v)

@@ -10,13 +10,16 @@ def _id(c):
     return f"{c['name']}-{c['attrs'].get('rounding', '')}"
 
 
+# test_op_qnn_requantize.py:25 runs every case under the three compute dtypes against the same goldens
+@pytest.mark.parametrize("compute_dtype", ["int64", "float32", "float64"])
 @pytest.mark.parametrize("case", load_cases("qnn.requantize"), ids=_id)
-def test_requantize_kat(case):
+def test_requantize_kat(case, compute_dtype):
     a = case["attrs"]
     x = load_array(case["inputs"]["data"])
     out = ref.requantize(x, scale_const(a["input_scale"]), np.int32(a["input_zero_point"]),
                          np.float32(a["output_scale"]), np.int32(a["output_zero_point"]),
-                         axis=a["axis"], rounding=a["rounding"], out_dtype=a["out_dtype"])
+                         axis=a["axis"], rounding=a["rounding"], out_dtype=a["out_dtype"],
+                         compute_dtype=compute_dtype)
     np.testing.assert_array_equal(out, load_array(case["expected"]))
     assert out.dtype == np.dtype(a["out_dtype"])
 

@@ -64,11 +64,38 @@ def test_unsupported_paths_fail_loudly():
     m = zoo.lenet5(batch=1)
     with pytest.raises(UnsupportedError):
         relay.build(m.mod, target="llvm", params=m.params)
-    x = relay.var("x", shape=(4,), dtype="int32")
+    # a float requantize form inside qnn.concatenate is not implemented: refused, not approximated
+    a = relay.var("a", shape=(1, 4), dtype="int8")
+    b = relay.var("b", shape=(1, 4), dtype="int8")
     with qnn.op.requantize_config(compute_dtype="float32"):
-        y = qnn.op.requantize(x, 0.5, 0, 0.25, 0)
+        y = qnn.op.concatenate(relay.Tuple([a, b]), [relay.const(0.5), relay.const(0.25)],
+                               [relay.const(0), relay.const(0)], relay.const(0.5), relay.const(0), axis=1)
     with pytest.raises(UnsupportedError):
         lower(relay.IRModule.from_expr(y))
+    x = relay.var("x", shape=(4,), dtype="int32")
+    with pytest.raises(ValueError):
+        lower(relay.IRModule.from_expr(qnn.op.requantize(x, 0.5, 0, 0.25, 0, compute_dtype="float16")))
+
+
+@pytest.mark.parametrize("cd", ["float32", "float64"])
+def test_float_compute_dtype_plan(cd):
+    """requantize_config(compute_dtype=float32|float64) selects RequantizeLowerFP<32|64>
+    (requantize.cc:392-403): the plan carries the double multipliers and the 'scaled' flag, and the
+    conv blocks are not fused (their epilogue is the int64 form) -- the requantize runs alone."""
+    x = relay.var("x", shape=(4,), dtype="int32")
+    with qnn.op.requantize_config(compute_dtype=cd):
+        y = qnn.op.requantize(x, 0.5, 0, 0.25, 0)
+        y2 = qnn.op.requantize(x, 0.5, 0, 0.5, 3)
+    rq = lower(relay.IRModule.from_expr(y)).ops[0]
+    assert rq.attrs["compute_dtype"] == cd and rq.attrs["fp_bits"] == (32 if cd == "float32" else 64)
+    assert rq.attrs["fp_scaled"] == 1 and rq.attrs["fp_multiplier"] == 2.0
+    assert lower(relay.IRModule.from_expr(y2)).ops[0].attrs["fp_scaled"] == 0   # equal scales skip the multiply
+    with qnn.op.requantize_config(compute_dtype=cd):
+        m = zoo.lenet5(batch=1)
+    plan = lower(m.mod, m.params)
+    kinds = [g.kind for g in exec_groups(plan)]
+    assert "conv_block" not in kinds and "dense_block" not in kinds
+    assert all(o.attrs["compute_dtype"] == cd for o in plan.ops if o.op == "qnn.requantize")
 
 
 def test_requantize_config_scope_resolution():

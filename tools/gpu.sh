@@ -20,6 +20,8 @@
 #   gloo2      2-rank rehearsal on one GPU (gloo collectives; both ranks' records cross one PCIe link)
 #   hostmem    host DRAM write / read bandwidth of the GPU's NUMA node, alone and beside a traced bench
 #   tests:<k>  pytest -m gpu -k <k>               file:<path>  pytest -m gpu of one test file
+# BARGS="..." is appended to every bench.py command line of bench / findstep / prof / pmc / layers
+# (e.g. BARGS="--model resnet18 --tune-table <table>" for BASELINE configs 3 and 5).
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:?tag}
@@ -39,9 +41,9 @@ for r in "$@"; do
   case "$r" in
     suite) run 900 suite.log python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) run 300 smoke.log python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) run 400 bench.json python3 -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench) run 400 bench.json python3 -u bench.py --gpus 1 --steps 20 --warmup 5 $BARGS ;;
     findstep) run 400 bench_find.json python3 -u bench.py --gpus 1 --steps 5 --warmup 2 --skip-cpu \
-        --tune-table none --write-tune-table "$O/tune_table.json" --tune-report "$O/find_step.json" ;;
+        --tune-table none --write-tune-table "$O/tune_table.json" --tune-report "$O/find_step.json" $BARGS ;;
     host) run 400 bench_host.json python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --skip-cpu --run-mode host ;;
     copytrace)
       run 400 copytrace.log bash tools/rocprof_one_hsa.sh --memory-copy-trace --kernel-trace --stats \
@@ -55,10 +57,10 @@ for r in "$@"; do
         -d "$O/copy_probe" -o run -- ./tools/probe_copies tools/resnet50_b64_record_sizes.txt 1 ;;
     copyprobe) run 300 copyprobe.jsonl ./tools/probe_copies tools/resnet50_b64_record_sizes.txt 3 ;;
     prof) run 400 prof.log rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
-        python3 -u bench.py --skip-cpu ;;
-    pmc) run 900 pmc.log bash tools/pmc.sh "$O/pmc" "$O/pmc/summary.json" ;;
+        python3 -u bench.py --skip-cpu $BARGS ;;
+    pmc) run 900 pmc.log bash tools/pmc.sh "$O/pmc" "$O/pmc/summary.json" $BARGS ;;
     layers) run 400 layers.log rocprofv3 --kernel-trace --output-format csv -d "$O/layers" -o run -- \
-        python3 -u bench.py --steps 3 --warmup 1 --skip-cpu --no-trace ;;
+        python3 -u bench.py --steps 3 --warmup 1 --skip-cpu --no-trace $BARGS ;;
     filesink)
       (df -hT /tmp . ; cat /proc/mounts) > "$O/mounts.txt" 2>&1
       run 600 bench_file.json python3 -u bench.py --gpus 1 --steps 10 --warmup 3 --skip-cpu --sink file --out-dir /tmp

@@ -17,8 +17,8 @@ def main(path, model="resnet50", batch=64):
     plan = lower(m.mod, m.params)
     groups = exec_groups(plan)
     blocks = [g for g in groups if g.kind in ("conv_block", "dense_block")]
-    fams = ("gemm_i8_kernel", "direct_conv_kernel", "conv_img_kernel", "conv_pf_kernel", "dense_tile_kernel",
-            "dense_slices_epilogue_kernel")
+    fams = ("gemm_i8_kernel", "direct_conv_kernel", "dw3x3_kernel", "conv_img_kernel", "conv_pf_kernel",
+            "dense_tile_kernel", "dense_slices_epilogue_kernel")
     g_rows = [r for r in rows if any(f in r["Kernel_Name"] for f in fams)]
     # idle time before each launch: end of the previous kernel (any) to this start
     prev_end = {}
@@ -64,6 +64,7 @@ def main(path, model="resnet50", batch=64):
             i += 1
     print(f"{'layer':34s} {'us':>8s} {'GB/s':>8s} {'TOPS':>7s} {'gap us':>7s}  kernel")
     tot = tgap = 0
+    cls = defaultdict(lambda: [0, 0.0, 0.0, 0.0])  # layer class -> [layers, us, bytes, ops]
     for i, g in enumerate(blocks):
         head = g.ops[0]
         w = plan.tensor(head.inputs[1]).shape
@@ -72,17 +73,30 @@ def main(path, model="resnet50", batch=64):
         if head.op == "qnn.conv2d":
             nb, co, oh, ow = head.out.shape
             macs = nb * co * oh * ow * w[1] * w[2] * w[3]
-            desc = f"conv {w[1]*(co//w[0]) if False else x.shape[1]}->{co} k{w[2]} s{head.attrs['strides'][0]} {oh}x{ow}"
+            grp = head.attrs.get("groups", 1)
+            desc = f"conv {x.shape[1]}->{co} k{w[2]} s{head.attrs['strides'][0]} {oh}x{ow}" + \
+                (" dw" if grp > 1 and grp == co else (f" g{grp}" if grp > 1 else ""))
+            kind = "depthwise 3x3" if grp > 1 else (f"{w[2]}x{w[3]} conv")
         else:
             macs = head.out.shape[0] * w[0] * w[1]
             desc = f"dense {w[1]}->{w[0]}"
+            kind = "dense"
         b = x.nbytes + int(w[0] * w[1] * w[2] * w[3] if len(w) == 4 else w[0] * w[1]) + outb
         d = sorted(dur[i])[len(dur[i]) // 2]
         gp = sorted(gap[i])[len(gap[i]) // 2] if gap[i] else 0.0
         tot += d
         tgap += gp
         print(f"{desc:34s} {d:8.1f} {b / d / 1e3:8.0f} {2 * macs / d / 1e6:7.1f} {gp:7.1f}  {kname.get(i, '')}")
+        c = cls[kind]
+        c[0] += 1
+        c[1] += d
+        c[2] += b
+        c[3] += 2 * macs
     print("total us", round(tot, 1), "idle before block launches us", round(tgap, 1))
+    # per layer class: summed algorithmic bytes / summed time, as a fraction of the 8 TB/s HBM peak
+    print(f"{'class':16s} {'layers':>6s} {'us':>9s} {'GB/s':>8s} {'HBM frac':>8s} {'TOPS':>7s}")
+    for kind, (nl, us, b, ops) in sorted(cls.items(), key=lambda kv: -kv[1][1]):
+        print(f"{kind:16s} {nl:6d} {us:9.1f} {b / us / 1e3:8.0f} {b / us / 1e3 / 8000:8.3f} {ops / us / 1e6:7.1f}")
 
 
 if __name__ == "__main__":

@@ -19,6 +19,30 @@ import time
 from collections import defaultdict
 
 KIB = 1024
+SIMDS = 1024   # gfx950 MI355X: 256 CUs x 4 SIMDs (rocprofiler-sdk SIMD_NUM)
+XCDS = 8       # GRBM_GUI_ACTIVE arrives summed over the 8 XCDs: /8 = the busy cycles of one (its max)
+
+
+def mfma_figures(c):
+    """Matrix-core use from pass 6's counters (rocprofiler-sdk counter_defs.yaml, gfx950):
+    MfmaUtil = sum(SQ_VALU_MFMA_BUSY_CYCLES) / (max(GRBM_GUI_ACTIVE) x SIMD_NUM).  rocprofv3 hands
+    GRBM_GUI_ACTIVE over summed across the XCDs, so max ~= sum / 8 (all XCDs run the grid).
+    Also: executed int8 ops (MOPS_I8 x 512) and busy cycles per int8 MFMA instruction (32 for
+    v_mfma_i32_32x32x32_i8: 65,536 ops per 32 cycles per SIMD = the 5.0 POPS dense peak at 2.4 GHz)."""
+    busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
+    gui = c.get("GRBM_GUI_ACTIVE")
+    if busy is None or not gui:
+        return None
+    insts = c.get("SQ_INSTS_VALU_MFMA_I8", 0.0)
+    dur = c.get("_dur_ns")
+    out = {"mfma_busy": round(busy / (gui / XCDS * SIMDS), 4),
+           "SQ_VALU_MFMA_BUSY_CYCLES": busy, "SQ_INSTS_VALU_MFMA_I8": insts,
+           "int8_ops_executed": c.get("SQ_INSTS_VALU_MFMA_MOPS_I8", 0.0) * 512,
+           "busy_cycles_per_i8_mfma": round(busy / insts, 2) if insts else None,
+           "gui_cycles_per_xcd": gui / XCDS}
+    if dur:
+        out["implied_clock_ghz"] = round(gui / XCDS / dur, 3)  # GUI-active cycles per ns of the dispatch
+    return out
 
 
 def load(d):
@@ -29,6 +53,8 @@ def load(d):
         for r in csv.DictReader(open(f)):
             key = (p, int(r["Dispatch_Id"]))
             per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            if r.get("Start_Timestamp") and r.get("End_Timestamp"):  # the dispatch under this pass
+                per[key]["_dur_ns"] = float(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
             meta[key] = {"kernel": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),
                          "agpr": int(r.get("Accum_VGPR_Count", 0) or 0), "lds": int(r["LDS_Block_Size"])}
     return per, meta
@@ -97,6 +123,8 @@ def summarise(d, launches=None, runs=None, model="resnet50", batch=64):
                      "lds_conflict_per_inst": round(steps[i].get("SQ_LDS_BANK_CONFLICT", 0.0) / lds_i, 3) if lds_i else None,
                      "SQ_INSTS_LDS": lds_i, "SQ_LDS_BANK_CONFLICT": steps[i].get("SQ_LDS_BANK_CONFLICT"),
                      "hbm_bytes": steps[i].get("FETCH_SIZE", 0.0) * KIB * 2 + steps[i].get("WRITE_SIZE", 0.0) * KIB,
+                     "dur_ns": steps[i].get("_dur_ns"),
+                     "mfma": mfma_figures(steps[i]),
                      # share of the waves' cycles spent waiting on counters / on issue / issuing
                      **{k: round(steps[i].get(c, 0.0) / steps[i]["SQ_WAVE_CYCLES"], 3)
                         for k, c in (("wait_any_per_wave_cycle", "SQ_WAIT_ANY"),
@@ -111,7 +139,8 @@ def summarise(d, launches=None, runs=None, model="resnet50", batch=64):
                             "conflict_per_lds_inst": round(f.get("SQ_LDS_BANK_CONFLICT", 0.0) / li, 3) if li else None,
                             "share_of_conflicts": round(f.get("SQ_LDS_BANK_CONFLICT", 0.0) /
                                                         max(tot.get("SQ_LDS_BANK_CONFLICT", 0.0), 1.0), 3),
-                            "SQ_INSTS_VALU": f.get("SQ_INSTS_VALU", 0.0)}
+                            "SQ_INSTS_VALU": f.get("SQ_INSTS_VALU", 0.0),
+                            "mfma": mfma_figures(f)}
     fetch = tot.get("FETCH_SIZE", 0.0) * KIB * 2
     write = tot.get("WRITE_SIZE", 0.0) * KIB
     out = {"launches_per_step": n,
@@ -123,6 +152,7 @@ def summarise(d, launches=None, runs=None, model="resnet50", batch=64):
            "example_dispatch": steps[0]["_meta"] if n else None,
            "lds_conflict_per_lds_inst": round(tot.get("SQ_LDS_BANK_CONFLICT", 0.0) / tot["SQ_INSTS_LDS"], 3)
            if tot.get("SQ_INSTS_LDS") else None,
+           "mfma": mfma_figures(tot),
            "per_kernel": per_kernel, "per_dispatch": disp}
     return out
 
@@ -172,6 +202,8 @@ def main():
           f"{s['write_bytes_per_step'] / 1e9:.3f} GB, per launch {s['hbm_bytes_per_launch'] / 1e6:.2f} MB")
     for c, v in s["counters_per_step"].items():
         print(f"  {c:24s} {v:16.0f}")
+    if s.get("mfma"):
+        print(f"MFMA busy (MfmaUtil, counted): {s['mfma']}")
     print(f"LDS bank conflicts per LDS instruction: {s['lds_conflict_per_lds_inst']}; per kernel:")
     for k, v in s["per_kernel"].items():
         print(f"  {v['share_of_conflicts']:6.3f} of conflicts, {v['conflict_per_lds_inst']} per inst, "
