@@ -37,6 +37,8 @@ import numpy as np  # noqa: E402
 
 INT8_MFMA_PEAK_OPS = 5.0e15  # gfx950 dense int8 (2x the 2.5 PF dense bf16 peak), MI355X_MICROARCH.md
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (6.3 TB/s measured streaming copy), MI355X_MICROARCH.md
+MFMA_SIMDS = 1024            # 256 CUs x 4 SIMDs
+PEAK_CLOCK_HZ = 2.4e9        # MI355X peak engine clock (5.0 POPS int8 = 1024 SIMDs x 2048 ops/cycle x 2.4 GHz)
 METRIC = "ResNet-50 int8 op-traces/sec at 1/2/4/8 GPU; bit-exact vs CPU"
 # the BASELINE.json config each --model measures (configs 3 and 5 are single-GPU batch-64 workloads)
 WORKLOADS = {
@@ -860,9 +862,15 @@ def main(argv=None) -> int:
                          "algorithmic_bytes_per_step": int(blk_bytes),
                          "mfma_tops": round(achieved_ops / 1e12, 1),
                          "mfma_frac": round(achieved_ops / INT8_MFMA_PEAK_OPS, 4),
-                         # counted: rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE per XCD x 1024
-                         # SIMDs) over the block kernels, from the same PMC summary as `traffic`
-                         "mfma_busy": None if pmc is None or not pmc.get("mfma") else pmc["mfma"]["mfma_busy"],
+                         # counted (rocprofv3, the same PMC summary as `traffic`): matrix-core busy
+                         # cycles per step (SQ_VALU_MFMA_BUSY_CYCLES, summed over the 1024 SIMDs; 32 per
+                         # v_mfma_i32_32x32x32_i8) over the SIMD-cycles of this run's event-timed block
+                         # kernels at the 2.4 GHz peak clock; mfma_busy_gui divides by the counters' own
+                         # GRBM_GUI_ACTIVE instead (rocprofiler-sdk's MfmaUtil; it also counts each
+                         # dispatch's setup, so it reads lower)
+                         "mfma_busy": None if pmc is None or not pmc.get("mfma") or blk_ms <= 0 else
+                         round(pmc["mfma"]["SQ_VALU_MFMA_BUSY_CYCLES"] / (MFMA_SIMDS * PEAK_CLOCK_HZ * blk_ms * 1e-3), 4),
+                         "mfma_busy_gui": None if pmc is None or not pmc.get("mfma") else pmc["mfma"]["mfma_busy"],
                          "mfma_counters": None if pmc is None else pmc.get("mfma"),
                          "d2h": {"achieved_GBps": round(d2h_achieved, 2), "measured_peak_GBps": round(d2h_peak, 2),
                                  "frac": round(d2h_achieved / d2h_peak, 4) if d2h_peak else None,

@@ -1,0 +1,364 @@
+// Depthwise 3x3 conv blocks: qnn.conv2d (groups == C == O, 3x3, stride 1 or 2, dilation 1) ->
+// bias_add -> requantize [-> clip] in one launch, for every plane size (MobileNetV2's seventeen
+// depthwise layers: 112x112 down to 7x7, stride 1 and 2) -- the non-MFMA path of BASELINE config 5.
+//
+// The layer writes ~10-11 bytes of records per output element (int32 conv + int32 bias_add +
+// int8 requantize + int8 clip + the next conv's int8 shadow) from 1 input byte and 9 weights per
+// channel, so it is HBM-write-bound: the kernel is built around the store pattern.
+//   * A workgroup owns a tile = one image x CT = 16 * cbg channels x a band of BH output rows (the
+//     whole plane when it is small).  Its records are one contiguous NCHW run per channel -- or, for
+//     whole planes, one run for all CT channels -- so the tile is walked as a flat array of 4-element
+//     groups, each lane storing 16 bytes (int32 records) / 4 bytes (int8 records) with buffer stores:
+//     the whole-line pattern that writes at ~5.3 TB/s in the store probes.
+//   * The input rows of the tile's channels (+ the one-row halo, out-of-image rows and columns
+//     holding the input zero point) are staged in LDS with dword loads; a tap row of an output is
+//     three bytes there: two ds_read_b32 + one v_alignbyte_b32 give them as one dword, and one
+//     v_dot4_i32_i8 against the channel's packed weight row (w0, w1, w2, 0) accumulates the three
+//     products -- 3 dot instructions per output instead of 9 multiply-adds on single bytes.
+//   * Zero points are folded, not subtracted per tap: with out-of-image taps holding za,
+//       sum (x - za)(w - zw) = sum x w - zw sum x - za sum w + 9 za zw   (exactly, in int32),
+//     the last two terms a per-channel constant, sum x another dot against 0x00010101 (only when a
+//     kernel zero point is nonzero).  uint8 operands are staged xor 0x80 (x - 128) with the zero
+//     point moved by 128, so every dot is signed x signed (python/tvm/relay/qnn/op/
+//     legalizations.py:195-226 defines the arithmetic: int16 operand shifts, int32 accumulation).
+//   * Epilogue per element as the other conv-block kernels: bias_add (int32 wrap), RequantizeLowerInt
+//     (src/relay/qnn/op/requantize.cc:195-273; the mul_hi form when every right shift is >= 2),
+//     clip (python/tvm/topi/math.py:615-640), and the last output's shadow byte into LDS, written
+//     after the tile as 16-byte chunks (16 channels of one pixel) contiguous across lanes.
+// Parity: tests/test_gpu_ops.py (depthwise blocks vs the oracle) and the MobileNetV2 traces.
+#include <algorithm>
+#include <cstdint>
+
+#include "tk_conv.h"
+
+namespace tk {
+
+namespace {
+
+constexpr int kDwThreads = 256;
+constexpr int kDwPL = 4;  // LDS bytes left of each staged input row (>= the conv's left padding)
+
+struct DwArgs {
+  const uint8_t* x;        // NCHW data (int8, or uint8 staged xor 0x80)
+  const uint8_t* w;        // (C, 1, 3, 3) weights (int8 / uint8)
+  const int32_t* zw_vec;   // per-channel kernel zero points (NULL: zw)
+  int32_t zw;
+  int32_t za_s;            // staged input zero point: za, or za - 128 for uint8 data
+  uint32_t xor_x, xor_w;   // 0x80 for uint8 data / weights
+  int32_t w_u8;            // weights are uint8 (their zero point moves by 128 too)
+  int32_t C, H, W, OH, OW, sh, pt, pl;
+  int32_t BH, bands, cbg;  // output rows per tile, tiles per plane, 16-channel groups per tile
+  int32_t rows_in, Wp;     // staged rows per channel (of Wp bytes)
+  int32_t wdw;             // W % 4 == 0: the data region of a staged row is whole dwords
+  int32_t npix;            // N * OH * OW: pixels per channel group of the shadow
+  uint32_t m_ow, m_plane, m_plane_last;  // fdiv_u magics of OW and of a tile's pixels (BH / last band)
+  int32_t lds_const, lds_tout;  // LDS byte offsets of the channel constants / shadow staging
+};
+
+struct DwConst {            // one channel's epilogue constants (32 bytes in LDS)
+  uint32_t fold;            // -za' sum w' + 9 za' zw'
+  int32_t zwc;              // zw' (the sum-x term's factor)
+  int32_t bias, m, s, zp;   // bias_add, requantize multiplier / shift / input zero point
+  uint32_t wrow0, pad;
+};
+
+__device__ __forceinline__ uint32_t fdiv_u(uint32_t x, uint32_t m) { return __umulhi(x, m); }
+
+template <bool ZW, bool FAST, bool CLIP, bool SHADOW>
+__device__ __forceinline__ void dw_walk(const DwArgs& d, const GemmArgs& g, const uint8_t* tin, const uint32_t* wts,
+                                        const DwConst* cst, uint8_t* tout, int n, int c0, int oh0, int bh) {
+  const int tid = threadIdx.x;
+  const int CT = 16 * d.cbg;
+  const uint32_t plane = (uint32_t)(bh * d.OW);                    // tile elements per channel
+  const uint32_t m_plane = bh == d.BH ? d.m_plane : d.m_plane_last;
+  const uint32_t m_ow = d.m_ow;
+  const uint32_t total = plane * (uint32_t)CT;
+  const int sh = d.sh;
+  const int Wp = d.Wp, rin = d.rows_in;
+  const int colofs = kDwPL - d.pl;
+  const uint32_t n4 = g.out_elems * 4u;
+  const auto r_conv = rec_rsrc(g.C, n4), r_bias = rec_rsrc(g.bias_out, n4);
+  const auto r_rq = rec_rsrc(g.rq_out, g.out_elems);
+  const auto r_clip = rec_rsrc(g.clip_out, CLIP ? g.out_elems : 0u);
+  const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
+  const int32_t clip_lo = g.clip_lo, clip_hi = g.clip_hi;
+  const int mode = g.rq.mode;
+  const uint32_t sxor = g.shadow_xor;
+  // (whole-plane tiles: the CT channel runs are adjacent in memory, so the tile is one run)
+  const uint32_t base0 = (uint32_t)(((n * d.C + c0) * d.OH + oh0) * d.OW);
+  const uint32_t cstride = (uint32_t)(d.OH * d.OW);
+  for (uint32_t f0 = 4u * tid; f0 < total; f0 += 4u * kDwThreads) {
+    int32_t v[4];
+    int cc[4], pp[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t f = f0 + e;
+      const uint32_t c = fdiv_u(f, m_plane);
+      const uint32_t rem = f - c * plane;
+      const uint32_t r = fdiv_u(rem, m_ow);
+      const uint32_t ow = rem - r * (uint32_t)d.OW;
+      cc[e] = (int)c;
+      pp[e] = (int)rem;
+      // tap row t of output (r, ow): bytes [a, a + 3) of the staged row r * sh + t
+      const int a0 = ((int)c * rin + (int)r * sh) * Wp + colofs + (int)ow * sh;
+      int32_t acc = 0, sx = 0;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int a = a0 + t * Wp;
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(tin + (a & ~3));
+        const uint32_t win = __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+        acc = __builtin_amdgcn_sdot4((int)win, (int)wts[c * 4 + t], acc, false);
+        if constexpr (ZW) sx = __builtin_amdgcn_sdot4((int)win, 0x00010101, sx, false);
+      }
+      const DwConst& k = cst[c];
+      uint32_t val = (uint32_t)acc + k.fold;
+      if constexpr (ZW) val -= (uint32_t)k.zwc * (uint32_t)sx;
+      v[e] = (int32_t)val;
+    }
+    // the group's 4 elements are contiguous in every record (tile runs are multiples of 4)
+    const uint32_t c_first = (uint32_t)cc[0];
+    const uint32_t o = base0 + c_first * cstride + (uint32_t)pp[0];
+    __builtin_amdgcn_raw_buffer_store_b128(v4i{v[0], v[1], v[2], v[3]}, r_conv, o * 4u, 0, 0);
+    int32_t q[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const DwConst& k = cst[cc[e]];
+      v[e] = (int32_t)((uint32_t)v[e] + (uint32_t)k.bias);
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(v4i{v[0], v[1], v[2], v[3]}, r_bias, o * 4u, 0, 0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const DwConst& k = cst[cc[e]];
+      const int32_t t = (int32_t)((uint32_t)v[e] - (uint32_t)k.zp);
+      int32_t y;
+      if constexpr (FAST) {
+        const int sh2 = -k.s - 1;
+        y = (int32_t)((uint32_t)__mulhi(t, k.m) + (1u << (sh2 - 1))) >> sh2;
+      } else {
+        y = rq_core(t, mode, k.m, k.s);
+      }
+      q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, 0);
+    if constexpr (CLIP) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
+      __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, 0);
+    }
+    if constexpr (SHADOW) {
+      // [group][pixel][16]: channel c of tile pixel p at ((c >> 4) * plane + p) * 16 + (c & 15)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        tout[(((uint32_t)cc[e] >> 4) * plane + (uint32_t)pp[e]) * 16u + (cc[e] & 15)] = (uint8_t)((uint32_t)q[e] ^ sxor);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kDwThreads) void dw_tile_kernel(DwArgs d, GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  const int tid = threadIdx.x;
+  const int CT = 16 * d.cbg;
+  int bid = blockIdx.x;
+  const int band = bid % d.bands;
+  bid /= d.bands;
+  const int cgroups = d.C / CT;
+  const int cg = bid % cgroups, n = bid / cgroups;
+  const int c0 = cg * CT;
+  const int oh0 = band * d.BH;
+  const int bh = min(d.BH, d.OH - oh0);
+  const int ih0 = oh0 * d.sh - d.pt;
+  uint8_t* tin = dsm;
+  uint32_t* wts = reinterpret_cast<uint32_t*>(dsm + d.lds_const);      // [CT][4] packed rows
+  DwConst* cst = reinterpret_cast<DwConst*>(dsm + d.lds_const + CT * 16);
+  uint8_t* tout = dsm + d.lds_tout;
+  // ---- stage the input rows: dword k of staged row (c, rr) holds bytes [4k, 4k + 4) of
+  // [kDwPL pad][W data][pad], pads and out-of-image rows holding the staged zero point
+  const uint32_t za4 = 0x01010101u * (uint8_t)d.za_s;
+  const int wpd = d.Wp / 4;
+  const int nrow = CT * d.rows_in;
+  const int ndw = nrow * wpd;
+  const uint32_t xx4 = 0x01010101u * d.xor_x;
+  for (int k0 = tid; k0 < ndw; k0 += 4 * kDwThreads) {
+    uint32_t val[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * kDwThreads;
+      val[u] = za4;
+      if (k < ndw) {
+        const int row = k / wpd, kd = k - row * wpd;
+        const int c = row / d.rows_in, rr = row - c * d.rows_in;
+        const int ih = ih0 + rr;
+        const int b0 = kd * 4 - kDwPL;  // input column of the dword's first byte
+        if (ih >= 0 && ih < d.H && b0 + 3 >= 0 && b0 < d.W) {
+          const uint8_t* src = d.x + ((int64_t)(n * d.C + c0 + c) * d.H + ih) * d.W;
+          if (d.wdw && b0 >= 0 && b0 + 3 < d.W) {
+            val[u] = ldg(reinterpret_cast<const uint32_t*>(src + b0)) ^ xx4;
+          } else {
+            uint32_t wv = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int col = b0 + j;
+              const uint32_t byte = (col >= 0 && col < d.W) ? ((uint32_t)ldg(src + col) ^ d.xor_x) : (uint32_t)(uint8_t)d.za_s;
+              wv |= (byte & 0xFFu) << (8 * j);
+            }
+            val[u] = wv;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * kDwThreads;
+      if (k < ndw) reinterpret_cast<uint32_t*>(tin)[k] = val[u];
+    }
+  }
+  // ---- per channel: packed weight rows (w0, w1, w2, 0) and the epilogue constants
+  int shift_ok = 1;  // this channel's right shift is >= 2 (the mul_hi requantize form applies)
+  if (tid < CT) {
+    const int ch = c0 + tid;
+    const int32_t zw = d.zw_vec ? ldg(d.zw_vec + ch) : d.zw;
+    const int32_t zws = d.w_u8 ? zw - 128 : zw;
+    int32_t sw = 0;
+    uint32_t rows[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      uint32_t pk = 0;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const uint32_t b = ((uint32_t)ldg(d.w + (int64_t)ch * 9 + r * 3 + s) ^ d.xor_w) & 0xFFu;
+        sw += (int32_t)(int8_t)b;
+        pk |= b << (8 * s);
+      }
+      rows[r] = pk;
+      wts[tid * 4 + r] = pk;
+    }
+    wts[tid * 4 + 3] = 0;
+    DwConst k{};
+    k.fold = (uint32_t)0 - (uint32_t)d.za_s * (uint32_t)sw + 9u * (uint32_t)d.za_s * (uint32_t)zws;
+    k.zwc = zws;
+    k.bias = ldg(g.bias + ch);
+    const bool axis = g.rq.mode == TK_RQ_AXIS_UPWARD || g.rq.mode == TK_RQ_AXIS_TONEAREST;
+    k.m = axis ? ldg(g.rq.ms + ch) : g.rq.multiplier;
+    k.s = axis ? ldg(g.rq.ss + ch) : g.rq.shift;
+    k.zp = g.rq.zps ? ldg(g.rq.zps + ch) : g.rq.zp_in;
+    k.wrow0 = rows[0];
+    cst[tid] = k;
+    shift_ok = k.s <= -2;
+  }
+  const bool fast = __syncthreads_and(shift_ok) && (g.rq.mode == TK_RQ_AXIS_UPWARD || g.rq.mode == TK_RQ_TENSOR_UPWARD);
+  const bool zw_any = d.zw_vec || d.w_u8 || d.zw != 0;
+  const bool shadow = g.shadow_out != nullptr;
+  using T = std::true_type;
+  using F = std::false_type;
+  auto go = [&](auto zw_c, auto fast_c, auto clip_c, auto sh_c) __attribute__((always_inline)) {
+    dw_walk<decltype(zw_c)::value, decltype(fast_c)::value, decltype(clip_c)::value, decltype(sh_c)::value>(
+        d, g, tin, wts, cst, tout, n, c0, oh0, bh);
+  };
+  auto by_shadow = [&](auto zw_c, auto fast_c, auto clip_c) __attribute__((always_inline)) {
+    if (shadow) go(zw_c, fast_c, clip_c, T{});
+    else go(zw_c, fast_c, clip_c, F{});
+  };
+  auto by_clip = [&](auto zw_c, auto fast_c) __attribute__((always_inline)) {
+    if (g.has_clip) by_shadow(zw_c, fast_c, T{});
+    else by_shadow(zw_c, fast_c, F{});
+  };
+  if (zw_any) {
+    if (fast) by_clip(T{}, T{});
+    else by_clip(T{}, F{});
+  } else {
+    if (fast) by_clip(F{}, T{});
+    else by_clip(F{}, F{});
+  }
+  if (!shadow) return;
+  __syncthreads();
+  // ---- the next conv's shadow: 16 channels of one pixel per 16-byte store, the tile's pixels of
+  // each channel group contiguous in [C / 16][N * OH * OW][16]
+  const int plane = bh * d.OW;
+  const int pix0 = (n * d.OH + oh0) * d.OW;
+  const int nchunk = d.cbg * plane;
+  for (int k = tid; k < nchunk; k += kDwThreads) {
+    const int grp = k / plane, p = k - grp * plane;
+    *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)(c0 / 16 + grp) * d.npix + pix0 + p) * 16) =
+        *reinterpret_cast<const v4i*>(tout + (size_t)k * 16);
+  }
+}
+
+}  // namespace
+
+// The depthwise tile plan of a conv block, when one applies: every output channel reads only its
+// own input channel (groups == C == O), 3x3 taps, stride 1 or 2 on both axes, dilation 1, channel
+// counts in whole 16-channel shadow groups, and records that fit 32-bit byte offsets.
+int dw_block_try(const tk_tensor* data, const tk_tensor* weight, const ConvGeom& g, const tk_conv2d_attrs* a,
+                 const GemmArgs& ga_in, hipStream_t s, int* rc) {
+  GemmArgs ga = ga_in;
+  const int sh = a->strides[0];
+  if (!(a->groups == g.C && g.C == g.O && g.C % 16 == 0 && g.KH == 3 && g.KW == 3 && a->dilation[0] == 1 &&
+        a->dilation[1] == 1 && a->strides[1] == sh && (sh == 1 || sh == 2) && a->padding[0] <= 2 &&
+        a->padding[1] <= kDwPL && ga.bias_out && ga.rq_out))
+    return 0;
+  if ((int64_t)g.N * g.O * g.OH * g.OW * 4 >= (int64_t)UINT32_MAX || !is_int8ish(data) || !is_int8ish(weight))
+    return 0;
+  const int OHW = g.OH * g.OW;
+  ga.out_elems = (uint32_t)((int64_t)g.N * g.O * OHW);  // every record's elements (buffer-store range)
+  DwArgs d{};
+  d.x = (const uint8_t*)ptr(data);
+  d.w = (const uint8_t*)ptr(weight);
+  d.zw_vec = a->kernel_zero_points;
+  d.zw = a->kernel_zero_point;
+  const bool xu = is_uint(data, 8), wu = is_uint(weight, 8);
+  d.xor_x = xu ? 0x80u : 0u;
+  d.xor_w = wu ? 0x80u : 0u;
+  d.w_u8 = wu;
+  d.za_s = xu ? a->input_zero_point - 128 : a->input_zero_point;
+  if (d.za_s < -128 || d.za_s > 127) return 0;  // the staged zero point must be a byte value
+  d.C = g.C;
+  d.H = g.H;
+  d.W = g.W;
+  d.OH = g.OH;
+  d.OW = g.OW;
+  d.sh = sh;
+  d.pt = a->padding[0];
+  d.pl = a->padding[1];
+  d.npix = g.N * OHW;
+  d.wdw = g.W % 4 == 0;
+  // tiles: whole planes of up to 1024 pixels (cbg 16-channel groups so that a tile has >= ~3k
+  // outputs), else bands of rows of whole 4-element groups
+  int cbg = 1, BH = g.OH;
+  if (OHW <= 1024) {
+    while (cbg < 4 && 16 * cbg * 2 * OHW <= 4096 && g.C % (32 * cbg) == 0) cbg *= 2;
+  } else {
+    if (g.OW % 4) return 0;
+    BH = std::max(1, (sh == 1 ? 1024 : 512) / g.OW);
+  }
+  d.cbg = cbg;
+  d.BH = BH;
+  d.bands = (g.OH + BH - 1) / BH;
+  if ((BH * g.OW) % 4 || (g.OH % BH && ((g.OH % BH) * g.OW) % 4)) return 0;
+  if (cbg > 1 && BH != g.OH) return 0;
+  d.rows_in = (BH - 1) * sh + 3;
+  // x / d as __umulhi(x, ceil(2^32 / d)): exact for x * d < 2^32 (tile indices < 2^16, d <= 2^16)
+  auto magic = [](uint32_t v) { return (uint32_t)((0x100000000ull + v - 1) / v); };
+  const int last = g.OH - (d.bands - 1) * BH;
+  if (g.OW < 2 || (int64_t)16 * cbg * BH * g.OW >= 65536) return 0;
+  d.m_ow = magic((uint32_t)g.OW);
+  d.m_plane = magic((uint32_t)(BH * g.OW));
+  d.m_plane_last = magic((uint32_t)(last * g.OW));
+  // staged row: [kDwPL][W][pads], long enough for the last output's taps plus the second dword
+  // a tap row reads
+  const int need = std::max(kDwPL + g.W + 4, kDwPL - d.pl + (g.OW - 1) * sh + 8);
+  d.Wp = (need + 3) & ~3;
+  const int CT = 16 * cbg;
+  const size_t tin = ((size_t)CT * d.rows_in * d.Wp + 8 + 15) & ~(size_t)15;
+  d.lds_const = (int32_t)tin;
+  const size_t cst = (size_t)CT * 16 + (size_t)CT * sizeof(DwConst);
+  d.lds_tout = (int32_t)(tin + cst);
+  const size_t lds = tin + cst + (size_t)CT * BH * g.OW;
+  if (lds > 64 * 1024) return 0;
+  const unsigned grid = (unsigned)((int64_t)g.N * (g.C / CT) * d.bands);
+  hipLaunchKernelGGL(dw_tile_kernel, dim3(grid), dim3(kDwThreads), lds, s, d, ga);
+  *rc = hipGetLastError() == hipSuccess ? TK_OK : TK_ERR_HIP;
+  if (*rc) set_error("dw_tile_kernel launch failed");
+  return 1;
+}
+
+}  // namespace tk

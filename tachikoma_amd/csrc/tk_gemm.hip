@@ -477,7 +477,15 @@ gemm_i8_kernel(GemmArgs g) {
 #pragma unroll
       for (int st = 0; st < kRing - 1; ++st)
         if (st < nst) issue(st);
-      if constexpr (kLateResid) issue_resid();  // younger than the prologue's stages (see there)
+      if constexpr (kLateResid) {
+        // younger than the prologue's stages (see there): the counted stage waits below let the
+        // kNR residual loads stay in flight only if they are issued after every prologue DMA, so
+        // the scheduler may not move them across (the plain loads and the LDS-DMAs are otherwise
+        // independent to it)
+        __builtin_amdgcn_sched_barrier(0);
+        issue_resid();
+        __builtin_amdgcn_sched_barrier(0);
+      }
       int cur = 0, nxt = kRing - 1;  // ring slots of stage it and of stage it + kRing - 1
       // one step: retire stage it (A_DMA + B_DMA LDS-DMAs per thread and stage) with `pending`
       // later stages still in flight, barrier (stage it visible to all waves; the slot read in
@@ -1458,6 +1466,10 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(const Tx* __restrict__ x, co
 // ---------------------------------------------------------------- host wrappers
 
 
+// tk_dw.hip: the depthwise 3x3 tile kernel (returns 1 and sets *rc when its plan applies)
+int dw_block_try(const tk_tensor* data, const tk_tensor* weight, const ConvGeom& g, const tk_conv2d_attrs* a,
+                 const GemmArgs& ga, hipStream_t s, int* rc);
+
 static int conv_geom(const tk_tensor* data, const tk_tensor* weight, const tk_conv2d_attrs* a, ConvGeom* g) {
   if (data->ndim != 4 || weight->ndim != 4) return TK_ERR_SHAPE;
   g->N = (int)data->shape[0];
@@ -1805,6 +1817,12 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
   if (rc) return rc;
   if (!use_mfma_conv(g, a->groups)) {
     TK_CHECK_ARG(!(blk && blk->attrs->has_add), "residual join needs an MFMA conv block");
+    // depthwise 3x3 blocks, every plane size: the tile kernel of tk_dw.hip (TK_DW2=0 in the
+    // ablation build keeps the older band / direct kernels below for A/B)
+    if (blk && env_int("TK_DW2", 1)) {
+      int rc_dw = TK_OK;
+      if (dw_block_try(data, weight, g, a, ga, s, &rc_dw)) return rc_dw;
+    }
     // depthwise 3x3 blocks: the LDS-staged band kernel (see dw3x3_kernel)
     // (large planes only: on 7x7 / 14x14 planes and strided 28x28 ones the generic kernel measured
     // faster, the band staging does not amortise; MobileNetV2 dw layers 1.2-2x faster otherwise)

@@ -1116,14 +1116,42 @@ int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, i
   // kernels that expose its load latency look faster than they run (the 56x56 expand: 115 us
   // cached, 136-153 cold, profiles/r05x_residual_cold_vs_cached.txt).  So each of its timed
   // launches follows a 512 MiB fill of a scratch buffer that evicts the caches, and is timed alone.
+  // If the device cannot spare the flush buffer (a module near the memory limit: packed mirrors
+  // are up to 4 x 7.45 GB at batch 64), the buffer shrinks to a quarter of the free memory, and
+  // below 64 MiB the node is timed warm, back to back like the others, instead of failing the tune.
   void* flush = nullptr;
-  const size_t flush_bytes = (size_t)512 << 20;
+  size_t flush_bytes = (size_t)512 << 20;
+  bool flush_unavailable = false;
+  auto timed_warm = [&](tk::Node& node, float* us) -> int {
+    if (hipEventRecord(e0, s) != hipSuccess) return TK_ERR_HIP;
+    for (int k = 0; k < reps; ++k) {
+      const int r = tk::run_node(node, s);
+      if (r) return r;
+    }
+    float ms = 0.0f;
+    if (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+        hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+      return TK_ERR_HIP;
+    *us = ms * 1e3f / (float)reps;
+    return TK_OK;
+  };
   auto timed_cold = [&](tk::Node& node, float* us) -> int {
-    if (!flush && hipMalloc(&flush, flush_bytes) != hipSuccess) {
+    if (!flush && !flush_unavailable && hipMalloc(&flush, flush_bytes) != hipSuccess) {
       flush = nullptr;
       (void)hipGetLastError();
-      return TK_ERR_HIP;
+      size_t free_b = 0, total_b = 0;
+      if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 4 >= ((size_t)64 << 20)) {
+        flush_bytes = (free_b / 4) & ~(((size_t)1 << 20) - 1);
+        if (hipMalloc(&flush, flush_bytes) != hipSuccess) {
+          flush = nullptr;
+          (void)hipGetLastError();
+        }
+      } else {
+        (void)hipGetLastError();
+      }
+      flush_unavailable = flush == nullptr;
     }
+    if (flush_unavailable) return timed_warm(node, us);
     float total = 0.0f;
     for (int k = 0; k < reps; ++k) {
       if (hipMemsetAsync(flush, k & 0xFF, flush_bytes, s) != hipSuccess || hipEventRecord(e0, s) != hipSuccess)
@@ -1162,16 +1190,7 @@ int tk_module_tune(tk_module* mod, void* stream, int max_candidates, int reps, i
           continue;
         }
         if (rc) break;
-        if (node.desc.attrs.block.has_add) {
-          rc = timed_cold(node, &r.us[c]);
-        } else {
-          if (hipEventRecord(e0, s) != hipSuccess) rc = TK_ERR_HIP;
-          for (int k = 0; k < reps && rc == TK_OK; ++k) rc = tk::run_node(node, s);
-          if (rc == TK_OK && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess)) rc = TK_ERR_HIP;
-          float ms = 0.0f;
-          if (rc == TK_OK && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = TK_ERR_HIP;
-          if (rc == TK_OK) r.us[c] = ms * 1e3f / (float)reps;
-        }
+        rc = node.desc.attrs.block.has_add ? timed_cold(node, &r.us[c]) : timed_warm(node, &r.us[c]);
         if (rc) break;
         if (best_us <= 0.0f || r.us[c] < best_us) best_us = r.us[c], r.best = r.algos[c];
       }

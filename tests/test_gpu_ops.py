@@ -695,6 +695,57 @@ def test_conv_block_matches_unfused_ops(tk, case):
     np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
 
 
+# depthwise 3x3 blocks on the tile kernel (tk_dw.hip): every MobileNetV2 depthwise shape class --
+# 112 / 56 planes in row bands (last band partial), whole 28 / 14 planes, 7x7 planes four channel
+# groups per tile (flat 4-element groups crossing rows and channels), stride 1 and 2, valid padding,
+# odd planes -- with uint8 data / weights, scalar and per-channel kernel zero points, per-tensor
+# and per-axis requantize, both roundings and the general (right shift < 2) requantize form
+DW_CASES = [
+    # N, C, H, W, stride, pad, dx, dw, za, zw ("vec": per channel), s_in ("axis" | scalar), rounding, out, clip
+    (2, 32, 112, 112, 1, 1, "int8", "int8", 3, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (1, 96, 112, 112, 2, 1, "int8", "int8", -5, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (2, 144, 56, 56, 1, 1, "int8", "int8", 0, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (2, 144, 56, 56, 2, 1, "int8", "int8", 7, 0, "axis", "TONEAREST", "int8", (0, 127)),
+    (2, 192, 28, 28, 1, 1, "int8", "int8", -1, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (3, 192, 28, 28, 2, 1, "int8", "int8", 2, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (2, 384, 14, 14, 1, 1, "int8", "int8", -8, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (2, 576, 14, 14, 2, 1, "int8", "int8", 4, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (2, 960, 7, 7, 1, 1, "int8", "int8", 1, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (1, 48, 7, 7, 1, 1, "int8", "int8", 1, 0, "axis", "UPWARD", "int8", None),
+    (2, 32, 28, 28, 1, 1, "uint8", "uint8", 130, 3, "axis", "UPWARD", "uint8", (128, 255)),
+    (2, 64, 14, 14, 2, 1, "int8", "int8", -2, "vec", "axis", "UPWARD", "int8", (0, 127)),
+    (2, 32, 30, 30, 1, 0, "int8", "uint8", 5, 120, "axis", "UPWARD", "int8", (-3, 90)),
+    (2, 16, 20, 20, 1, 1, "int8", "int8", 0, 0, 0.5, "TONEAREST", "int8", None),
+    (2, 16, 9, 9, 2, 1, "uint8", "int8", 125, 0, 0.0007, "UPWARD", "uint8", (130, 250)),
+]
+
+
+@pytest.mark.parametrize("case", DW_CASES, ids=[f"dw{i}" for i in range(len(DW_CASES))])
+def test_depthwise_block(tk, case):
+    n, c, h, w, st, p, dx, dw_, za, zw, sk, rounding, odt, clip = case
+    rng = np.random.default_rng(zlib.crc32(repr(case).encode()))
+    x = _rand(rng, (n, c, h, w), dx)
+    wt = _rand(rng, (c, 1, 3, 3), dw_)
+    bias = rng.integers(-2**14, 2**14, size=c).astype(np.int32)
+    s_in = rng.uniform(1e-4, 3e-3, size=c).astype(np.float32) if sk == "axis" else np.float32(sk)
+    s_out = np.float32(0.01)
+    zv = rng.integers(-6, 7, size=c).astype(np.int32) if zw == "vec" else None
+    zs = 0 if zw == "vec" else zw
+    pad = (p, p, p, p)
+    outs = tk.conv2d_block(x, wt, bias, za, zs, s_in, s_out, 3, clip=clip, strides=(st, st), padding=pad, groups=c,
+                           out_dtype=odt, want_shadow=True, rounding=rounding, zw_vec=zv)
+    conv = ref.qnn_conv2d(x, wt, za, zv if zv is not None else zs, strides=(st, st), padding=pad, groups=c)
+    badd = ref.bias_add(conv, bias, 1)
+    rq = ref.requantize(badd, s_in, np.int32(0), s_out, np.int32(3), axis=1, rounding=rounding, out_dtype=odt)
+    exp = [conv, badd, rq] + ([ref.clip(rq, *clip)] if clip is not None else [])
+    for i, (got, e) in enumerate(zip(outs, exp)):
+        if not np.array_equal(got, e):
+            bad = np.argwhere(got != e)[0]
+            raise AssertionError(f"record {i}: {int((got != e).sum())} mismatches, first at {tuple(bad)}: "
+                                 f"{got[tuple(bad)]} vs {e[tuple(bad)]}")
+    np.testing.assert_array_equal(outs[-1], blocked_shadow(exp[-1]))
+
+
 @pytest.mark.parametrize("dt,value", [("int8", -5), ("uint8", 200), ("int32", -70000), ("float32", 1.5)])
 def test_pad(tk, dt, value):
     """tk_pad (nn.pad, constant mode) against the oracle's np.pad restatement."""

@@ -251,7 +251,7 @@ def _rq_attrs(r, keep, input_scale, output_scale, output_zero_point, rounding="U
 
 def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1, 1), padding=(0, 0, 0, 0),
                  dilation=(1, 1), groups=1, out_dtype="int8", want_shadow=False, residual=None, add_params=None,
-                 block_is_rhs=False, rounding="UPWARD", algo=0, algos_only=False):
+                 block_is_rhs=False, rounding="UPWARD", algo=0, algos_only=False, zw_vec=None):
     """Fused conv -> bias_add -> requantize(axis 1) [-> qnn.add(., residual)] [-> clip] through
     tk_qnn_conv2d_block.  add_params = (ls, lz, rs, rz, os, oz) of the qnn.add (lhs = the block's
     requantize output unless block_is_rhs).  algo: tk_block_attrs.algo; algos_only: return the
@@ -277,6 +277,9 @@ def conv2d_block(x, w, bias, za, zw, s_in, s_out, zp_out, clip=None, strides=(1,
     a.conv.input_zero_point = int(za)
     a.conv.kernel_zero_point = int(zw)
     keep = []
+    if zw_vec is not None:  # per-output-channel kernel zero points
+        keep.append(dev(np.asarray(zw_vec, np.int32)))
+        a.conv.kernel_zero_points = keep[-1].data_ptr()
     _rq_attrs(a.requantize, keep, s_in, s_out, zp_out, rounding=rounding)
     if clip is not None:
         a.has_clip = 1
