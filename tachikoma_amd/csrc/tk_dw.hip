@@ -36,7 +36,13 @@ namespace tk {
 namespace {
 
 constexpr int kDwThreads = 256;
-constexpr int kDwPL = 4;  // LDS bytes left of each staged input row (>= the conv's left padding)
+constexpr int kDwPL = 16;  // LDS bytes left of each staged input row (>= the conv's left padding; 16-byte
+                           // aligned so that the vector loads of a row land on aligned LDS slots)
+
+// how the 4-element groups of a tile are formed
+enum { kDwGen = 0,    // any plane: elements decoded one by one (groups may cross rows and channels)
+       kDwRow1 = 1,   // OW % 4 == 0, stride 1, left padding 1: a group is 4 outputs of one row
+       kDwRow2 = 2 }; // the same at stride 2
 
 struct DwArgs {
   const uint8_t* x;        // NCHW data (int8, or uint8 staged xor 0x80)
@@ -48,10 +54,11 @@ struct DwArgs {
   int32_t w_u8;            // weights are uint8 (their zero point moves by 128 too)
   int32_t C, H, W, OH, OW, sh, pt, pl;
   int32_t BH, bands, cbg;  // output rows per tile, tiles per plane, 16-channel groups per tile
-  int32_t rows_in, Wp;     // staged rows per channel (of Wp bytes)
-  int32_t wdw;             // W % 4 == 0: the data region of a staged row is whole dwords
+  int32_t rows_in, Wp;     // staged rows per channel (of Wp bytes, a multiple of 16)
+  int32_t vw;              // bytes per staging load: 16, 8, 4, 2 or 1 (divides W)
   int32_t npix;            // N * OH * OW: pixels per channel group of the shadow
   uint32_t m_ow, m_plane, m_plane_last;  // fdiv_u magics of OW and of a tile's pixels (BH / last band)
+  uint32_t m_cpr, m_rin;   // fdiv_u magics of the loads per staged row (W / vw) and of rows_in
   int32_t lds_const, lds_tout;  // LDS byte offsets of the channel constants / shadow staging
 };
 
@@ -59,102 +66,207 @@ struct DwConst {            // one channel's epilogue constants (32 bytes in LDS
   uint32_t fold;            // -za' sum w' + 9 za' zw'
   int32_t zwc;              // zw' (the sum-x term's factor)
   int32_t bias, m, s, zp;   // bias_add, requantize multiplier / shift / input zero point
-  uint32_t wrow0, pad;
+  uint32_t pad0, pad1;
 };
 
 __device__ __forceinline__ uint32_t fdiv_u(uint32_t x, uint32_t m) { return __umulhi(x, m); }
 
-template <bool ZW, bool FAST, bool CLIP, bool SHADOW>
+// The block epilogue of one 4-element group (values v: the convolution sums), elements in channel
+// cc[e] at tile pixel pp[e]; o = the group's first element offset in every record (the 4 are
+// contiguous there).  Writes conv, bias_add, requantize [, clip] and the shadow bytes (LDS).
+template <bool FAST>
+__device__ __forceinline__ void dw_epilogue(const GemmArgs& g, const DwConst* cst, uint8_t* tout, uint32_t plane,
+                                            int32_t v[4], const int cc[4], const int pp[4], uint32_t o,
+                                            __amdgpu_buffer_rsrc_t r_conv, __amdgpu_buffer_rsrc_t r_bias,
+                                            __amdgpu_buffer_rsrc_t r_rq, __amdgpu_buffer_rsrc_t r_clip,
+                                            bool clip, bool shadow, bool same_c) {
+  const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
+  const int mode = g.rq.mode;
+  DwConst k[4];
+  k[0] = cst[cc[0]];
+#pragma unroll
+  for (int e = 1; e < 4; ++e) k[e] = same_c ? k[0] : cst[cc[e]];
+  __builtin_amdgcn_raw_buffer_store_b128(v4i{v[0], v[1], v[2], v[3]}, r_conv, o * 4u, 0, 0);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = (int32_t)((uint32_t)v[e] + (uint32_t)k[e].bias);
+  __builtin_amdgcn_raw_buffer_store_b128(v4i{v[0], v[1], v[2], v[3]}, r_bias, o * 4u, 0, 0);
+  int32_t q[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int32_t t = (int32_t)((uint32_t)v[e] - (uint32_t)k[e].zp);
+    int32_t y;
+    if constexpr (FAST) {
+      // right shift >= 2: (x·m + 2^(30+rs)) >> (31+rs) only needs the high word of x·m
+      const int sh2 = -k[e].s - 1;
+      y = (int32_t)((uint32_t)__mulhi(t, k[e].m) + (1u << (sh2 - 1))) >> sh2;
+    } else {
+      y = rq_core(t, mode, k[e].m, k[e].s);
+    }
+    q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
+  }
+  __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, 0);
+  if (clip) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], g.clip_lo, g.clip_hi);
+    __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, 0);
+  }
+  if (shadow) {
+    // [group][pixel][16]: channel c of tile pixel p at ((c >> 4) * plane + p) * 16 + (c & 15)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      tout[(((uint32_t)cc[e] >> 4) * plane + (uint32_t)pp[e]) * 16u + (cc[e] & 15)] =
+          (uint8_t)((uint32_t)q[e] ^ g.shadow_xor);
+  }
+}
+
+template <int MODE, bool FAST>
 __device__ __forceinline__ void dw_walk(const DwArgs& d, const GemmArgs& g, const uint8_t* tin, const uint32_t* wts,
-                                        const DwConst* cst, uint8_t* tout, int n, int c0, int oh0, int bh) {
+                                        const DwConst* cst, uint8_t* tout, int n, int c0, int oh0, int bh, bool zw,
+                                        bool clip, bool shadow) {
   const int tid = threadIdx.x;
   const int CT = 16 * d.cbg;
   const uint32_t plane = (uint32_t)(bh * d.OW);                    // tile elements per channel
   const uint32_t m_plane = bh == d.BH ? d.m_plane : d.m_plane_last;
   const uint32_t m_ow = d.m_ow;
   const uint32_t total = plane * (uint32_t)CT;
-  const int sh = d.sh;
   const int Wp = d.Wp, rin = d.rows_in;
-  const int colofs = kDwPL - d.pl;
   const uint32_t n4 = g.out_elems * 4u;
   const auto r_conv = rec_rsrc(g.C, n4), r_bias = rec_rsrc(g.bias_out, n4);
   const auto r_rq = rec_rsrc(g.rq_out, g.out_elems);
-  const auto r_clip = rec_rsrc(g.clip_out, CLIP ? g.out_elems : 0u);
-  const int32_t qmin = (int32_t)g.rq.qmin, qmax = (int32_t)g.rq.qmax, zpo = g.rq.zp_out;
-  const int32_t clip_lo = g.clip_lo, clip_hi = g.clip_hi;
-  const int mode = g.rq.mode;
-  const uint32_t sxor = g.shadow_xor;
+  const auto r_clip = rec_rsrc(g.clip_out, clip ? g.out_elems : 0u);
   // (whole-plane tiles: the CT channel runs are adjacent in memory, so the tile is one run)
   const uint32_t base0 = (uint32_t)(((n * d.C + c0) * d.OH + oh0) * d.OW);
   const uint32_t cstride = (uint32_t)(d.OH * d.OW);
   for (uint32_t f0 = 4u * tid; f0 < total; f0 += 4u * kDwThreads) {
     int32_t v[4];
     int cc[4], pp[4];
+    if constexpr (MODE == kDwGen) {
+      const int colofs = kDwPL - d.pl, sh = d.sh;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t f = f0 + e;
-      const uint32_t c = fdiv_u(f, m_plane);
-      const uint32_t rem = f - c * plane;
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t f = f0 + e;
+        const uint32_t c = fdiv_u(f, m_plane);
+        const uint32_t rem = f - c * plane;
+        const uint32_t r = fdiv_u(rem, m_ow);
+        const uint32_t ow = rem - r * (uint32_t)d.OW;
+        cc[e] = (int)c;
+        pp[e] = (int)rem;
+        // tap row t of output (r, ow): bytes [a, a + 3) of the staged row r * sh + t
+        const int a0 = ((int)c * rin + (int)r * sh) * Wp + colofs + (int)ow * sh;
+        int32_t acc = 0, sx = 0;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int a = a0 + t * Wp;
+          const uint32_t* q = reinterpret_cast<const uint32_t*>(tin + (a & ~3));
+          const uint32_t win = __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+          acc = __builtin_amdgcn_sdot4((int)win, (int)wts[c * 4 + t], acc, false);
+          if (zw) sx = __builtin_amdgcn_sdot4((int)win, 0x00010101, sx, false);
+        }
+        uint32_t val = (uint32_t)acc + cst[c].fold;
+        if (zw) val -= (uint32_t)cst[c].zwc * (uint32_t)sx;
+        v[e] = (int32_t)val;
+      }
+      dw_epilogue<FAST>(g, cst, tout, plane, v, cc, pp, base0 + (uint32_t)cc[0] * cstride + (uint32_t)pp[0], r_conv,
+                        r_bias, r_rq, r_clip, clip, shadow, false);
+    } else {
+      // 4 outputs of one row: channel c, row r, columns ow0 .. ow0 + 3 (ow0 % 4 == 0); with the
+      // left padding 1 the first tap byte sits at 3 mod 4, so each tap row is 3 (stride 1) or 4
+      // (stride 2) aligned dwords and the windows are fixed byte shifts of them
+      constexpr int SH = MODE == kDwRow1 ? 1 : 2;
+      const uint32_t c = fdiv_u(f0, m_plane);
+      const uint32_t rem = f0 - c * plane;
       const uint32_t r = fdiv_u(rem, m_ow);
-      const uint32_t ow = rem - r * (uint32_t)d.OW;
-      cc[e] = (int)c;
-      pp[e] = (int)rem;
-      // tap row t of output (r, ow): bytes [a, a + 3) of the staged row r * sh + t
-      const int a0 = ((int)c * rin + (int)r * sh) * Wp + colofs + (int)ow * sh;
-      int32_t acc = 0, sx = 0;
+      const uint32_t ow0 = rem - r * (uint32_t)d.OW;
+      const int al = ((int)c * rin + (int)r * SH) * Wp + (kDwPL - 4) + (int)ow0 * SH;  // = first tap byte - 3
+      int32_t acc[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        const int a = a0 + t * Wp;
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(tin + (a & ~3));
-        const uint32_t win = __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
-        acc = __builtin_amdgcn_sdot4((int)win, (int)wts[c * 4 + t], acc, false);
-        if constexpr (ZW) sx = __builtin_amdgcn_sdot4((int)win, 0x00010101, sx, false);
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(tin + al + t * Wp);
+        const int wr = (int)wts[c * 4 + t];
+        uint32_t win[4];
+        if constexpr (SH == 1) {
+          const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+          win[0] = __builtin_amdgcn_alignbyte(d1, d0, 3);
+          win[1] = d1;
+          win[2] = __builtin_amdgcn_alignbyte(d2, d1, 1);
+          win[3] = __builtin_amdgcn_alignbyte(d2, d1, 2);
+        } else {
+          const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+          win[0] = __builtin_amdgcn_alignbyte(d1, d0, 3);
+          win[1] = __builtin_amdgcn_alignbyte(d2, d1, 1);
+          win[2] = __builtin_amdgcn_alignbyte(d2, d1, 3);
+          win[3] = __builtin_amdgcn_alignbyte(d3, d2, 1);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[e] = __builtin_amdgcn_sdot4((int)win[e], wr, acc[e], false);
+          if (zw) sx[e] = __builtin_amdgcn_sdot4((int)win[e], 0x00010101, sx[e], false);
+        }
       }
-      const DwConst& k = cst[c];
-      uint32_t val = (uint32_t)acc + k.fold;
-      if constexpr (ZW) val -= (uint32_t)k.zwc * (uint32_t)sx;
-      v[e] = (int32_t)val;
-    }
-    // the group's 4 elements are contiguous in every record (tile runs are multiples of 4)
-    const uint32_t c_first = (uint32_t)cc[0];
-    const uint32_t o = base0 + c_first * cstride + (uint32_t)pp[0];
-    __builtin_amdgcn_raw_buffer_store_b128(v4i{v[0], v[1], v[2], v[3]}, r_conv, o * 4u, 0, 0);
-    int32_t q[4];
+      const uint32_t fold = cst[c].fold;
+      const uint32_t zwc = (uint32_t)cst[c].zwc;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const DwConst& k = cst[cc[e]];
-      v[e] = (int32_t)((uint32_t)v[e] + (uint32_t)k.bias);
-    }
-    __builtin_amdgcn_raw_buffer_store_b128(v4i{v[0], v[1], v[2], v[3]}, r_bias, o * 4u, 0, 0);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const DwConst& k = cst[cc[e]];
-      const int32_t t = (int32_t)((uint32_t)v[e] - (uint32_t)k.zp);
-      int32_t y;
-      if constexpr (FAST) {
-        const int sh2 = -k.s - 1;
-        y = (int32_t)((uint32_t)__mulhi(t, k.m) + (1u << (sh2 - 1))) >> sh2;
-      } else {
-        y = rq_core(t, mode, k.m, k.s);
+      for (int e = 0; e < 4; ++e) {
+        uint32_t val = (uint32_t)acc[e] + fold;
+        if (zw) val -= zwc * (uint32_t)sx[e];
+        v[e] = (int32_t)val;
+        cc[e] = (int)c;
+        pp[e] = (int)rem + e;
       }
-      q[e] = clamp_i32((int32_t)((uint32_t)zpo + (uint32_t)y), qmin, qmax);
-    }
-    __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_rq, o, 0, 0);
-    if constexpr (CLIP) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) q[e] = clamp_i32(q[e], clip_lo, clip_hi);
-      __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, 0);
-    }
-    if constexpr (SHADOW) {
-      // [group][pixel][16]: channel c of tile pixel p at ((c >> 4) * plane + p) * 16 + (c & 15)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        tout[(((uint32_t)cc[e] >> 4) * plane + (uint32_t)pp[e]) * 16u + (cc[e] & 15)] = (uint8_t)((uint32_t)q[e] ^ sxor);
+      dw_epilogue<FAST>(g, cst, tout, plane, v, cc, pp, base0 + c * cstride + rem, r_conv, r_bias, r_rq, r_clip, clip,
+                        shadow, true);
     }
   }
 }
 
-__global__ __launch_bounds__(kDwThreads) void dw_tile_kernel(DwArgs d, GemmArgs g) {
+// Staged input: row (c, rr) = input row ih0 + rr of channel c0 + c at LDS bytes [kDwPL, kDwPL + W)
+// of a Wp-byte row; the pads and out-of-image rows hold the staged zero point.  VW-byte loads,
+// UNROLL of them in flight per thread before they are written.
+template <int VW>
+__device__ __forceinline__ void dw_stage_data(const DwArgs& d, uint8_t* tin, int n, int c0, int ih0, int CT) {
+  typedef typename std::conditional<VW == 16, v4u, typename std::conditional<VW == 8, uint64_t,
+          typename std::conditional<VW == 4, uint32_t, typename std::conditional<VW == 2, uint16_t, uint8_t>::type>::type>::type>::type VT;
+  constexpr int UNROLL = VW == 16 ? 4 : VW == 8 ? 6 : 8;
+  const int tid = threadIdx.x;
+  const int cpr = d.W / VW;                 // loads per row
+  const int total = CT * d.rows_in * cpr;   // (rows outside the image keep the zero-point fill)
+  const uint32_t xb = d.xor_x;
+  const uint8_t* xbase = d.x + (int64_t)(n * d.C + c0) * d.H * d.W;
+  for (int k0 = tid; k0 < total; k0 += UNROLL * kDwThreads) {
+    VT val[UNROLL];
+    int dst[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = k0 + u * kDwThreads;
+      const int row = (int)fdiv_u((uint32_t)k, d.m_cpr), j = k - row * cpr;
+      const int c = (int)fdiv_u((uint32_t)row, d.m_rin), rr = row - c * d.rows_in;
+      const int ih = ih0 + rr;
+      const bool ok = k < total && ih >= 0 && ih < d.H;
+      dst[u] = ok ? row * d.Wp + kDwPL + j * VW : -1;
+      if (ok) val[u] = ldg(reinterpret_cast<const VT*>(xbase + ((int64_t)c * d.H + ih) * d.W + j * VW));
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (dst[u] < 0) continue;
+      VT x = val[u];
+      if constexpr (VW == 16) {
+        x ^= v4u{xb * 0x01010101u, xb * 0x01010101u, xb * 0x01010101u, xb * 0x01010101u};
+      } else if constexpr (VW == 8) {
+        x ^= (uint64_t)xb * 0x0101010101010101ull;
+      } else if constexpr (VW == 4) {
+        x ^= xb * 0x01010101u;
+      } else if constexpr (VW == 2) {
+        x = (uint16_t)(x ^ (uint16_t)(xb * 0x0101u));
+      } else {
+        x = (uint8_t)(x ^ (uint8_t)xb);
+      }
+      *reinterpret_cast<VT*>(tin + dst[u]) = x;
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kDwThreads, 6) void dw_tile_kernel(DwArgs d, GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   const int tid = threadIdx.x;
   const int CT = 16 * d.cbg;
@@ -171,104 +283,67 @@ __global__ __launch_bounds__(kDwThreads) void dw_tile_kernel(DwArgs d, GemmArgs 
   uint32_t* wts = reinterpret_cast<uint32_t*>(dsm + d.lds_const);      // [CT][4] packed rows
   DwConst* cst = reinterpret_cast<DwConst*>(dsm + d.lds_const + CT * 16);
   uint8_t* tout = dsm + d.lds_tout;
-  // ---- stage the input rows: dword k of staged row (c, rr) holds bytes [4k, 4k + 4) of
-  // [kDwPL pad][W data][pad], pads and out-of-image rows holding the staged zero point
-  const uint32_t za4 = 0x01010101u * (uint8_t)d.za_s;
-  const int wpd = d.Wp / 4;
-  const int nrow = CT * d.rows_in;
-  const int ndw = nrow * wpd;
-  const uint32_t xx4 = 0x01010101u * d.xor_x;
-  for (int k0 = tid; k0 < ndw; k0 += 4 * kDwThreads) {
-    uint32_t val[4];
+  // ---- this channel's weights and epilogue operands, loaded before the staging so that their
+  // latency overlaps it (written to LDS after it)
+  const int ch = c0 + min(tid, CT - 1);
+  const bool axis = g.rq.mode == TK_RQ_AXIS_UPWARD || g.rq.mode == TK_RQ_AXIS_TONEAREST;
+  uint32_t wb[9];
+  int32_t zw = d.zw, bias = 0, m = g.rq.multiplier, sft = g.rq.shift, zp = g.rq.zp_in;
+  if (tid < CT) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = k0 + u * kDwThreads;
-      val[u] = za4;
-      if (k < ndw) {
-        const int row = k / wpd, kd = k - row * wpd;
-        const int c = row / d.rows_in, rr = row - c * d.rows_in;
-        const int ih = ih0 + rr;
-        const int b0 = kd * 4 - kDwPL;  // input column of the dword's first byte
-        if (ih >= 0 && ih < d.H && b0 + 3 >= 0 && b0 < d.W) {
-          const uint8_t* src = d.x + ((int64_t)(n * d.C + c0 + c) * d.H + ih) * d.W;
-          if (d.wdw && b0 >= 0 && b0 + 3 < d.W) {
-            val[u] = ldg(reinterpret_cast<const uint32_t*>(src + b0)) ^ xx4;
-          } else {
-            uint32_t wv = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int col = b0 + j;
-              const uint32_t byte = (col >= 0 && col < d.W) ? ((uint32_t)ldg(src + col) ^ d.xor_x) : (uint32_t)(uint8_t)d.za_s;
-              wv |= (byte & 0xFFu) << (8 * j);
-            }
-            val[u] = wv;
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = k0 + u * kDwThreads;
-      if (k < ndw) reinterpret_cast<uint32_t*>(tin)[k] = val[u];
-    }
+    for (int i = 0; i < 9; ++i) wb[i] = (uint32_t)ldg(d.w + (int64_t)ch * 9 + i);
+    if (d.zw_vec) zw = ldg(d.zw_vec + ch);
+    bias = ldg(g.bias + ch);
+    if (axis) m = ldg(g.rq.ms + ch), sft = ldg(g.rq.ss + ch);
+    if (g.rq.zps) zp = ldg(g.rq.zps + ch);
+  }
+  // ---- every staged byte to the zero point (16-byte stores), then the image's bytes over it
+  {
+    const uint32_t za4 = 0x01010101u * (uint8_t)d.za_s;
+    const int n16 = CT * d.rows_in * d.Wp / 16;
+    for (int k = tid; k < n16; k += kDwThreads) reinterpret_cast<v4u*>(tin)[k] = v4u{za4, za4, za4, za4};
+    lds_barrier();  // (orders LDS only: the operand loads above stay in flight)
+  }
+  switch (d.vw) {
+    case 16: dw_stage_data<16>(d, tin, n, c0, ih0, CT); break;
+    case 8: dw_stage_data<8>(d, tin, n, c0, ih0, CT); break;
+    case 4: dw_stage_data<4>(d, tin, n, c0, ih0, CT); break;
+    case 2: dw_stage_data<2>(d, tin, n, c0, ih0, CT); break;
+    default: dw_stage_data<1>(d, tin, n, c0, ih0, CT); break;
   }
   // ---- per channel: packed weight rows (w0, w1, w2, 0) and the epilogue constants
   int shift_ok = 1;  // this channel's right shift is >= 2 (the mul_hi requantize form applies)
   if (tid < CT) {
-    const int ch = c0 + tid;
-    const int32_t zw = d.zw_vec ? ldg(d.zw_vec + ch) : d.zw;
     const int32_t zws = d.w_u8 ? zw - 128 : zw;
     int32_t sw = 0;
-    uint32_t rows[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       uint32_t pk = 0;
 #pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        const uint32_t b = ((uint32_t)ldg(d.w + (int64_t)ch * 9 + r * 3 + s) ^ d.xor_w) & 0xFFu;
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const uint32_t b = (wb[r * 3 + s2] ^ d.xor_w) & 0xFFu;
         sw += (int32_t)(int8_t)b;
-        pk |= b << (8 * s);
+        pk |= b << (8 * s2);
       }
-      rows[r] = pk;
       wts[tid * 4 + r] = pk;
     }
     wts[tid * 4 + 3] = 0;
     DwConst k{};
     k.fold = (uint32_t)0 - (uint32_t)d.za_s * (uint32_t)sw + 9u * (uint32_t)d.za_s * (uint32_t)zws;
     k.zwc = zws;
-    k.bias = ldg(g.bias + ch);
-    const bool axis = g.rq.mode == TK_RQ_AXIS_UPWARD || g.rq.mode == TK_RQ_AXIS_TONEAREST;
-    k.m = axis ? ldg(g.rq.ms + ch) : g.rq.multiplier;
-    k.s = axis ? ldg(g.rq.ss + ch) : g.rq.shift;
-    k.zp = g.rq.zps ? ldg(g.rq.zps + ch) : g.rq.zp_in;
-    k.wrow0 = rows[0];
+    k.bias = bias;
+    k.m = m;
+    k.s = sft;
+    k.zp = zp;
     cst[tid] = k;
     shift_ok = k.s <= -2;
   }
   const bool fast = __syncthreads_and(shift_ok) && (g.rq.mode == TK_RQ_AXIS_UPWARD || g.rq.mode == TK_RQ_TENSOR_UPWARD);
   const bool zw_any = d.zw_vec || d.w_u8 || d.zw != 0;
   const bool shadow = g.shadow_out != nullptr;
-  using T = std::true_type;
-  using F = std::false_type;
-  auto go = [&](auto zw_c, auto fast_c, auto clip_c, auto sh_c) __attribute__((always_inline)) {
-    dw_walk<decltype(zw_c)::value, decltype(fast_c)::value, decltype(clip_c)::value, decltype(sh_c)::value>(
-        d, g, tin, wts, cst, tout, n, c0, oh0, bh);
-  };
-  auto by_shadow = [&](auto zw_c, auto fast_c, auto clip_c) __attribute__((always_inline)) {
-    if (shadow) go(zw_c, fast_c, clip_c, T{});
-    else go(zw_c, fast_c, clip_c, F{});
-  };
-  auto by_clip = [&](auto zw_c, auto fast_c) __attribute__((always_inline)) {
-    if (g.has_clip) by_shadow(zw_c, fast_c, T{});
-    else by_shadow(zw_c, fast_c, F{});
-  };
-  if (zw_any) {
-    if (fast) by_clip(T{}, T{});
-    else by_clip(T{}, F{});
-  } else {
-    if (fast) by_clip(F{}, T{});
-    else by_clip(F{}, F{});
-  }
+  const bool clip = g.has_clip != 0;
+  if (fast) dw_walk<MODE, true>(d, g, tin, wts, cst, tout, n, c0, oh0, bh, zw_any, clip, shadow);
+  else dw_walk<MODE, false>(d, g, tin, wts, cst, tout, n, c0, oh0, bh, zw_any, clip, shadow);
   if (!shadow) return;
   __syncthreads();
   // ---- the next conv's shadow: 16 channels of one pixel per 16-byte store, the tile's pixels of
@@ -294,7 +369,7 @@ int dw_block_try(const tk_tensor* data, const tk_tensor* weight, const ConvGeom&
   const int sh = a->strides[0];
   if (!(a->groups == g.C && g.C == g.O && g.C % 16 == 0 && g.KH == 3 && g.KW == 3 && a->dilation[0] == 1 &&
         a->dilation[1] == 1 && a->strides[1] == sh && (sh == 1 || sh == 2) && a->padding[0] <= 2 &&
-        a->padding[1] <= kDwPL && ga.bias_out && ga.rq_out))
+        a->padding[1] <= 2 && g.OW >= 2 && ga.bias_out && ga.rq_out))
     return 0;
   if ((int64_t)g.N * g.O * g.OH * g.OW * 4 >= (int64_t)UINT32_MAX || !is_int8ish(data) || !is_int8ish(weight))
     return 0;
@@ -320,42 +395,51 @@ int dw_block_try(const tk_tensor* data, const tk_tensor* weight, const ConvGeom&
   d.pt = a->padding[0];
   d.pl = a->padding[1];
   d.npix = g.N * OHW;
-  d.wdw = g.W % 4 == 0;
+  d.vw = g.W % 16 == 0 ? 16 : g.W % 8 == 0 ? 8 : g.W % 4 == 0 ? 4 : g.W % 2 == 0 ? 2 : 1;
+  // row groups (4 outputs of one row, taps from aligned dwords) where the plane allows them
+  const int mode = g.OW % 4 == 0 && d.pl == 1 ? (sh == 1 ? kDwRow1 : kDwRow2) : kDwGen;
+  // staged row: [kDwPL][W][pads], long enough for the last group's tap dwords
+  const int need = std::max(kDwPL + g.W + 4, kDwPL - d.pl + (g.OW - 1) * sh + 16);
+  d.Wp = (need + 15) & ~15;
+  auto lds_of = [&](int cbg, int BH) {
+    const int CT = 16 * cbg;
+    const size_t tin = (size_t)CT * ((BH - 1) * sh + 3) * d.Wp + 16;
+    return tin + (size_t)CT * 16 + (size_t)CT * sizeof(DwConst) + (size_t)CT * BH * g.OW;
+  };
+  constexpr size_t kLds = 64 * 1024;
   // tiles: whole planes of up to 1024 pixels (cbg 16-channel groups so that a tile has >= ~3k
-  // outputs), else bands of rows of whole 4-element groups
+  // outputs) when they fit, else bands of rows (whole 4-element groups per channel run)
   int cbg = 1, BH = g.OH;
-  if (OHW <= 1024) {
-    while (cbg < 4 && 16 * cbg * 2 * OHW <= 4096 && g.C % (32 * cbg) == 0) cbg *= 2;
+  if (OHW <= 1024 && lds_of(1, g.OH) <= kLds) {
+    while (cbg < 4 && 16 * cbg * 2 * OHW <= 8192 && g.C % (32 * cbg) == 0 && lds_of(2 * cbg, g.OH) <= kLds) cbg *= 2;
   } else {
     if (g.OW % 4) return 0;
-    BH = std::max(1, (sh == 1 ? 1024 : 512) / g.OW);
+    BH = std::max(1, std::min(g.OH, (sh == 1 ? 512 : 256) / g.OW));
+    while (BH > 1 && lds_of(1, BH) > kLds) --BH;
+    if (lds_of(1, BH) > kLds) return 0;
   }
   d.cbg = cbg;
   d.BH = BH;
   d.bands = (g.OH + BH - 1) / BH;
-  if ((BH * g.OW) % 4 || (g.OH % BH && ((g.OH % BH) * g.OW) % 4)) return 0;
-  if (cbg > 1 && BH != g.OH) return 0;
   d.rows_in = (BH - 1) * sh + 3;
   // x / d as __umulhi(x, ceil(2^32 / d)): exact for x * d < 2^32 (tile indices < 2^16, d <= 2^16)
   auto magic = [](uint32_t v) { return (uint32_t)((0x100000000ull + v - 1) / v); };
   const int last = g.OH - (d.bands - 1) * BH;
-  if (g.OW < 2 || (int64_t)16 * cbg * BH * g.OW >= 65536) return 0;
+  if ((int64_t)16 * cbg * BH * g.OW >= 65536 || g.W / d.vw < 2) return 0;
   d.m_ow = magic((uint32_t)g.OW);
   d.m_plane = magic((uint32_t)(BH * g.OW));
   d.m_plane_last = magic((uint32_t)(last * g.OW));
-  // staged row: [kDwPL][W][pads], long enough for the last output's taps plus the second dword
-  // a tap row reads
-  const int need = std::max(kDwPL + g.W + 4, kDwPL - d.pl + (g.OW - 1) * sh + 8);
-  d.Wp = (need + 3) & ~3;
+  d.m_cpr = magic((uint32_t)(g.W / d.vw));
+  d.m_rin = magic((uint32_t)d.rows_in);
   const int CT = 16 * cbg;
-  const size_t tin = ((size_t)CT * d.rows_in * d.Wp + 8 + 15) & ~(size_t)15;
+  const size_t tin = (size_t)CT * d.rows_in * d.Wp + 16;
   d.lds_const = (int32_t)tin;
-  const size_t cst = (size_t)CT * 16 + (size_t)CT * sizeof(DwConst);
-  d.lds_tout = (int32_t)(tin + cst);
-  const size_t lds = tin + cst + (size_t)CT * BH * g.OW;
-  if (lds > 64 * 1024) return 0;
+  d.lds_tout = (int32_t)(tin + (size_t)CT * 16 + (size_t)CT * sizeof(DwConst));
+  const size_t lds = lds_of(cbg, BH);
   const unsigned grid = (unsigned)((int64_t)g.N * (g.C / CT) * d.bands);
-  hipLaunchKernelGGL(dw_tile_kernel, dim3(grid), dim3(kDwThreads), lds, s, d, ga);
+  if (mode == kDwRow1) hipLaunchKernelGGL(dw_tile_kernel<kDwRow1>, dim3(grid), dim3(kDwThreads), lds, s, d, ga);
+  else if (mode == kDwRow2) hipLaunchKernelGGL(dw_tile_kernel<kDwRow2>, dim3(grid), dim3(kDwThreads), lds, s, d, ga);
+  else hipLaunchKernelGGL(dw_tile_kernel<kDwGen>, dim3(grid), dim3(kDwThreads), lds, s, d, ga);
   *rc = hipGetLastError() == hipSuccess ? TK_OK : TK_ERR_HIP;
   if (*rc) set_error("dw_tile_kernel launch failed");
   return 1;

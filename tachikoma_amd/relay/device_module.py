@@ -84,6 +84,7 @@ class DeviceModule:
         self._keep: List[object] = []
         self.node_records: List[List[str]] = []  # tk node index -> record names of its outputs
         self.node_kinds: List[str] = []
+        self.node_native_kinds: List[int] = []  # tk_node kind (TK_NODE_*) of each node
         # param name -> re-derivations of the build-time buffers computed from it (packed MFMA
         # weights + weight sums), re-run whenever the param's device copy is rewritten
         self._derived: Dict[str, List[Callable[[int], None]]] = {}
@@ -337,6 +338,7 @@ class DeviceModule:
         def emit(n, kind, records):
             nodes.append(n)
             self.node_kinds.append(kind)
+            self.node_native_kinds.append(int(n.kind))
             self.node_records.append(records)
 
         def ensure_shadow(name: str):

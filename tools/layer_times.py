@@ -17,7 +17,7 @@ def main(path, model="resnet50", batch=64):
     plan = lower(m.mod, m.params)
     groups = exec_groups(plan)
     blocks = [g for g in groups if g.kind in ("conv_block", "dense_block")]
-    fams = ("gemm_i8_kernel", "direct_conv_kernel", "dw3x3_kernel", "conv_img_kernel", "conv_pf_kernel",
+    fams = ("gemm_i8_kernel", "direct_conv_kernel", "dw3x3_kernel", "dw_tile_kernel", "conv_img_kernel", "conv_pf_kernel",
             "dense_tile_kernel", "dense_slices_epilogue_kernel")
     g_rows = [r for r in rows if any(f in r["Kernel_Name"] for f in fams)]
     # idle time before each launch: end of the previous kernel (any) to this start

@@ -19,7 +19,7 @@ for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_
              "SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES" \
              "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_I8 SQ_INSTS_VALU_MFMA_MOPS_I8 GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $group --kernel-include-regex "gemm_i8_kernel|conv_img_kernel|conv_pf_kernel|dense_tile_kernel|dense_slices_epilogue_kernel|dw3x3_kernel|direct_conv_kernel" --output-format csv \
+  timeout -k 10 300 rocprofv3 --pmc $group --kernel-include-regex "gemm_i8_kernel|conv_img_kernel|conv_pf_kernel|dense_tile_kernel|dense_slices_epilogue_kernel|dw3x3_kernel|dw_tile_kernel|direct_conv_kernel" --output-format csv \
       -d "$OUT/pass$i" -o run -- python3 bench.py --steps 2 --warmup 1 --skip-cpu --no-trace "$@" \
       > "$OUT/pass$i.log" 2>&1 || { echo "pass $i ($group) failed"; tail -5 "$OUT/pass$i.log"; exit 1; }
 done
