@@ -111,11 +111,11 @@ __device__ __forceinline__ void dw_epilogue(const GemmArgs& g, const DwConst* cs
     __builtin_amdgcn_raw_buffer_store_b32(pack4u(q[0], q[1], q[2], q[3]), r_clip, o, 0, 0);
   }
   if (shadow) {
-    // [group][pixel][16]: channel c of tile pixel p at ((c >> 4) * plane + p) * 16 + (c & 15)
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      tout[(((uint32_t)cc[e] >> 4) * plane + (uint32_t)pp[e]) * 16u + (cc[e] & 15)] =
-          (uint8_t)((uint32_t)q[e] ^ g.shadow_xor);
+    // the shadow bytes in the tile's flat order ([channel][pixel]: element f at byte f): one
+    // aligned dword per group (a [pixel][16] layout here would put the lanes' bytes 64 bytes apart,
+    // a 16-way LDS bank conflict per store); transposed to 16-channel chunks after the tile
+    const uint32_t f0 = (uint32_t)cc[0] * plane + (uint32_t)pp[0];
+    *reinterpret_cast<uint32_t*>(tout + f0) = pack4u(q[0], q[1], q[2], q[3]) ^ (g.shadow_xor * 0x01010101u);
   }
 }
 
@@ -347,14 +347,44 @@ __global__ __launch_bounds__(kDwThreads, 6) void dw_tile_kernel(DwArgs d, GemmAr
   if (!shadow) return;
   __syncthreads();
   // ---- the next conv's shadow: 16 channels of one pixel per 16-byte store, the tile's pixels of
-  // each channel group contiguous in [C / 16][N * OH * OW][16]
+  // each channel group contiguous in [C / 16][N * OH * OW][16]; staged as [channel][pixel] bytes,
+  // so 4 pixels of 16 channels are 16 dwords transposed in registers (v_perm_b32)
   const int plane = bh * d.OW;
   const int pix0 = (n * d.OH + oh0) * d.OW;
-  const int nchunk = d.cbg * plane;
-  for (int k = tid; k < nchunk; k += kDwThreads) {
-    const int grp = k / plane, p = k - grp * plane;
-    *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)(c0 / 16 + grp) * d.npix + pix0 + p) * 16) =
-        *reinterpret_cast<const v4i*>(tout + (size_t)k * 16);
+  if (plane % 4 == 0) {
+    const int pq = plane / 4;
+    for (int k = tid; k < d.cbg * pq; k += kDwThreads) {
+      const int grp = k / pq, p4 = (k - grp * pq) * 4;
+      uint32_t in[16];
+#pragma unroll
+      for (int ch = 0; ch < 16; ++ch) in[ch] = *reinterpret_cast<const uint32_t*>(tout + (grp * 16 + ch) * plane + p4);
+      uint8_t* dst = g.shadow_out + ((int64_t)(c0 / 16 + grp) * d.npix + pix0 + p4) * 16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t o[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t lo = __builtin_amdgcn_perm(in[4 * m + 1], in[4 * m], 0x0c0c0000u | ((4u + j) << 8) | (uint32_t)j);
+          const uint32_t hi = __builtin_amdgcn_perm(in[4 * m + 3], in[4 * m + 2], 0x00000c0cu | ((uint32_t)j << 16) | ((4u + j) << 24));
+          o[m] = lo | hi;
+        }
+        *reinterpret_cast<v4i*>(dst + j * 16) = v4i{(int)o[0], (int)o[1], (int)o[2], (int)o[3]};
+      }
+    }
+  } else {
+    for (int k = tid; k < d.cbg * plane; k += kDwThreads) {
+      const int grp = k / plane, p = k - grp * plane;
+      uint32_t o[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) w |= (uint32_t)tout[(grp * 16 + 4 * m + b) * plane + p] << (8 * b);
+        o[m] = w;
+      }
+      *reinterpret_cast<v4i*>(g.shadow_out + ((int64_t)(c0 / 16 + grp) * d.npix + pix0 + p) * 16) =
+          v4i{(int)o[0], (int)o[1], (int)o[2], (int)o[3]};
+    }
   }
 }
 
@@ -407,16 +437,20 @@ int dw_block_try(const tk_tensor* data, const tk_tensor* weight, const ConvGeom&
     return tin + (size_t)CT * 16 + (size_t)CT * sizeof(DwConst) + (size_t)CT * BH * g.OW;
   };
   constexpr size_t kLds = 64 * 1024;
-  // tiles: whole planes of up to 1024 pixels (cbg 16-channel groups so that a tile has >= ~3k
-  // outputs) when they fit, else bands of rows (whole 4-element groups per channel run)
+  // tiles: whole planes of up to 1024 pixels, 1, 2 or 4 16-channel groups per tile so that a tile
+  // has ~3k outputs (14x14: one group, 1536 tiles at B = 64; 7x7: four); larger planes in bands of
+  // ~512 (stride 1) / ~256 (stride 2) output pixels per channel.  (Measured on MobileNetV2 at
+  // B = 64: more, smaller tiles -- 14-row bands of the 28x28 planes, 6-row bands of a 14x14 one,
+  // two groups on 7x7 -- ran 1-5 us slower per layer; two groups on 14x14 planes 4 us slower.)
+  auto band_ok = [&](int bh) { return (bh * g.OW) % 4 == 0 && ((g.OH % bh) * g.OW) % 4 == 0; };
   int cbg = 1, BH = g.OH;
   if (OHW <= 1024 && lds_of(1, g.OH) <= kLds) {
-    while (cbg < 4 && 16 * cbg * 2 * OHW <= 8192 && g.C % (32 * cbg) == 0 && lds_of(2 * cbg, g.OH) <= kLds) cbg *= 2;
+    while (cbg < 4 && 16 * cbg * 2 * OHW <= 4096 && g.C % (32 * cbg) == 0 && lds_of(2 * cbg, g.OH) <= kLds) cbg *= 2;
   } else {
-    if (g.OW % 4) return 0;
-    BH = std::max(1, std::min(g.OH, (sh == 1 ? 512 : 256) / g.OW));
-    while (BH > 1 && lds_of(1, BH) > kLds) --BH;
-    if (lds_of(1, BH) > kLds) return 0;
+    int bh = std::max(1, std::min(g.OH, (sh == 1 ? 512 : 256) / g.OW));
+    while (bh > 1 && (lds_of(1, bh) > kLds || !band_ok(bh))) --bh;
+    if (!band_ok(bh) || lds_of(1, bh) > kLds) return 0;
+    BH = bh;
   }
   d.cbg = cbg;
   d.BH = BH;

@@ -717,6 +717,10 @@ DW_CASES = [
     (2, 32, 30, 30, 1, 0, "int8", "uint8", 5, 120, "axis", "UPWARD", "int8", (-3, 90)),
     (2, 16, 20, 20, 1, 1, "int8", "int8", 0, 0, 0.5, "TONEAREST", "int8", None),
     (2, 16, 9, 9, 2, 1, "uint8", "int8", 125, 0, 0.0007, "UPWARD", "uint8", (130, 250)),
+    # full-batch shapes whose plans differ from the small-batch ones: row bands of 14-wide planes
+    # (flat groups, 6-row bands and a 2-row last band) and 28-wide bands with many tiles
+    (64, 192, 28, 28, 2, 1, "int8", "int8", 2, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (64, 192, 28, 28, 1, 1, "int8", "int8", -3, 0, "axis", "UPWARD", "int8", (0, 127)),
 ]
 
 
