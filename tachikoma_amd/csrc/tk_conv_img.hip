@@ -451,10 +451,13 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     rowc[tid] = r;
   }
   if (has_add) {
-    // RequantizeOrUpcast of every 8-bit value of both qnn.add operands (op_common.h:186-200)
-    const int32_t x = g.rq.qmin == 0 ? tid : (int32_t)(int8_t)(uint8_t)tid;
-    lut[tid] = g.add_up_b ? x : rq_tensor(x, g.add_pb);
-    lut[256 + tid] = g.add_up_r ? x : rq_tensor(x, g.add_pr);
+    // RequantizeOrUpcast of every 8-bit value of both qnn.add operands (op_common.h:186-200): the
+    // block's own values indexed by value - qmin (one v_lshl_add per lookup), the residual's by its
+    // raw byte, with the add's - zp_out folded in
+    const int32_t xb = (int32_t)g.rq.qmin + tid;
+    const int32_t xr = g.rq.qmin == 0 ? tid : (int32_t)(int8_t)(uint8_t)tid;
+    lut[tid] = g.add_up_b ? xb : rq_tensor(xb, g.add_pb);
+    lut[256 + tid] = (int32_t)((uint32_t)(g.add_up_r ? xr : rq_tensor(xr, g.add_pr)) - (uint32_t)g.add_zp);
   }
   const int ts = h.tstride;
   // columns of the tile staged per pass: [c0, c0 + span)
@@ -486,6 +489,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   const int32_t clip_lo = g.clip_lo, clip_hi = g.clip_hi, add_zp = g.add_zp;
   const int mode = g.rq.mode, Mrows = g.M;
   const int dr = 1024 / W, dp = 1024 - dr * W;
+  // the walk's record offset o and staging slot base advance by fixed steps plus a correction
+  // for each pixel / row wrap (no per-group products)
+  const uint32_t dO = (uint32_t)(dr * hw + dp), dOp = (uint32_t)(hw - W), dOr = (uint32_t)((Mrows - R) * hw);
+  const int dB = dr * ts + dp, dBp = ts - W, dBr = W - R * ts;
+  const int32_t* lut_b = lut - (int32_t)g.rq.qmin;  // lut_b[q], q in [qmin, qmin + 255]
   int c0 = 0;  // first pixel of the current pass
   // nontemporal record stores (plain ones measured no faster, also on multi-pass epilogues:
   // profiles/r03k_img_epilogue_ablations.txt)
@@ -500,6 +508,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     constexpr bool ROWU = decltype(rowu_c)::value;
     int kk = 0, r0 = (4 * tid) / W, p0 = 4 * tid - r0 * W;
     while (r0 >= R) r0 -= R, ++kk;
+    uint32_t on = (uint32_t)(((img0 + kk) * Mrows + m0 + r0) * hw + c0 + p0);
     // software pipeline by one group: the next group's tile values, row constants and residual
     // word are read from LDS before this group's arithmetic and stores (at one or two waves per
     // SIMD nothing else hides the LDS latency); slots are read unconditionally (in bounds: the
@@ -529,7 +538,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     int basen = r0 * ts + kk * W + p0;
     load(r0, basen, p0, tid, vn, ran, rbn, resn);
     for (int gi = tid; gi < total; gi += kGemmThreads) {
-      const uint32_t o = (uint32_t)(((img0 + kk) * Mrows + m0 + r0) * hw + c0 + p0);
+      const uint32_t o = on;
       const int base = basen, pc = p0;
       v4u v = vn;
       const EpiRow ra = ran, rb = rbn;
@@ -537,10 +546,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       // next group: 1024 elements on
       r0 += dr;
       p0 += dp;
-      if (p0 >= W) p0 -= W, ++r0;
-      while (r0 >= R) r0 -= R, ++kk;
-      basen = r0 * ts + kk * W + p0;
-      if (gi + kGemmThreads < total) load(r0, basen, p0, gi + kGemmThreads, vn, ran, rbn, resn);
+      on += dO;
+      basen += dB;
+      if (p0 >= W) p0 -= W, ++r0, on += dOp, basen += dBp;
+      while (r0 >= R) r0 -= R, on += dOr, basen += dBr;
+      load(r0, basen, p0, gi + kGemmThreads, vn, ran, rbn, resn);  // (past the end: in-bounds LDS reads, unused)
       uint32_t fold[4], zp[4];
       int32_t bias[4], m[4], sh[4];
 #pragma unroll
@@ -589,7 +599,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           q[e] = clamp_i32(TK_ABL(8192) ? q[e] + (int32_t)((res >> (8 * e)) & 0xFFu) - add_zp
-                                        : lut[q[e] & 0xFF] + lut[256 + ((res >> (8 * e)) & 0xFFu)] - add_zp,
+                                        : (int32_t)((uint32_t)lut_b[q[e]] + (uint32_t)lut[256 + ((res >> (8 * e)) & 0xFFu)]),
                            qmin, qmax);
         if (!TK_ABL(16384 | 2)) st32(pack4u(q[0], q[1], q[2], q[3]), r_add, o);
       }
@@ -639,6 +649,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     // are the images' pixels in order, so column col is shadow pixel img0 * hw + c0 + col
     if (g.shadow_out && !TK_ABL(1)) {
       lds_barrier();
+      const uint32_t sx4 = (uint32_t)g.shadow_xor * 0x01010101u;
       const int pe = npass > 1 ? W : nimg * hw;  // this pass's pixels (the last workgroup may hold fewer images)
 #pragma unroll
       for (int grp = 0; grp < R / 16; ++grp)
@@ -646,11 +657,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
           uint32_t wd[4];
 #pragma unroll
           for (int d = 0; d < 4; ++d) {
-            uint32_t word = 0;
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq)
-              word |= (((uint32_t)tileI[(grp * 16 + d * 4 + qq) * ts + col] ^ g.shadow_xor) & 0xFFu) << (8 * qq);
-            wd[d] = word;
+            const int32_t* t = tileI + (grp * 16 + d * 4) * ts + col;
+            wd[d] = pack4u((uint32_t)t[0], (uint32_t)t[ts], (uint32_t)t[2 * ts], (uint32_t)t[3 * ts]) ^ sx4;
           }
           *reinterpret_cast<v4i*>(g.shadow_out +
                                   ((int64_t)((m0 >> 4) + grp) * g.N + (int64_t)img0 * hw + c0 + col) * 16) =
