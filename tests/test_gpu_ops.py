@@ -429,6 +429,11 @@ ALGO_CASES = [
     # and a stride-2 3x3 on an odd input width (no column-parity patch), uint8 with a residual join
     (4, 160, 7, 64, 3, 1, "int8", -3, None, (0, 127)),
     (2, 64, 13, 64, 3, 2, "uint8", 131, (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
+    # round 6, the weight-stationary 1x1 kernel (algo 6): a partial last 32-row chunk under a uint8
+    # residual join (MobileNetV2's 24 -> 144), and 40 channels (a partial 16-channel shadow group)
+    # on a plane that several tiles share
+    (3, 24, 28, 144, 1, 1, "uint8", 131, (0.1, 130, 0.2, 120, 0.15, 128), (128, 255)),
+    (2, 32, 20, 40, 1, 1, "int8", 2, (0.05, 3, 0.07, -2, 0.09, 1), None),
     # dense heads as 1x1 blocks over [B, K, 1, 1] (the dense tile kernel, algo 5): ResNet-50's
     # 2048 -> 1000 over 8 K slices, and a ragged 40-sample uint8 batch
     (64, 2048, 1, 1000, 1, 1, "int8", -3, None, (0, 127)),
