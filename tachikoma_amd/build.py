@@ -31,8 +31,7 @@ LIB = os.path.join(HERE, "libtachikoma.so")
 ARCH = "gfx950"
 
 SOURCES = ["tk_host.cc", "tk_calibrate.cc", "tk_format.cc", "tk_runtime.cc", "tk_elementwise.hip", "tk_gemm.hip",
-           "tk_residual.hip", "tk_realize.hip", "tk_conv_img.hip", "tk_conv_pf.hip", "tk_qnn_ops.hip", "tk_dense.hip", "tk_dw.hip",
-           "tk_conv_ws.hip"]
+           "tk_residual.hip", "tk_realize.hip", "tk_conv_img.hip", "tk_conv_pf.hip", "tk_qnn_ops.hip", "tk_dense.hip", "tk_dw.hip"]
 HEADERS = ["tk_common.h", "tk_conv.h"]
 BASE_FLAGS = ["-std=c++20", "-O3", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-Wall",
               "-Wno-unused-function"]

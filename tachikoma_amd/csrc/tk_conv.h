@@ -262,8 +262,7 @@ int conv_img_pack(const tk_tensor* weight, int8_t* dst, int rows_pad, int cin_pa
 // (gemm_i8_kernel), 2 image tiles with the planner's plan, 3 / 4 persistent im2col tiles with
 // cross-tile prefetch and a 2- / 3-slot ring (conv_pf_kernel), 16 + i image-tile plan i.
 // 5: the small-batch dense tile kernel (tk_dense.hip) for dense blocks run as 1x1 conv blocks.
-// 6: weight-stationary 1x1 tiles (tk_conv_ws.hip).
-constexpr int kAlgoIm2col = 1, kAlgoImg = 2, kAlgoPf2 = 3, kAlgoPf3 = 4, kAlgoDense = 5, kAlgoWs = 6, kAlgoImg0 = 16;
+constexpr int kAlgoIm2col = 1, kAlgoImg = 2, kAlgoPf2 = 3, kAlgoPf3 = 4, kAlgoDense = 5, kAlgoImg0 = 16;
 // Runs the conv block on the image-tile kernel when its plan applies (returns 1 and sets *rc;
 // algo 0: the cheapest plan by the planner's estimate), else returns 0 (im2col path).
 // `chunked`: the chunked weight image (NULL for 1x1 convs, whose packed weight has that layout).
@@ -280,13 +279,6 @@ int conv_img_algos(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& 
 // persistent kernel, and its launch (ring: 2 or 3 slots).
 bool conv_pf_applies(const ConvGeom& g, const GemmArgs& ga);
 int conv_pf_run(const ConvGeom& g, GemmArgs ga, int ring, hipStream_t s);
-
-// ---------------------------------------------------------------- weight-stationary 1x1 blocks
-// (tk_conv_ws.hip) all output channels x a run of one image's pixels per workgroup, the whole
-// weight resident in LDS (algo kAlgoWs): whether it applies, a description, and its launch.
-bool conv_ws_applies(const ConvGeom& g, const GemmArgs& ga);
-int conv_ws_describe(const ConvGeom& g, const GemmArgs& ga, char* buf, int len);
-int conv_ws_run(const ConvGeom& g, GemmArgs ga, hipStream_t s);
 
 // ---------------------------------------------------------------- small-batch dense blocks
 // (tk_dense.hip) [B, K] x [U, K]^T on 32 x 32 tiles with K split over the four waves, one launch.

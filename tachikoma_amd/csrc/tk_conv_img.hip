@@ -1092,7 +1092,7 @@ static int set_lds(ImgKernel kern, size_t lds, int* rc) {
 
 int conv_img_try(const ConvGeom& g, const tk_conv2d_attrs* a, const GemmArgs& ga, const int8_t* chunked, void* scratch,
                  int algo, hipStream_t s, int* rc) {
-  if (algo == kAlgoIm2col || algo == kAlgoPf2 || algo == kAlgoPf3 || algo == kAlgoWs) return 0;
+  if (algo == kAlgoIm2col || algo == kAlgoPf2 || algo == kAlgoPf3) return 0;
   const ImgPlans pp = img_plans(g, a, ga, chunked != nullptr);
   const std::vector<ImgPlan>& plans = *pp;
   if (plans.empty() && algo == 0) return 0;

@@ -1964,14 +1964,6 @@ static int conv2d_run(const tk_tensor* data, const void* shadow, const tk_tensor
       }
       return conv_pf_run(g, ga, algo == kAlgoPf2 ? 2 : 3, s);
     }
-    if (algo == kAlgoWs) {
-      if (!conv_ws_applies(g, ga)) {
-        set_error("tk_qnn_conv2d_block: algo 6 (weight-stationary 1x1 tiles) does not apply to this conv; see "
-                  "tk_conv2d_block_algos");
-        return TK_ERR_INVALID_ARG;
-      }
-      return conv_ws_run(g, ga, s);
-    }
   }
   const bool mt1 = conv_mt1(g, blk != nullptr);
   const int ipt = mt1 ? conv_image_tiles(g, blk != nullptr, conv_needs_patch(weight, a)) : 0;
@@ -2078,11 +2070,6 @@ int conv2d_block_algo_info_impl(const tk_tensor* data, const tk_tensor* weight, 
     std::snprintf(buf, (size_t)len, "%s", fixed);
     return TK_OK;
   }
-  if (algo == kAlgoWs) {
-    const int rc = conv_ws_describe(g, ga, buf, len);
-    if (rc) set_error("tk_conv2d_block_algo_info: algo 6 is not listed for this block");
-    return rc;
-  }
   const int rc = conv_img_describe(g, &attrs->conv, ga,
                                    g.KH * g.KW == 1 || conv_img_chunked_bytes(g.rows_pad, g.cin_pad, g.KH * g.KW), algo,
                                    buf, len);
@@ -2132,15 +2119,6 @@ int conv2d_block_algos_impl(const tk_tensor* data, const tk_tensor* weight, cons
         if (n < max_algos) algos[n] = al;
         ++n;
       }
-    }
-    // the weight-stationary 1x1 kernel (its stride / padding gates read the conv attributes)
-    pa.sh = attrs->conv.strides[0];
-    pa.sw = attrs->conv.strides[1];
-    pa.pt = attrs->conv.padding[0];
-    pa.pl = attrs->conv.padding[1];
-    if (conv_ws_applies(g, pa)) {
-      if (n < max_algos) algos[n] = kAlgoWs;
-      ++n;
     }
   }
   return n;
