@@ -56,6 +56,7 @@ struct DwArgs {
   int32_t BH, bands, cbg;  // output rows per tile, tiles per plane, 16-channel groups per tile
   int32_t rows_in, Wp;     // staged rows per channel (of Wp bytes, a multiple of 16)
   int32_t vw;              // bytes per staging load: 16, 8, 4, 2 or 1 (divides W)
+  int32_t flat;            // whole-plane tiles staged from the planes' flat run (dw_stage_flat)
   int32_t npix;            // N * OH * OW: pixels per channel group of the shadow
   uint32_t m_ow, m_plane, m_plane_last;  // fdiv_u magics of OW and of a tile's pixels (BH / last band)
   uint32_t m_cpr, m_rin;   // fdiv_u magics of the loads per staged row (W / vw) and of rows_in
@@ -265,6 +266,44 @@ __device__ __forceinline__ void dw_stage_data(const DwArgs& d, uint8_t* tin, int
   }
 }
 
+// Whole-plane tiles on narrow rows (14x14, 7x7: W % 8 != 0, so row loads would be 2- or 1-byte
+// loads, 12+ per thread in a chain of load latencies): the tile's CT input planes are one
+// contiguous, 16-byte aligned run of CT * H * W bytes (c0 is a multiple of 16), loaded 16 bytes per
+// lane; each byte then goes to its padded LDS row, the position advanced byte by byte.
+__device__ __forceinline__ void dw_stage_flat(const DwArgs& d, uint8_t* tin, int n, int c0, int ih0, int CT) {
+  constexpr int UNROLL = 4;
+  const int tid = threadIdx.x;
+  const int HW = d.H * d.W;
+  const int nq = CT * HW / 16;
+  const v4u* src = reinterpret_cast<const v4u*>(d.x + (int64_t)(n * d.C + c0) * HW);
+  const uint32_t xb4 = d.xor_x * 0x01010101u;
+  for (int q0 = tid; q0 < nq; q0 += UNROLL * kDwThreads) {
+    v4u val[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+      if (q0 + u * kDwThreads < nq) val[u] = ldg(src + q0 + u * kDwThreads);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int q = q0 + u * kDwThreads;
+      if (q >= nq) continue;
+      const int idx = 16 * q;
+      const int c = idx / HW, rem = idx - c * HW;
+      int ih = rem / d.W, iw = rem - ih * d.W;
+      int dst = (c * d.rows_in + ih - ih0) * d.Wp + kDwPL + iw;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        tin[dst] = (uint8_t)((val[u][b >> 2] ^ xb4) >> (8 * (b & 3)));
+        ++dst;
+        if (++iw == d.W) {
+          iw = 0;
+          dst += d.Wp - d.W;
+          if (++ih == d.H) ih = 0, dst += (d.rows_in - d.H) * d.Wp;
+        }
+      }
+    }
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kDwThreads, 6) void dw_tile_kernel(DwArgs d, GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
@@ -304,7 +343,8 @@ __global__ __launch_bounds__(kDwThreads, 6) void dw_tile_kernel(DwArgs d, GemmAr
     for (int k = tid; k < n16; k += kDwThreads) reinterpret_cast<v4u*>(tin)[k] = v4u{za4, za4, za4, za4};
     lds_barrier();  // (orders LDS only: the operand loads above stay in flight)
   }
-  switch (d.vw) {
+  if (d.flat) dw_stage_flat(d, tin, n, c0, ih0, CT);
+  else switch (d.vw) {
     case 16: dw_stage_data<16>(d, tin, n, c0, ih0, CT); break;
     case 8: dw_stage_data<8>(d, tin, n, c0, ih0, CT); break;
     case 4: dw_stage_data<4>(d, tin, n, c0, ih0, CT); break;
@@ -465,6 +505,9 @@ int dw_block_try(const tk_tensor* data, const tk_tensor* weight, const ConvGeom&
   d.m_plane_last = magic((uint32_t)(last * g.OW));
   d.m_cpr = magic((uint32_t)(g.W / d.vw));
   d.m_rin = magic((uint32_t)d.rows_in);
+  // narrow rows of whole-plane tiles whose staged rows cover every input row: the flat staging
+  d.flat = d.bands == 1 && d.vw < 8 && d.rows_in - d.pt >= g.H && (reinterpret_cast<uintptr_t>(d.x) & 15) == 0 &&
+           env_int("TK_DW_FLAT", 1);
   const int CT = 16 * cbg;
   const size_t tin = (size_t)CT * d.rows_in * d.Wp + 16;
   d.lds_const = (int32_t)tin;

@@ -726,6 +726,11 @@ DW_CASES = [
     # (flat groups, 6-row bands and a 2-row last band) and 28-wide bands with many tiles
     (64, 192, 28, 28, 2, 1, "int8", "int8", 2, 0, "axis", "UPWARD", "int8", (0, 127)),
     (64, 192, 28, 28, 1, 1, "int8", "int8", -3, 0, "axis", "UPWARD", "int8", (0, 127)),
+    # round 6, the flat staging of narrow whole planes: four 16-channel groups of 7x7 planes per
+    # tile at the full batch, and a stride-2 unpadded 14x14 plane whose staged rows stop short of the
+    # last input row (the row-load staging keeps it)
+    (64, 960, 7, 7, 1, 1, "int8", "int8", -4, 0, "axis", "UPWARD", "int8", (0, 127)),
+    (2, 16, 14, 14, 2, 0, "uint8", "int8", 120, 0, "axis", "UPWARD", "uint8", None),
 ]
 
 
