@@ -488,6 +488,12 @@ int dw_block_try(const tk_tensor* data, const tk_tensor* weight, const ConvGeom&
     while (cbg < 4 && 16 * cbg * 2 * OHW <= 4096 && g.C % (32 * cbg) == 0 && lds_of(2 * cbg, g.OH) <= kLds) cbg *= 2;
   } else {
     int bh = std::max(1, std::min(g.OH, (sh == 1 ? 512 : 256) / g.OW));
+    // equal bands where a height within [bh / 2, bh] divides the plane (28 rows: 4 x 7, not 9 9 9 1)
+    for (int b = bh; b > 0 && 2 * b >= bh; --b)
+      if (g.OH % b == 0 && band_ok(b) && lds_of(1, b) <= kLds) {
+        bh = b;
+        break;
+      }
     while (bh > 1 && (lds_of(1, bh) > kLds || !band_ok(bh))) --bh;
     if (!band_ok(bh) || lds_of(1, bh) > kLds) return 0;
     BH = bh;
