@@ -477,7 +477,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   // group gi = 4 consecutive elements of image run kk = gi / runq (channels m0 .. m0 + R, the W
   // pixels [c0, c0 + W) of each channel row: contiguous NCHW memory when W = hw), element
   // f = 4 (gi % runq) = row r0 (channel m0 + r0), pixel p0.  A thread's groups are 256 apart: the
-  // walk advances (kk, r0, p0) by 1024 elements per step without divisions.  W % 4 == 0: a group
+  // walk advances (r0, p0) and the record / staging offsets by 1024 elements per step, without
+  // divisions or products.  W % 4 == 0: a group
   // lies in one channel row (one b128 read of the tile, one row of constants); else (7x7, one pass)
   // it may cross into the next row, whose elements take that row's constants.
   const uint32_t n4 = g.out_elems * 4u;
@@ -494,6 +495,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
   const uint32_t dO = (uint32_t)(dr * hw + dp), dOp = (uint32_t)(hw - W), dOr = (uint32_t)((Mrows - R) * hw);
   const int dB = dr * ts + dp, dBp = ts - W, dBr = W - R * ts;
   const int32_t* lut_b = lut - (int32_t)g.rq.qmin;  // lut_b[q], q in [qmin, qmin + 255]
+  const int tile_end = R * ts;  // staging words (a group's reads are clamped below it)
   int c0 = 0;  // first pixel of the current pass
   // nontemporal record stores (plain ones measured no faster, also on multi-pass epilogues:
   // profiles/r03k_img_epilogue_ablations.txt)
@@ -511,8 +513,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
     uint32_t on = (uint32_t)(((img0 + kk) * Mrows + m0 + r0) * hw + c0 + p0);
     // software pipeline by one group: the next group's tile values, row constants and residual
     // word are read from LDS before this group's arithmetic and stores (at one or two waves per
-    // SIMD nothing else hides the LDS latency); slots are read unconditionally (in bounds: the
-    // walk position of a group past the end still lies inside the staging tile)
+    // SIMD nothing else hides the LDS latency); every step reads the next group's slots, also past
+    // the last group, whose position (up to W + 4 words beyond the staging tile) is clamped into
+    // the tile (values unused)
     auto load = [&](int r, int base, int p, int gi, v4u& v, EpiRow& ra, EpiRow& rb, uint32_t& res)
         __attribute__((always_inline)) {
       if (TK_ABL(1 << 25)) {  // (ablation build: no LDS reads in the walk -- values from registers)
@@ -523,12 +526,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       }
       ra = rowc[min(r, R - 1)];
       if constexpr (ROWU) {
-        v = *reinterpret_cast<const v4u*>(tileI + base);
+        v = *reinterpret_cast<const v4u*>(tileI + min(base, tile_end - 4));
         rb = ra;
       } else {
         rb = rowc[min(r + 1, R - 1)];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (uint32_t)tileI[base + e + (p + e >= W ? ts - W : 0)];
+        for (int e = 0; e < 4; ++e) v[e] = (uint32_t)tileI[min(base + e + (p + e >= W ? ts - W : 0), tile_end - 1)];
       }
       if constexpr (ADD) res = TK_ABL(32768) ? 0x01010101u : resw[min(gi, total - 1)];
     };
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void conv_img_kernel(GemmArgs g, I
       basen += dB;
       if (p0 >= W) p0 -= W, ++r0, on += dOp, basen += dBp;
       while (r0 >= R) r0 -= R, on += dOr, basen += dBr;
-      load(r0, basen, p0, gi + kGemmThreads, vn, ran, rbn, resn);  // (past the end: in-bounds LDS reads, unused)
+      load(r0, basen, p0, gi + kGemmThreads, vn, ran, rbn, resn);
       uint32_t fold[4], zp[4];
       int32_t bias[4], m[4], sh[4];
 #pragma unroll

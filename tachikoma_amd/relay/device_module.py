@@ -961,7 +961,9 @@ class DeviceModule:
             # algo numbers are plan indices that move when the planner changes: a table from another
             # library is replayed by kernel description (version 2 tables), never by number
             algo = int(e["algo"])
-            if e.get("kernel"):
+            if algo == 0:
+                pass  # the library's own choice (blocks with no kernel list, e.g. depthwise): no description to match
+            elif e.get("kernel"):
                 if not (same_lib and self.algo_info(i, algo) == e["kernel"]):
                     match = [a for a in self.node_algos(i) if self.algo_info(i, a) == e["kernel"]]
                     if not match:
