@@ -11,10 +11,14 @@
 //     groups, each lane storing 16 bytes (int32 records) / 4 bytes (int8 records) with buffer stores:
 //     the whole-line pattern that writes at ~5.3 TB/s in the store probes.
 //   * The input rows of the tile's channels (+ the one-row halo, out-of-image rows and columns
-//     holding the input zero point) are staged in LDS with dword loads; a tap row of an output is
-//     three bytes there: two ds_read_b32 + one v_alignbyte_b32 give them as one dword, and one
+//     holding the input zero point) are staged in LDS: row loads of 16 / 8 / 4 bytes, or, for
+//     narrow whole planes (14x14, 7x7), 16-byte loads of the tile's contiguous input run placed
+//     byte by byte (dw_stage_flat).  A tap row of an output is three bytes there; one
 //     v_dot4_i32_i8 against the channel's packed weight row (w0, w1, w2, 0) accumulates the three
-//     products -- 3 dot instructions per output instead of 9 multiply-adds on single bytes.
+//     products -- 3 dot instructions per output instead of 9 multiply-adds on single bytes.  On
+//     planes with OW % 4 == 0 a group is 4 outputs of one row whose tap windows are fixed
+//     v_alignbyte_b32 shifts of 3 (stride 1) or 4 (stride 2) aligned dwords per tap row; other
+//     planes decode each element and read two dwords + one alignbyte per tap row.
 //   * Zero points are folded, not subtracted per tap: with out-of-image taps holding za,
 //       sum (x - za)(w - zw) = sum x w - zw sum x - za sum w + 9 za zw   (exactly, in int32),
 //     the last two terms a per-channel constant, sum x another dot against 0x00010101 (only when a
