@@ -15,9 +15,9 @@ Launch: python bench.py [--gpus N --steps K --warmup W]
   * --dist-backend gloo rehearses N ranks on one GPU (all ranks share cuda:0).
 
 After the timed region, the trace image is checked record for record against the CPU
-oracle: at N > 1 every rank checks ceil(64 / N) samples spread over its shard (64 samples,
-14,912 records in all, as at N = 1), and rank 0 then times the CPU baseline at every N
-(checking each sample it traces too); any mismatch makes the run exit non-zero.
+oracle: at N > 1 every rank checks ceil(64 / N) samples spread over its shard, and rank 0 then
+times the CPU baseline at every N, checking each sample it traces and then (untimed) the rest of
+its shard -- at N = 1 all 64 samples; any mismatch makes the run exit non-zero.
 """
 from __future__ import annotations
 
@@ -249,7 +249,8 @@ def spread_samples(count: int, n: int):
 def cpu_baseline(model_fn, offset: int, batch: int, budget_s: float, threads: int, parity: Parity):
     """Time the oracle's C restatement (OpenMP port of the reference's int16 conv / int64
     requantize semantics) doing the same per-op record-and-run, one sample at a time, on
-    `threads` host cores; every sample it traces is also checked against the GPU trace."""
+    `threads` host cores; every sample it traces is also checked against the GPU trace, and so are
+    the shard's other samples (untimed), so that the in-run parity covers the whole shard."""
     from oracle import graph_ref
     model = model_fn(batch=1)
     one = model.sample_inputs(offset, 1)
@@ -271,6 +272,12 @@ def cpu_baseline(model_fn, offset: int, batch: int, budget_s: float, threads: in
     timed = len(picks) or 1
     if not picks:
         dt = first
+    # the shard's other samples are checked too (untimed): in-run parity covers the whole shard
+    for i in sorted(set(range(1, batch)) - set(picks)):
+        rec = graph_ref.calibrate(model.mod, model.params, {"data": model.sample_inputs(offset + i, 1)}, backend="c",
+                                  threads=threads)
+        parity.check(i, offset + i, rec)
+        del rec
     return {"value": round(timed / dt, 3), "unit": "op-traces/s", "cores": threads, "kind": "port",
             "sample": f"{timed} samples of {model.name} int8 224x224 spread over the shard, traced one by one "
                       f"(batch-1 record-and-run, every op output kept), C/OpenMP oracle on {threads} threads, "
