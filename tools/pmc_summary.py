@@ -112,7 +112,7 @@ def summarise(d, launches=None, runs=None, model="resnet50", batch=64):
     disp = []
     for i in sorted(steps):
         m = steps[i]["_meta"]
-        name = m["kernel"].split("(")[0].replace("void ", "").replace("tk::", "").strip()
+        name = m["kernel"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("tk::", "").strip()
         f = fam[name]
         f["dispatches"] += 1
         for c, v in steps[i].items():
