@@ -863,7 +863,7 @@ def main(argv=None) -> int:
                          "kernel": "fused conv/dense layer blocks, the find step's pick per node: conv_img_kernel "
                                    "(whole-image tiles on 28x28/14x14/7x7 planes, 3x3 split-K as a partial and an "
                                    "epilogue pass), gemm_i8_kernel<*,*,block> (im2col tiles), conv_pf_kernel "
-                                   "(persistent im2col), dw3x3_kernel (depthwise LDS band, MobileNetV2), "
+                                   "(persistent im2col), dw_tile_kernel (depthwise 3x3 tiles on v_dot4_i32_i8, MobileNetV2), "
                                    "dense_tile_kernel (classifier); v_mfma_i32_32x32x32_i8",
                          "nodes_per_step": n_launch, "kernel_ms_per_step": round(blk_ms, 3),
                          "algorithmic_bytes_per_step": int(blk_bytes),
